@@ -1,0 +1,84 @@
+"""ctypes binding of libdmx.so (include/dmx.h).  The library is built in-tree by
+depthmapx_amd.build (hipcc, gfx950); importing this module never falls back to anything else:
+if the shared object is missing or a call fails, a DmxError is raised."""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libdmx.so")
+
+DMX_OK = 0
+STATUS_NAMES = {-1: "DMX_ERR_ARG", -2: "DMX_ERR_HIP", -3: "DMX_ERR_CAPACITY", -4: "DMX_ERR_STATE",
+                -5: "DMX_ERR_UNSUPPORTED", -6: "DMX_ERR_OUTSIDE"}
+
+# every symbol include/dmx.h declares, with (restype, argtypes)
+_vp, _i64, _i32, _dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double
+SIGNATURES = {
+    "dmx_abi_version": (_i32, []),
+    "dmx_last_error": (ctypes.c_char_p, []),
+    "dmx_ctx_create": (_i32, [_i32, _vp]),
+    "dmx_ctx_free": (_i32, [_vp]),
+    "dmx_ctx_last_timing": (_i32, [_vp, _vp, _vp]),
+    "dmx_ctx_last_stats": (_i32, [_vp, _vp, _i32]),
+    "dmx_pointmap_create": (_i32, [_vp, _dbl, _vp, _i64, _vp]),
+    "dmx_pointmap_free": (_i32, [_vp]),
+    "dmx_pointmap_fill": (_i32, [_vp, _dbl, _dbl, _vp]),
+    "dmx_pointmap_info": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "dmx_pointmap_state": (_i32, [_vp, _vp]),
+    "dmx_pointmap_cell_lines": (_i32, [_vp, _vp, _vp, _vp]),
+    "dmx_makegraph": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp]),
+    "dmx_graph_free": (_i32, [_vp]),
+    "dmx_graph_info": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "dmx_graph_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "dmx_graph_blob_size": (_i32, [_vp, _vp]),
+    "dmx_graph_blob_write_device": (_i32, [_vp, _vp, _i64]),
+    "dmx_graph_assemble_device": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp]),
+    "dmx_vga_global": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp, _vp]),
+    "dmx_vga_global_device": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp]),
+}
+
+
+class DmxError(RuntimeError):
+    def __init__(self, status, message):
+        super().__init__("%s (%d): %s" % (STATUS_NAMES.get(status, "?"), status, message))
+        self.status = status
+
+
+_lib = None
+
+
+def _share_hip_runtime_with_torch():
+    # torch bundles its own libamdhip64.so.7 / libhsa-runtime64; two HIP runtimes in one process
+    # cannot both own the GPU.  Loading torch first makes libdmx.so bind to the same runtime
+    # (same SONAME), so device pointers, streams and RCCL from torch interoperate with it.
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _share_hip_runtime_with_torch()
+        if not os.path.exists(LIB_PATH):
+            raise DmxError(-2, "native library %s is missing: run depthmapx_amd.build.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status):
+    if status != DMX_OK:
+        raise DmxError(status, lib().dmx_last_error().decode(errors="replace"))
+    return status
+
+
+def ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)

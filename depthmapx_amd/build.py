@@ -1,0 +1,47 @@
+"""In-tree build of libdmx.so for gfx950 (hipcc).  Sources: csrc/dmx_api.hip (unity build with the
+kernels) + csrc/host/*.cpp.  -ffp-contract=off keeps every FP64 expression in the reference's
+rounding order (no FMA contraction) on host and device."""
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+OUT = os.path.join(HERE, "_lib", "libdmx.so")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("DMX_OFFLOAD_ARCH", "gfx950")
+
+SOURCES = ["dmx_api.hip", "host/pointmap.cpp"]
+FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+         "-fno-fast-math", "-Wall", "-Wno-unused-variable", "-Wno-unused-function"]
+
+
+def _deps():
+    out = []
+    for root, _, files in os.walk(CSRC):
+        for f in files:
+            if f.endswith((".hip", ".cpp", ".hpp", ".h")):
+                out.append(os.path.join(root, f))
+    out.append(os.path.join(os.path.dirname(HERE), "include", "dmx.h"))
+    return out
+
+
+def up_to_date():
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(p) <= t for p in _deps())
+
+
+def build(force=False, verbose=True):
+    if not force and up_to_date():
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    cmd = [HIPCC] + FLAGS + ["-o", OUT] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force=True)

@@ -1,0 +1,710 @@
+// dmx_api.hip -- implementation of the C ABI in include/dmx.h (unity build with the kernels).
+//
+// Host orchestration only: uploads the point map (SoA in HBM), launches the HIP kernels on the
+// context stream, sizes/retries scratch, and copies results out in reference layout.  There is no
+// CPU implementation of the sweep or the BFS behind this ABI: if the GPU path cannot run, the call
+// fails with a status code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/dmx.h"
+#include "host/pointmap.hpp"
+#include "kernels/makegraph.hip"
+#include "kernels/vga.hip"
+
+using namespace dmx;
+
+namespace {
+thread_local std::string g_err;
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return fail(DMX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+template <typename T> struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { reset(); }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t count) {
+        if (count <= n && p) return hipSuccess;
+        reset();
+        hipError_t e = hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) n = count;
+        return e;
+    }
+};
+} // namespace
+
+struct dmx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    int num_cu = 0;
+    double last_mk_s = 0, last_vga_s = 0;
+    DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
+    DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
+    long long last_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
+struct dmx_pointmap {
+    std::unique_ptr<PointMapHost> host;
+    // device copies (per context device; refreshed when the host state changes)
+    int uploaded_for = -1;
+    uint64_t version = 1, uploaded_version = 0;
+    int64_t nnodes = 0;
+    std::vector<int32_t> node_cell;
+    DevBuf<uint32_t> d_cellw;
+    DevBuf<double> d_segs;
+    DevBuf<int32_t> d_node_cell;
+    DevBuf<int32_t> d_cell_node;
+    DevBuf<uint8_t> d_node_flags;
+    DevBuf<unsigned long long> d_seed_tiles;
+};
+
+struct dmx_graph {
+    dmx_ctx* ctx = nullptr;
+    dmx_pointmap* pm = nullptr;
+    int64_t nnodes = 0, node_begin = 0, node_end = 0;
+    int64_t nruns = 0;
+    DevBuf<Run> pool;
+    DevBuf<int64_t> node_run_start;
+    DevBuf<int32_t> node_nruns;
+    DevBuf<int32_t> bin_nruns;
+    DevBuf<uint16_t> bin_count;
+    DevBuf<float> bin_dist;
+    DevBuf<float> attrs;
+    DevBuf<uint8_t> gridconn;
+    // VGA early-exit universe
+    DevBuf<unsigned long long> uf_tiles;
+    int64_t uf_count = -1;
+};
+
+namespace {
+
+int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
+    PointMapHost& h = *pm->host;
+    if (!h.lines_blocked()) h.block_lines();
+    if (pm->uploaded_version == pm->version && pm->uploaded_for == ctx->device) return DMX_OK;
+    const int64_t C = h.cells();
+    std::vector<uint32_t> cellw((size_t)C);
+    const auto& st = h.state();
+    const auto& off = h.seg_off();
+    pm->node_cell.clear();
+    std::vector<int32_t> cell_node((size_t)C, -1);
+    std::vector<uint8_t> flags;
+    for (int64_t c = 0; c < C; c++) {
+        const int32_t n = off[c + 1] - off[c];
+        if (n > 127) return fail(DMX_ERR_UNSUPPORTED, "more than 127 occluder pieces in one grid cell");
+        if ((int64_t)off[c] >= (1 << 24)) return fail(DMX_ERR_UNSUPPORTED, "more than 16M occluder pieces");
+        const bool filled = st[c] & CELL_FILLED;
+        cellw[c] = pack_cell(filled, (uint32_t)n, (uint32_t)off[c]);
+        if (filled) {
+            cell_node[c] = (int32_t)pm->node_cell.size();
+            pm->node_cell.push_back((int32_t)c);
+            flags.push_back((st[c] & CELL_CONTEXTFILLED) ? 1 : 0);
+        }
+    }
+    pm->nnodes = (int64_t)pm->node_cell.size();
+    // seed bitmap for the BFS: 1 = not a filled cell (or padding), 8x8 tiles
+    const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
+    std::vector<unsigned long long> seed((size_t)tw * th, ~0ull);
+    for (int x = 0; x < h.cols(); x++)
+        for (int y = 0; y < h.rows(); y++)
+            if (st[h.index(x, y)] & CELL_FILLED)
+                seed[(size_t)(y >> 3) * tw + (x >> 3)] &= ~(1ull << ((y & 7) * 8 + (x & 7)));
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(pm->d_cellw.alloc(C));
+    HIPCHK(pm->d_segs.alloc(std::max<size_t>(h.segs().size(), 4)));
+    HIPCHK(pm->d_node_cell.alloc(std::max<int64_t>(pm->nnodes, 1)));
+    HIPCHK(pm->d_cell_node.alloc(C));
+    HIPCHK(pm->d_node_flags.alloc(std::max<int64_t>(pm->nnodes, 1)));
+    HIPCHK(pm->d_seed_tiles.alloc(seed.size()));
+    HIPCHK(hipMemcpyAsync(pm->d_cellw.p, cellw.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
+    if (!h.segs().empty())
+        HIPCHK(hipMemcpyAsync(pm->d_segs.p, h.segs().data(), h.segs().size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (pm->nnodes) {
+        HIPCHK(hipMemcpyAsync(pm->d_node_cell.p, pm->node_cell.data(), pm->nnodes * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(pm->d_node_flags.p, flags.data(), pm->nnodes, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIPCHK(hipMemcpyAsync(pm->d_cell_node.p, cell_node.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(pm->d_seed_tiles.p, seed.data(), seed.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    pm->uploaded_version = pm->version;
+    pm->uploaded_for = ctx->device;
+    return DMX_OK;
+}
+
+__global__ void node_nruns_kernel(const int32_t* bin_nruns, int64_t n, int32_t* out) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    int s = 0;
+    for (int b = 0; b < 32; b++) s += bin_nruns[k * 32 + b];
+    out[k] = s;
+}
+
+// copy each node's runs to a contiguous node-ordered destination
+__global__ void gather_runs_kernel(const Run* pool, const int64_t* start, const int32_t* nruns, const int64_t* dst_off,
+                                   int64_t n, Run* dst) {
+    int64_t k = blockIdx.x;
+    if (k >= n) return;
+    const int64_t s = start[k], d = dst_off[k];
+    for (int i = threadIdx.x; i < nruns[k]; i += blockDim.x) dst[d + i] = pool[s + i];
+}
+
+size_t makegraph_lds(int gcap, int bcap, int D) {
+    size_t b = 0;
+    b += 16 * (size_t)gcap * 2 + 16 * (size_t)bcap; // gaps, gaps2, blocks
+    b += 4 * 32 * 3 + 4 * 32;                        // binc, bfar, bnr, misc
+    b += 16 * (size_t)bcap;                          // bsorted
+    b += 4 * (size_t)gcap + 4 * (size_t)bcap + 4 * ((size_t)gcap + 4);
+    b += 4 * ((size_t)D + 4);
+    b += 2 * (3 * ((size_t)D + 1) + 2);
+    return (b + 15) & ~(size_t)15;
+}
+
+} // namespace
+
+extern "C" {
+
+int dmx_abi_version(void) { return DMX_ABI_VERSION; }
+const char* dmx_last_error(void) { return g_err.c_str(); }
+
+int dmx_ctx_create(int device, dmx_ctx** out) {
+    if (!out) return fail(DMX_ERR_ARG, "out is NULL");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(DMX_ERR_ARG, "device ordinal out of range");
+    HIPCHK(hipSetDevice(device));
+    auto* c = new dmx_ctx();
+    c->device = device;
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    c->num_cu = prop.multiProcessorCount;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev0));
+    HIPCHK(hipEventCreate(&c->ev1));
+    HIPCHK(c->counters.alloc(16));
+    HIPCHK(c->stats.alloc(8));
+    *out = c;
+    return DMX_OK;
+}
+
+int dmx_ctx_free(dmx_ctx* c) {
+    if (!c) return DMX_OK;
+    (void)hipSetDevice(c->device);
+    c->counters.reset();
+    c->stats.reset();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return DMX_OK;
+}
+
+int dmx_ctx_last_stats(dmx_ctx* c, int64_t* out, int n) {
+    if (!c || !out) return fail(DMX_ERR_ARG, "bad arguments");
+    for (int i = 0; i < n && i < 8; i++) out[i] = c->last_stats[i];
+    return DMX_OK;
+}
+
+int dmx_ctx_last_timing(dmx_ctx* c, double* mk, double* vga) {
+    if (!c) return fail(DMX_ERR_ARG, "ctx is NULL");
+    if (mk) *mk = c->last_mk_s;
+    if (vga) *vga = c->last_vga_s;
+    return DMX_OK;
+}
+
+int dmx_pointmap_create(const double* region, double spacing, const double* lines, int64_t nlines, dmx_pointmap** out) {
+    if (!region || !out || (nlines > 0 && !lines) || nlines < 0) return fail(DMX_ERR_ARG, "bad arguments");
+    if (!(spacing > 0)) return fail(DMX_ERR_ARG, "spacing must be > 0");
+    Rect r{region[0], region[1], region[2], region[3]};
+    auto* pm = new dmx_pointmap();
+    pm->host.reset(new PointMapHost(r, spacing, lines, nlines));
+    if (pm->host->cols() > 16000 || pm->host->rows() > 16000) {
+        delete pm;
+        return fail(DMX_ERR_UNSUPPORTED, "grid larger than 16000 cells per side");
+    }
+    *out = pm;
+    return DMX_OK;
+}
+
+int dmx_pointmap_free(dmx_pointmap* pm) {
+    delete pm;
+    return DMX_OK;
+}
+
+int dmx_pointmap_fill(dmx_pointmap* pm, double x, double y, int* made) {
+    if (!pm) return fail(DMX_ERR_ARG, "pointmap is NULL");
+    int r = pm->host->fill(x, y);
+    pm->version++;
+    if (made) *made = (r == 0);
+    if (r == 1) return fail(DMX_ERR_OUTSIDE, "Point outside of target region");
+    return DMX_OK;
+}
+
+int dmx_pointmap_info(const dmx_pointmap* pm, int32_t* cols, int32_t* rows, double* bx, double* by, int64_t* filled) {
+    if (!pm) return fail(DMX_ERR_ARG, "pointmap is NULL");
+    if (cols) *cols = pm->host->cols();
+    if (rows) *rows = pm->host->rows();
+    if (bx) *bx = pm->host->bottom_left().x;
+    if (by) *by = pm->host->bottom_left().y;
+    if (filled) *filled = pm->host->filled_count();
+    return DMX_OK;
+}
+
+int dmx_pointmap_state(const dmx_pointmap* pm, int32_t* out) {
+    if (!pm || !out) return fail(DMX_ERR_ARG, "bad arguments");
+    std::memcpy(out, pm->host->state().data(), pm->host->state().size() * 4);
+    return DMX_OK;
+}
+
+int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, int64_t* total) {
+    if (!pm) return fail(DMX_ERR_ARG, "pointmap is NULL");
+    pm->host->block_lines();
+    const auto& off = pm->host->seg_off();
+    const auto& segs = pm->host->segs();
+    if (total) *total = (int64_t)segs.size() / 4;
+    if (counts)
+        for (size_t c = 0; c + 1 < off.size(); c++) counts[c] = off[c + 1] - off[c];
+    if (pieces && !segs.empty()) std::memcpy(pieces, segs.data(), segs.size() * 8);
+    return DMX_OK;
+}
+
+int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int64_t node_begin, int64_t node_end,
+                  dmx_graph** out) {
+    if (!ctx || !pm || !out) return fail(DMX_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    PointMapHost& h = *pm->host;
+    if (!h.lines_blocked()) h.block_lines();
+    if (boundary) { h.keep_edges_only(); pm->version++; }
+    int rc = upload_pointmap(ctx, pm);
+    if (rc) return rc;
+    const int64_t N = pm->nnodes;
+    if (node_end < 0 || node_end > N) node_end = N;
+    if (node_begin < 0 || node_begin > node_end) return fail(DMX_ERR_ARG, "bad node range");
+    const int64_t n = node_end - node_begin;
+    std::unique_ptr<dmx_graph> g(new dmx_graph());
+    g->ctx = ctx;
+    g->pm = pm;
+    g->nnodes = N;
+    g->node_begin = node_begin;
+    g->node_end = node_end;
+    const int D = std::max(h.cols(), h.rows());
+    HIPCHK(g->node_run_start.alloc(std::max<int64_t>(n, 1)));
+    HIPCHK(g->node_nruns.alloc(std::max<int64_t>(n, 1)));
+    HIPCHK(g->bin_nruns.alloc(std::max<int64_t>(n, 1) * 32));
+    HIPCHK(g->bin_count.alloc(std::max<int64_t>(n, 1) * 32));
+    HIPCHK(g->bin_dist.alloc(std::max<int64_t>(n, 1) * 32));
+    HIPCHK(g->attrs.alloc(std::max<int64_t>(n, 1) * 3));
+    HIPCHK(g->gridconn.alloc(std::max<int64_t>(n, 1)));
+
+    // capacities (retried on overflow)
+    int gcap = 128, bcap = 128;
+    int64_t capB = 32 * (int64_t)D + 2048;
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    int64_t pool_cap = std::max<int64_t>(n * std::max<int64_t>(64, 6 * (int64_t)D), 1024);
+    ctx->last_mk_s = 0;
+    for (int attempt = 0; attempt < 8; attempt++) {
+        size_t lds = makegraph_lds(gcap, bcap, D);
+        if (lds > 160 * 1024) return fail(DMX_ERR_CAPACITY, "makegraph LDS requirement exceeds 160 KiB");
+        int occ = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, makegraph_kernel, 64, lds));
+        if (occ < 1) occ = 1;
+        const int64_t waves = std::min<int64_t>((int64_t)ctx->num_cu * occ, std::max<int64_t>(n, 1));
+        const int64_t capA = capB;
+        const size_t stage_bytes = (size_t)waves * (capA * 8 + capB * 8 + (3 * ((size_t)D + 1) + 4) * 4);
+        HIPCHK(hipMemGetInfo(&free_b, &total_b));
+        const size_t pool_bytes_max = free_b > stage_bytes + (1ull << 30) ? (free_b - stage_bytes - (1ull << 30)) : 0;
+        if ((size_t)pool_cap * sizeof(Run) > pool_bytes_max) pool_cap = (int64_t)(pool_bytes_max / sizeof(Run));
+        if (pool_cap <= 0) return fail(DMX_ERR_HIP, "not enough device memory for the run pool");
+        HIPCHK(g->pool.alloc(pool_cap));
+        DevBuf<unsigned long long> stA;
+        DevBuf<Run> stB;
+        DevBuf<uint32_t> pref;
+        HIPCHK(stA.alloc((size_t)waves * capA));
+        HIPCHK(stB.alloc((size_t)waves * capB));
+        HIPCHK(pref.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
+        HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+        MakeGraphParams P;
+        P.cols = h.cols(); P.rows = h.rows();
+        P.spacing = h.spacing(); P.blx = h.bottom_left().x; P.bly = h.bottom_left().y;
+        P.maxdist = maxdist;
+        P.cellw = pm->d_cellw.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
+        P.node_begin = node_begin; P.node_end = node_end;
+        P.work_counter = ctx->counters.p + 0;
+        P.error = ctx->counters.p + 1;
+        P.pool_cursor = (unsigned long long*)(ctx->counters.p + 2);
+        P.pool_capacity = pool_cap; P.pool = g->pool.p;
+        P.node_run_start = g->node_run_start.p; P.bin_nruns = g->bin_nruns.p; P.bin_count = g->bin_count.p;
+        P.bin_dist = g->bin_dist.p; P.attrs = g->attrs.p;
+        P.stageA = stA.p; P.stageB = stB.p; P.prefix = pref.p;
+        P.capA = (int)capA; P.capB = (int)capB; P.gcap = gcap; P.bcap = bcap; P.dmax = D;
+        P.stats = ctx->stats.p;
+        HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+        if (n > 0) {
+            hipLaunchKernelGGL(makegraph_kernel, dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(gridconn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, h.rows(),
+                               pm->d_node_cell.p + node_begin, n, g->node_run_start.p, g->bin_nruns.p, g->pool.p,
+                               g->gridconn.p);
+            HIPCHK(hipGetLastError());
+            hipLaunchKernelGGL(node_nruns_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                               g->bin_nruns.p, n, g->node_nruns.p);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        int hc[4] = {0, 0, 0, 0};
+        HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+        const int err = hc[1];
+        unsigned long long used = 0;
+        std::memcpy(&used, &hc[2], 8);
+        if (err == 0) {
+            unsigned long long st[2];
+            HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+            ctx->last_stats[0] = (long long)st[0];
+            ctx->last_stats[1] = (long long)st[1];
+            ctx->last_stats[2] = (long long)used;
+            ctx->last_mk_s = ms * 1e-3;
+            g->nruns = (int64_t)used;
+            *out = g.release();
+            return DMX_OK;
+        }
+        if (err & KERR_BIN_MISMATCH) return fail(DMX_ERR_STATE, "internal: whichbin outside octant");
+        if (err & KERR_GAP_CAPACITY) gcap *= 2;
+        if (err & KERR_BLOCK_CAPACITY) bcap *= 2;
+        if (err & KERR_STAGE_CAPACITY) capB *= 2;
+        if (err & KERR_POOL_CAPACITY) pool_cap = (int64_t)used + 1024;
+    }
+    return fail(DMX_ERR_CAPACITY, "makegraph capacities exceeded after retries");
+}
+
+int dmx_graph_free(dmx_graph* g) {
+    if (g && g->ctx) (void)hipSetDevice(g->ctx->device);
+    delete g;
+    return DMX_OK;
+}
+
+int dmx_graph_info(const dmx_graph* g, int64_t* nnodes, int64_t* nb, int64_t* ne, int64_t* nruns) {
+    if (!g) return fail(DMX_ERR_ARG, "graph is NULL");
+    if (nnodes) *nnodes = g->nnodes;
+    if (nb) *nb = g->node_begin;
+    if (ne) *ne = g->node_end;
+    if (nruns) *nruns = g->nruns;
+    return DMX_OK;
+}
+
+int dmx_graph_copy(dmx_graph* g, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn) {
+    if (!g) return fail(DMX_ERR_ARG, "graph is NULL");
+    HIPCHK(hipSetDevice(g->ctx->device));
+    const int64_t n = g->node_end - g->node_begin;
+    if (n == 0) return DMX_OK;
+    if (attrs) HIPCHK(hipMemcpy(attrs, g->attrs.p, n * 3 * 4, hipMemcpyDeviceToHost));
+    if (gridconn) HIPCHK(hipMemcpy(gridconn, g->gridconn.p, n, hipMemcpyDeviceToHost));
+    std::vector<int32_t> bn((size_t)n * 32);
+    HIPCHK(hipMemcpy(bn.data(), g->bin_nruns.p, n * 32 * 4, hipMemcpyDeviceToHost));
+    if (bins) {
+        std::vector<uint16_t> bc((size_t)n * 32);
+        std::vector<float> bd((size_t)n * 32);
+        HIPCHK(hipMemcpy(bc.data(), g->bin_count.p, n * 32 * 2, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(bd.data(), g->bin_dist.p, n * 32 * 4, hipMemcpyDeviceToHost));
+        for (int64_t k = 0; k < n; k++)
+            for (int b = 0; b < 32; b++) {
+                const int64_t i = k * 32 + b;
+                int dir; // Node::make (ngraph.cpp:43-54); empty bins keep NODIR
+                if (b == 4 || b == 20) dir = 4;
+                else if (b == 12 || b == 28) dir = 8;
+                else if ((b > 4 && b < 12) || (b > 20 && b < 28)) dir = 2;
+                else dir = 1;
+                bins[i * 4 + 0] = bn[i] > 0 ? dir : 0;
+                bins[i * 4 + 1] = bc[i];
+                std::memcpy(&bins[i * 4 + 2], &bd[i], 4);
+                bins[i * 4 + 3] = bn[i];
+            }
+    }
+    if (runs) {
+        // node-ordered copy (the pool is in completion order)
+        std::vector<int64_t> start((size_t)n), dst((size_t)n);
+        std::vector<int32_t> nr((size_t)n);
+        HIPCHK(hipMemcpy(start.data(), g->node_run_start.p, n * 8, hipMemcpyDeviceToHost));
+        int64_t acc = 0;
+        for (int64_t k = 0; k < n; k++) {
+            int s = 0;
+            for (int b = 0; b < 32; b++) s += bn[k * 32 + b];
+            nr[k] = s;
+            dst[k] = acc;
+            acc += s;
+        }
+        DevBuf<int64_t> d_dst;
+        DevBuf<Run> d_runs;
+        HIPCHK(d_dst.alloc(n));
+        HIPCHK(d_runs.alloc(std::max<int64_t>(acc, 1)));
+        HIPCHK(hipMemcpy(d_dst.p, dst.data(), n * 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(gather_runs_kernel, dim3((unsigned)n), dim3(256), 0, g->ctx->stream, g->pool.p,
+                           g->node_run_start.p, g->node_nruns.p, d_dst.p, n, d_runs.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(g->ctx->stream));
+        if (acc) HIPCHK(hipMemcpy(runs, d_runs.p, acc * sizeof(Run), hipMemcpyDeviceToHost));
+    }
+    return DMX_OK;
+}
+
+// ---------------------------------------------------------------- shard blobs
+// layout: int64 header[4] {node_begin, node_end, nruns, magic}, then (8-byte aligned sections)
+// bin_nruns i32[n*32], bin_count u16[n*32], bin_dist f32[n*32], attrs f32[n*3], gridconn u8[n],
+// runs (node order).
+static const int64_t kBlobMagic = 0x31424d58444d44LL;
+static inline int64_t al8(int64_t x) { return (x + 7) & ~7LL; }
+static void blob_layout(int64_t n, int64_t nruns, int64_t* off /*7*/) {
+    off[0] = 32;
+    off[1] = off[0] + al8(n * 32 * 4);
+    off[2] = off[1] + al8(n * 32 * 2);
+    off[3] = off[2] + al8(n * 32 * 4);
+    off[4] = off[3] + al8(n * 3 * 4);
+    off[5] = off[4] + al8(n);
+    off[6] = off[5] + nruns * 8;
+}
+
+int dmx_graph_blob_size(dmx_graph* g, int64_t* bytes) {
+    if (!g || !bytes) return fail(DMX_ERR_ARG, "bad arguments");
+    int64_t off[7];
+    blob_layout(g->node_end - g->node_begin, g->nruns, off);
+    *bytes = off[6];
+    return DMX_OK;
+}
+
+int dmx_graph_blob_write_device(dmx_graph* g, void* dst, int64_t bytes) {
+    if (!g || !dst) return fail(DMX_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(g->ctx->device));
+    const int64_t n = g->node_end - g->node_begin;
+    int64_t off[7];
+    blob_layout(n, g->nruns, off);
+    if (bytes < off[6]) return fail(DMX_ERR_ARG, "blob buffer too small");
+    char* d = (char*)dst;
+    hipStream_t s = g->ctx->stream;
+    int64_t hdr[4] = {g->node_begin, g->node_end, g->nruns, kBlobMagic};
+    HIPCHK(hipMemcpyAsync(d, hdr, 32, hipMemcpyHostToDevice, s));
+    if (n) {
+        HIPCHK(hipMemcpyAsync(d + off[0], g->bin_nruns.p, n * 32 * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(d + off[1], g->bin_count.p, n * 32 * 2, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(d + off[2], g->bin_dist.p, n * 32 * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(d + off[3], g->attrs.p, n * 3 * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(hipMemcpyAsync(d + off[4], g->gridconn.p, n, hipMemcpyDeviceToDevice, s));
+        std::vector<int32_t> nr((size_t)n);
+        HIPCHK(hipMemcpyAsync(nr.data(), g->node_nruns.p, n * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<int64_t> dsto((size_t)n);
+        int64_t acc = 0;
+        for (int64_t k = 0; k < n; k++) { dsto[k] = acc; acc += nr[k]; }
+        DevBuf<int64_t> d_dst;
+        HIPCHK(d_dst.alloc(n));
+        HIPCHK(hipMemcpyAsync(d_dst.p, dsto.data(), n * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(gather_runs_kernel, dim3((unsigned)n), dim3(256), 0, s, g->pool.p, g->node_run_start.p,
+                           g->node_nruns.p, d_dst.p, n, (Run*)(d + off[5]));
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    return DMX_OK;
+}
+
+int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const* blobs, const int64_t* sizes,
+                              int nshards, dmx_graph** out) {
+    if (!ctx || !pm || !blobs || !out || nshards <= 0) return fail(DMX_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    int rc = upload_pointmap(ctx, pm);
+    if (rc) return rc;
+    const int64_t N = pm->nnodes;
+    std::vector<std::array<int64_t, 4>> hdr((size_t)nshards);
+    int64_t total_runs = 0;
+    for (int i = 0; i < nshards; i++) {
+        HIPCHK(hipMemcpy(hdr[i].data(), blobs[i], 32, hipMemcpyDeviceToHost));
+        if (hdr[i][3] != kBlobMagic) return fail(DMX_ERR_ARG, "not a dmx graph blob");
+        total_runs += hdr[i][2];
+    }
+    std::unique_ptr<dmx_graph> g(new dmx_graph());
+    g->ctx = ctx; g->pm = pm; g->nnodes = N; g->node_begin = 0; g->node_end = N; g->nruns = total_runs;
+    HIPCHK(g->node_run_start.alloc(std::max<int64_t>(N, 1)));
+    HIPCHK(g->node_nruns.alloc(std::max<int64_t>(N, 1)));
+    HIPCHK(g->bin_nruns.alloc(std::max<int64_t>(N, 1) * 32));
+    HIPCHK(g->bin_count.alloc(std::max<int64_t>(N, 1) * 32));
+    HIPCHK(g->bin_dist.alloc(std::max<int64_t>(N, 1) * 32));
+    HIPCHK(g->attrs.alloc(std::max<int64_t>(N, 1) * 3));
+    HIPCHK(g->gridconn.alloc(std::max<int64_t>(N, 1)));
+    HIPCHK(g->pool.alloc(std::max<int64_t>(total_runs, 1)));
+    hipStream_t s = ctx->stream;
+    std::vector<char> covered((size_t)N, 0);
+    // shards are placed in node order; runs of a shard are contiguous in node order
+    std::vector<int> order(nshards);
+    for (int i = 0; i < nshards; i++) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return hdr[a][0] < hdr[b][0]; });
+    int64_t run_base = 0;
+    for (int oi = 0; oi < nshards; oi++) {
+        const int i = order[oi];
+        const int64_t b = hdr[i][0], e = hdr[i][1], n = e - b, nr = hdr[i][2];
+        if (b < 0 || e > N || b > e) return fail(DMX_ERR_ARG, "blob node range does not fit the point map");
+        int64_t off[7];
+        blob_layout(n, nr, off);
+        if (sizes && sizes[i] < off[6]) return fail(DMX_ERR_ARG, "blob shorter than its header says");
+        for (int64_t k = b; k < e; k++) {
+            if (covered[k]) return fail(DMX_ERR_ARG, "overlapping shards");
+            covered[k] = 1;
+        }
+        const char* d = (const char*)blobs[i];
+        if (n) {
+            HIPCHK(hipMemcpyAsync(g->bin_nruns.p + b * 32, d + off[0], n * 32 * 4, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(g->bin_count.p + b * 32, d + off[1], n * 32 * 2, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(g->bin_dist.p + b * 32, d + off[2], n * 32 * 4, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(g->attrs.p + b * 3, d + off[3], n * 3 * 4, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(g->gridconn.p + b, d + off[4], n, hipMemcpyDeviceToDevice, s));
+        }
+        if (nr) HIPCHK(hipMemcpyAsync(g->pool.p + run_base, d + off[5], nr * 8, hipMemcpyDeviceToDevice, s));
+        run_base += nr;
+    }
+    for (int64_t k = 0; k < N; k++)
+        if (!covered[k]) return fail(DMX_ERR_ARG, "shards do not cover every node");
+    if (N) {
+        hipLaunchKernelGGL(node_nruns_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, g->bin_nruns.p, N,
+                           g->node_nruns.p);
+        HIPCHK(hipGetLastError());
+        std::vector<int32_t> nr((size_t)N);
+        HIPCHK(hipMemcpyAsync(nr.data(), g->node_nruns.p, N * 4, hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        std::vector<int64_t> st((size_t)N);
+        int64_t acc = 0;
+        for (int64_t k = 0; k < N; k++) { st[k] = acc; acc += nr[k]; }
+        if (acc != total_runs) return fail(DMX_ERR_ARG, "blob run counts inconsistent");
+        HIPCHK(hipMemcpyAsync(g->node_run_start.p, st.data(), N * 8, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    *out = g.release();
+    return DMX_OK;
+}
+
+// ---------------------------------------------------------------- VGA global
+static int prepare_uf(dmx_graph* g) {
+    if (g->uf_count >= 0) return DMX_OK;
+    dmx_ctx* ctx = g->ctx;
+    PointMapHost& h = *g->pm->host;
+    const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
+    HIPCHK(g->uf_tiles.alloc((size_t)tw * th));
+    HIPCHK(hipMemsetAsync(g->uf_tiles.p, 0, (size_t)tw * th * 8, ctx->stream));
+    if (g->nnodes)
+        hipLaunchKernelGGL(mark_runs_kernel, dim3((unsigned)g->nnodes), dim3(64), 0, ctx->stream, tw,
+                           g->node_run_start.p, g->node_nruns.p, g->pool.p, g->nnodes, g->uf_tiles.p);
+    HIPCHK(hipGetLastError());
+    std::vector<unsigned long long> uf((size_t)tw * th), seed((size_t)tw * th);
+    HIPCHK(hipMemcpyAsync(uf.data(), g->uf_tiles.p, uf.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(seed.data(), g->pm->d_seed_tiles.p, seed.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    int64_t cnt = 0;
+    for (size_t i = 0; i < uf.size(); i++) {
+        uf[i] &= ~seed[i];
+        cnt += __builtin_popcountll(uf[i]);
+    }
+    HIPCHK(hipMemcpy(g->uf_tiles.p, uf.data(), uf.size() * 8, hipMemcpyHostToDevice));
+    g->uf_count = cnt;
+    return DMX_OK;
+}
+
+static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
+                    bool out_on_device, int64_t* levels) {
+    if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");
+    if (g->node_begin != 0 || g->node_end != g->nnodes)
+        return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int64_t N = g->nnodes;
+    if (se < 0 || se > N) se = N;
+    if (sb < 0 || sb > se) return fail(DMX_ERR_ARG, "bad source range");
+    int rc = prepare_uf(g);
+    if (rc) return rc;
+    PointMapHost& h = *g->pm->host;
+    const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
+    const int maxlev = 4096;
+    const size_t lds = (size_t)tw * th * 8 + (maxlev + 4) * 4 + 64;
+    if (lds > 160 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the LDS visited bitmap (v1 limit)");
+    int occ = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_global_kernel, VGA_THREADS, lds));
+    if (occ < 1) occ = 1;
+    const int64_t nsrc = se - sb;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cu * occ, nsrc));
+    DevBuf<int32_t> frontier;
+    HIPCHK(frontier.alloc((size_t)blocks * 2 * std::max<int64_t>(N, 1)));
+    DevBuf<float> d_out;
+    float* outp = out;
+    if (!out_on_device) {
+        HIPCHK(d_out.alloc(std::max<int64_t>(N, 1) * 7));
+        outp = d_out.p;
+    }
+    DevBuf<int64_t> d_lv;
+    if (levels) HIPCHK(d_lv.alloc(std::max<int64_t>(N, 1) * 3));
+    HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    VgaParams P;
+    P.cols = h.cols(); P.rows = h.rows(); P.tw = tw; P.th = th;
+    P.seed_tiles = g->pm->d_seed_tiles.p; P.uf_tiles = g->uf_tiles.p; P.uf_count = g->uf_count;
+    P.node_cell = g->pm->d_node_cell.p; P.cell_node = g->pm->d_cell_node.p; P.node_flags = g->pm->d_node_flags.p;
+    P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
+    P.src_begin = sb; P.src_end = se; P.radius = (int)radius; P.gates_only = gates_only;
+    P.work_counter = ctx->counters.p + 0; P.error = ctx->counters.p + 1;
+    P.frontier = frontier.p; P.nnodes = N; P.maxlev = maxlev;
+    P.out = outp; P.levels_out = levels ? d_lv.p : nullptr;
+    P.stats = ctx->stats.p;
+    HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+    if (nsrc > 0) {
+        hipLaunchKernelGGL(vga_global_kernel, dim3((unsigned)blocks), dim3(VGA_THREADS), lds, ctx->stream, P);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_vga_s = ms * 1e-3;
+    int hc[2];
+    HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+    if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level/frontier capacity");
+    unsigned long long st[3];
+    HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+    ctx->last_stats[4] = (long long)st[0];
+    ctx->last_stats[5] = (long long)st[1];
+    ctx->last_stats[6] = (long long)st[2];
+    ctx->last_stats[7] = nsrc;
+    if (!out_on_device && nsrc > 0)
+        HIPCHK(hipMemcpy(out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
+    if (levels && nsrc > 0)
+        HIPCHK(hipMemcpy(levels + sb * 3, d_lv.p + sb * 3, nsrc * 3 * 8, hipMemcpyDeviceToHost));
+    return DMX_OK;
+}
+
+int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
+                   int64_t* levels) {
+    return vga_impl(ctx, g, radius, gates_only, sb, se, out, false, levels);
+}
+
+int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se,
+                          float* out_device) {
+    return vga_impl(ctx, g, radius, gates_only, sb, se, out_device, true, nullptr);
+}
+
+} // extern "C"

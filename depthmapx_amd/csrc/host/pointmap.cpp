@@ -1,0 +1,181 @@
+// pointmap.cpp -- see pointmap.hpp.
+#include "pointmap.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+
+namespace dmx {
+
+PointMapHost::PointMapHost(const Rect& region, double spacing, const double* lines, int64_t nlines)
+    : parent_(region), spacing_(spacing), draw_(lines, lines + 4 * nlines) {
+    // PointMap::setGrid(spacing, Point2f(0,0)) -- pointdata.cpp:122-171
+    double xoffset = fmod(parent_.blx + 0.0, spacing_);
+    double yoffset = fmod(parent_.bly + 0.0, spacing_);
+    if (xoffset < spacing_ / 2.0) xoffset += spacing_;
+    if (xoffset > spacing_ / 2.0) xoffset -= spacing_;
+    if (yoffset < spacing_ / 2.0) yoffset += spacing_;
+    if (yoffset > spacing_ / 2.0) yoffset -= spacing_;
+    cols_ = (int)floor((xoffset + parent_.width()) / spacing_ + 0.5) + 1;
+    rows_ = (int)floor((yoffset + parent_.height()) / spacing_ + 0.5) + 1;
+    bl_ = Vec2{parent_.blx + -xoffset, parent_.bly + -yoffset};
+    region_ = Rect{bl_.x - spacing_ / 2.0, bl_.y - spacing_ / 2.0,
+                   bl_.x + double(cols_ - 1) * spacing_ + spacing_ / 2.0,
+                   bl_.y + double(rows_ - 1) * spacing_ + spacing_ / 2.0};
+    state_.assign((size_t)cells(), CELL_EMPTY);
+    seg_off_.assign((size_t)cells() + 1, 0);
+}
+
+Rect PointMapHost::cell_rect(int x, int y, double border) const {
+    return Rect{bl_.x + spacing_ * (double(x) - 0.5 - border), bl_.y + spacing_ * (double(y) - 0.5 - border),
+                bl_.x + spacing_ * (double(x) + 0.5 + border), bl_.y + spacing_ * (double(y) + 0.5 + border)};
+}
+
+// PixelBase::pixelateLineTouching(l, 1e-10) -- spacepix.cpp:144-214.  Appends (x,y) pairs.
+void PointMapHost::rasterise(const Seg& in, std::vector<int32_t>& out) const {
+    const double tol = 1e-10;
+    Seg l = in;
+    // normalScale to the grid region (top_right first, then bottom_left), then scale to cells
+    double rw = region_.width(), rh = region_.height();
+    l.r.trx = rw ? (l.r.trx - region_.blx) / rw : 0.0;
+    l.r.tr_y = rh ? (l.r.tr_y - region_.bly) / rh : 0.0;
+    l.r.blx = rw ? (l.r.blx - region_.blx) / rw : 0.0;
+    l.r.bly = rh ? (l.r.bly - region_.bly) / rh : 0.0;
+    l.r.trx *= double(cols_); l.r.tr_y *= double(rows_);
+    l.r.blx *= double(cols_); l.r.bly *= double(rows_);
+    auto emit = [&](int x, int y) {
+        short sx = (short)x, sy = (short)y; // PixelRef(short, short), PixelRef::encloses
+        if (sx >= 0 && sx < (short)cols_ && sy >= 0 && sy < (short)rows_) {
+            out.push_back(sx);
+            out.push_back(sy);
+        }
+    };
+    const bool along_x = l.r.width() > l.r.height();
+    const double grad = along_x ? l.sign() * l.r.height() / l.r.width() : l.sign() * l.r.width() / l.r.height();
+    const double constant = along_x ? l.ay() - grad * l.ax() : l.ax() - grad * l.ay();
+    const double lo = along_x ? l.ax() : l.r.bly, hi = along_x ? l.bx() : l.r.tr_y;
+    int first = (int)floor(lo - tol), last = (int)floor(hi + tol);
+    for (int i = first; i <= last; i++) {
+        int j1 = (int)floor((first == i ? lo : double(i)) * grad + constant - l.sign() * tol);
+        int j2 = (int)floor((last == i ? hi : double(i + 1)) * grad + constant + l.sign() * tol);
+        int js[3] = {j1, j2, (j1 + j2) / 2};
+        int nj = (j1 != j2) ? (std::abs(j2 - j1) == 2 ? 3 : 2) : 1;
+        for (int k = 0; k < nj; k++) {
+            if (along_x) emit(i, js[k]);
+            else emit(js[k], i);
+        }
+    }
+}
+
+// PointMap::blockLines / blockLine (pointdata.cpp:296-357): every drawing line is appended to each
+// touched cell (cells become BLOCKED), then each cell crops its copies to regionate(cell, 1e-10).
+void PointMapHost::block_lines() {
+    if (blocked_) return;
+    const int64_t C = cells();
+    const int64_t L = (int64_t)draw_.size() / 4;
+    std::vector<Seg> dl((size_t)L);
+    std::vector<std::vector<int32_t>> touched((size_t)L);
+    std::vector<int64_t> count((size_t)C + 1, 0);
+    for (int64_t k = 0; k < L; k++) {
+        dl[k] = make_seg(Vec2{draw_[4 * k], draw_[4 * k + 1]}, Vec2{draw_[4 * k + 2], draw_[4 * k + 3]});
+        rasterise(dl[k], touched[k]);
+        for (size_t i = 0; i < touched[k].size(); i += 2) count[index(touched[k][i], touched[k][i + 1]) + 1]++;
+    }
+    for (int64_t c = 0; c < C; c++) count[c + 1] += count[c];
+    std::vector<int64_t> cursor(count.begin(), count.end() - 1);
+    std::vector<int32_t> raw((size_t)count[C]);
+    for (int64_t k = 0; k < L; k++)
+        for (size_t i = 0; i < touched[k].size(); i += 2) {
+            int64_t c = index(touched[k][i], touched[k][i + 1]);
+            raw[cursor[c]++] = (int32_t)k;
+            state_[c] |= CELL_BLOCKED;
+        }
+    segs_.clear();
+    for (int x = 0; x < cols_; x++)
+        for (int y = 0; y < rows_; y++) {
+            int64_t c = index(x, y);
+            seg_off_[c] = (int32_t)(segs_.size() / 4);
+            Rect cell = cell_rect(x, y, 1e-10);
+            for (int64_t i = count[c]; i < count[c + 1]; i++) {
+                Seg s = dl[raw[i]];
+                if (clip_seg(s, cell)) {
+                    Vec2 a = s.start(), b = s.end();
+                    segs_.push_back(a.x); segs_.push_back(a.y);
+                    segs_.push_back(b.x); segs_.push_back(b.y);
+                }
+            }
+        }
+    seg_off_[C] = (int32_t)(segs_.size() / 4);
+    blocked_ = true;
+}
+
+// PointMap::expand (pointdata.cpp:483-514): 1 off-grid, 2 already filled, 4 blocked, 8 filled now.
+int PointMapHost::expand(int x1, int y1, int x2, int y2, std::vector<int32_t>& next) {
+    if ((short)x2 < 0 || (short)x2 >= (short)cols_ || (short)y2 < 0 || (short)y2 >= (short)rows_) return 1;
+    const int64_t c1 = index(x1, y1), c2 = index(x2, y2);
+    if (state_[c2] & CELL_FILLED) return 2;
+    Seg l = make_seg(cell_centre(x1, y1), cell_centre(x2, y2));
+    const double tol = spacing_ * 1e-10;
+    for (int64_t c : {c1, c2})
+        for (int32_t k = seg_off_[c]; k < seg_off_[c + 1]; k++) {
+            Seg s = seg_at(k);
+            if (rects_touch(l.r, s.r, tol) && segs_cross(l, s, tol)) return 4;
+        }
+    state_[c2] = CELL_FILLED | (state_[c2] & CELL_BLOCKED); // Point::set keeps BLOCKED
+    filled_++;
+    next.push_back(x2);
+    next.push_back(y2);
+    return 8;
+}
+
+int PointMapHost::fill(double px, double py) {
+    // fillGraph: graph.getRegion().contains(point) -- strict (p2dpoly.h:338-340)
+    if (!(px > parent_.blx && px < parent_.trx && py > parent_.bly && py < parent_.tr_y)) return 1;
+    // PointMap::pixelate(p, false) (pointdata.cpp:283-305) into PixelRef(short, short)
+    int sx = (short)(int)floor((px - bl_.x + (spacing_ / 2.0)) / (spacing_ / 1.0));
+    int sy = (short)(int)floor((py - bl_.y + (spacing_ / 2.0)) / (spacing_ / 1.0));
+    if (!includes(sx, sy) || (state_[index(sx, sy)] & CELL_FILLED)) return 2;
+    if (blocked_) { // seed must see its own cell centre (only once lines are blocked: pointdata.cpp:422-428)
+        Seg ls = make_seg(Vec2{px, py}, cell_centre(sx, sy));
+        int64_t c = index(sx, sy);
+        for (int32_t k = seg_off_[c]; k < seg_off_[c + 1]; k++)
+            if (segs_cross_strict(seg_at(k), ls, 0.0)) return 2;
+    }
+    block_lines();
+    int64_t c0 = index(sx, sy);
+    state_[c0] = CELL_FILLED | (state_[c0] & CELL_BLOCKED);
+    filled_++;
+    // pflipper flood fill: pop from the back of the current layer, push into the next layer
+    std::vector<int32_t> layer[2];
+    int cur = 0;
+    layer[0] = {sx, sy};
+    while (!layer[cur].empty()) {
+        int x = layer[cur][layer[cur].size() - 2], y = layer[cur].back();
+        std::vector<int32_t>& nxt = layer[cur ^ 1];
+        int res = 0;
+        res |= expand(x, y, x, y + 1, nxt);
+        res |= expand(x, y, x, y - 1, nxt);
+        res |= expand(x, y, x - 1, y, nxt);
+        res |= expand(x, y, x + 1, y, nxt);
+        res |= expand(x, y, x - 1, y + 1, nxt);
+        res |= expand(x, y, x + 1, y + 1, nxt);
+        res |= expand(x, y, x - 1, y - 1, nxt);
+        res |= expand(x, y, x + 1, y - 1, nxt);
+        int64_t c = index(x, y);
+        if ((res & 4) || (state_[c] & CELL_BLOCKED)) state_[c] |= CELL_EDGE;
+        layer[cur].pop_back();
+        layer[cur].pop_back();
+        if (layer[cur].empty()) cur ^= 1;
+    }
+    return 0;
+}
+
+void PointMapHost::keep_edges_only() {
+    for (auto& s : state_)
+        if ((s & CELL_FILLED) && !(s & CELL_EDGE)) {
+            s &= ~CELL_FILLED;
+            filled_--;
+        }
+}
+
+} // namespace dmx

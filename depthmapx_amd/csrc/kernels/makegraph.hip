@@ -1,0 +1,690 @@
+// makegraph.hip -- K1/K2: the spark-sieve inter-visibility sweep + run-length binning on gfx950.
+//
+// Replaces PointMap::sparkGraph2 / sparkPixel2 / sieve2 (salalib/pointdata.cpp:1246-1341,
+// :1380-1565), sparkSieve2 (salalib/sparksieve2.cpp:33-173), whichbin (pointdata.h:432-520),
+// Node::make / Bin::make (ngraph.cpp:27-58, :234-304) and addGridConnections (pointdata.cpp:1735).
+//
+// Decomposition (MI355X-first, not the reference's per-pixel std::set loop):
+//   * one wavefront owns one source cell at a time (persistent grid, dynamic source counter);
+//     the 8 octants run in reference order q = 0..7 so the FP64 moment sums keep their order;
+//   * inside an octant the depth loop is sequential (each depth's gaps depend on the previous),
+//     but the candidate cells of one depth are spread over the 64 lanes: per-gap index ranges and
+//     the reference's monotone `firstind` rule become a prefix-max + prefix-sum over the gap list;
+//   * the gap list, the per-depth block list and per-row run state live in LDS;
+//   * visible cells never go through a sort: each octant row (fixed `ind`) is walked in depth
+//     order, so runs are closed incrementally per row; a per-(bin,row) count array gives every run
+//     its final slot in reference (PixelRefH/V) order without sorting (counting placement);
+//   * runs are staged per wave in scratch, then copied once into a global pool reserved with one
+//     atomic per source, bins in reference order 0..31.
+//   All geometry is IEEE double in the reference's operation order (-ffp-contract=off).
+#include "common.hpp"
+
+namespace dmx {
+
+struct MakeGraphParams {
+    int cols, rows;
+    double spacing, blx, bly;
+    double maxdist;
+    const uint32_t* cellw;     // [C] packed cell word (common.hpp)
+    const double* segs;        // [S][4] cropped segment start/end
+    const int32_t* node_cell;  // [N] node -> x-major cell index
+    int64_t node_begin, node_end;
+    int* work_counter;         // dynamic source counter (zeroed by the host each launch)
+    unsigned long long* pool_cursor;
+    int64_t pool_capacity;     // in runs
+    Run* pool;
+    int64_t* node_run_start;   // [N] (indexed by node - node_begin)
+    int32_t* bin_nruns;        // [N][32]
+    uint16_t* bin_count;       // [N][32]
+    float* bin_dist;           // [N][32]
+    float* attrs;              // [N][3]
+    unsigned long long* stageA;  // per wave: capA packed emission records
+    Run* stageB;               // per wave: capB runs (canonical octant segments)
+    uint32_t* prefix;          // per wave: 3*(D+1)+2 counts/prefix
+    int capA, capB;
+    int gcap, bcap;            // LDS gap / block capacities
+    int dmax;                  // max(cols, rows)
+    int* error;
+    unsigned long long* stats; // [0] sieve cells examined, [1] visible (source, target) pairs
+};
+
+// ------------------------------------------------------------------ octant tables
+// q octants (sparksieve2.cpp:134-141):   \ 6 | 7 /   0 \ | / 1   2 / | \ 3   / 4 | 5 \ .
+__constant__ int c_sector_base[8] = {13, 1, 17, 29, 21, 25, 9, 5};
+__constant__ int c_axis_bin[8] = {16, 0, -1, -1, -1, 24, 8, -1};
+__constant__ int c_diag_bin[8] = {12, 4, 20, 28, -1, -1, -1, -1};
+// canonical (PixelRefH: y then x / PixelRefV: x then y) order expressed in (ind, depth)
+__constant__ int c_row_asc[8] = {1, 1, 0, 0, 0, 1, 0, 1};
+__constant__ int c_d_asc[8] = {0, 1, 0, 1, 0, 0, 1, 1};
+// 1 if the octant's axis / diagonal bin sorts before its sectors (lower bin number)
+__constant__ int c_axis_low[8] = {0, 1, 0, 0, 0, 1, 1, 0};
+__constant__ int c_diag_low[8] = {1, 0, 0, 1, 0, 0, 0, 0};
+// the order in which octant segments are laid out so bins come out 0..31 (Node::make order)
+__constant__ int c_seg_order[8] = {1, 7, 6, 0, 2, 4, 5, 3};
+
+__device__ __forceinline__ void octant_cell(int q, int cx, int cy, int depth, int ind, int& hx, int& hy) {
+    int x = (q >= 4 ? ind : depth);
+    int y = (q >= 4 ? depth : ind);
+    hx = (short)(cx + ((q & 1) ? x : -x));                // pointdata.cpp:1536-1540
+    hy = (short)(cy + ((q <= 1 || q >= 6) ? y : -y));
+}
+
+// sparkSieve2::tanify (sparksieve2.cpp:143-173)
+__device__ __forceinline__ double tanify(double cxp, double cyp, double px, double py, int q) {
+    switch (q) {
+    case 0: return (py - cyp) / (cxp - px);
+    case 1: return (py - cyp) / (px - cxp);
+    case 2: return (cyp - py) / (cxp - px);
+    case 3: return (cyp - py) / (px - cxp);
+    case 4: return (cxp - px) / (cyp - py);
+    case 5: return (px - cxp) / (cyp - py);
+    case 6: return (cxp - px) / (py - cyp);
+    default: return (px - cxp) / (py - cyp);
+    }
+}
+
+// whichbin (pointdata.h:432-520)
+__device__ __forceinline__ int whichbin(double gx, double gy) {
+    int bin;
+    double ratio;
+    if (!(fabs(gy) > fabs(gx))) {
+        ratio = fabs(gy) / fabs(gx);
+        if (gx > 0.0) bin = (gy >= 0.0) ? 0 : -32;
+        else bin = (gy >= 0.0) ? -16 : 16;
+    } else {
+        ratio = fabs(gx) / fabs(gy);
+        if (gy > 0.0) bin = (gx >= 0.0) ? -8 : 8;
+        else bin = (gx >= 0.0) ? 24 : -24;
+    }
+    if (ratio < 1e-12) {
+    } else if (ratio < 0.2679491924311227) bin += 1;
+    else if (ratio < 0.5773502691896257) bin += 2;
+    else if (ratio < 1.0 - 1e-12) bin += 3;
+    else bin += 4;
+    if (bin < 0) bin = -bin;
+    return bin % 32;
+}
+
+// block zone ordering (sparksieve2.h:72-75)
+__device__ __forceinline__ bool zone_less(double as, double ae, double bs, double be) {
+    return (as == bs) ? (ae > be) : (as < bs);
+}
+
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int prefix_popc(unsigned long long m) {
+    return __popcll(m & ((1ull << lane_id()) - 1ull));
+}
+
+// wave-wide inclusive scans over 64 lanes (int)
+__device__ __forceinline__ int wave_incl_sum(int v) {
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o);
+        if (lane_id() >= o) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v) {
+    for (int o = 1; o < 64; o <<= 1) {
+        int t = __shfl_up(v, o);
+        if (lane_id() >= o) v = max(v, t);
+    }
+    return v;
+}
+__device__ __forceinline__ double wave_max_d(double v) {
+    for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+
+// emission record: slot(2) | ind(14) | dstart(14) | dend(14) | k(14)
+__device__ __forceinline__ unsigned long long pack_emit(int slot, int ind, int ds, int de, int k) {
+    return (unsigned long long)slot | ((unsigned long long)ind << 2) | ((unsigned long long)ds << 16) |
+           ((unsigned long long)de << 30) | ((unsigned long long)k << 44);
+}
+
+// Run for (ind, depth range) in octant q; H octants (q<4) run along x, V octants along y.
+__device__ __forceinline__ Run make_run(int q, int cx, int cy, int ind, int ds, int de) {
+    int ax, ay, bx, by;
+    octant_cell(q, cx, cy, ds, ind, ax, ay);
+    octant_cell(q, cx, cy, de, ind, bx, by);
+    Run r;
+    if (q < 4) { // horizontal: start is the smaller x
+        if (ax <= bx) { r.x0 = ax; r.y0 = ay; r.x1 = bx; r.y1 = by; }
+        else { r.x0 = bx; r.y0 = by; r.x1 = ax; r.y1 = ay; }
+    } else {     // vertical: start is the smaller y
+        if (ay <= by) { r.x0 = ax; r.y0 = ay; r.x1 = bx; r.y1 = by; }
+        else { r.x0 = bx; r.y0 = by; r.x1 = ax; r.y1 = ay; }
+    }
+    return r;
+}
+
+// open-run state per row: valid(1) | slot(2) | start(14) | last(14)
+__device__ __forceinline__ uint32_t pack_open(int slot, int s, int l) {
+    return 1u | ((uint32_t)slot << 1) | ((uint32_t)s << 3) | ((uint32_t)l << 17);
+}
+
+struct Lds {
+    double2* gaps;    // [gcap]
+    double2* gaps2;   // [gcap] merge output
+    double2* blocks;  // [bcap]
+    int* ga;          // [gcap] first visited ind per gap
+    int* gpre;        // [gcap+1] exclusive prefix of visited counts
+    uint32_t* openr;  // [dmax+2]
+    uint16_t* cnt;    // [3*(dmax+1)]
+    unsigned* binc;   // [32] node counts per bin
+    unsigned* bfar;   // [32] far distance (float bits)
+    int* bnr;         // [32] runs per bin
+    int* misc;        // [32] scalars: 0 ng, 1 nb, 16..23 segment start, 24..31 segment length
+    double2* bsorted; // [bcap] sort output
+    int* bflag;       // [bcap] first-occurrence flags
+};
+
+__global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int lane = lane_id();
+    const int gcap = P.gcap, bcap = P.bcap, D = P.dmax;
+    Lds L;
+    {
+        unsigned char* p = smem;
+        L.gaps = (double2*)p; p += sizeof(double2) * gcap;
+        L.gaps2 = (double2*)p; p += sizeof(double2) * gcap;
+        L.blocks = (double2*)p; p += sizeof(double2) * bcap;
+        L.binc = (unsigned*)p; p += 4 * 32;
+        L.bfar = (unsigned*)p; p += 4 * 32;
+        L.bnr = (int*)p; p += 4 * 32;
+        L.misc = (int*)p; p += 4 * 32;
+        L.bsorted = (double2*)p; p += sizeof(double2) * bcap;
+        L.ga = (int*)p; p += 4 * gcap;
+        L.bflag = (int*)p; p += 4 * bcap;
+        L.gpre = (int*)p; p += 4 * (gcap + 4);
+        L.openr = (uint32_t*)p; p += 4 * (D + 4);
+        L.cnt = (uint16_t*)p;
+    }
+    const int wave_global = blockIdx.x;
+    unsigned long long* stA = P.stageA + (size_t)wave_global * P.capA;
+    Run* stB = P.stageB + (size_t)wave_global * P.capB;
+    uint32_t* pref = P.prefix + (size_t)wave_global * (3 * (D + 1) + 4);
+    const double sp = P.spacing;
+
+    // LDS state that persists across sources is reset here once
+    const int AX = 3 * (D + 1); // cnt[AX] counts the runs of the axis row (ind 0)
+    for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
+    for (int i = lane; i <= AX; i += 64) L.cnt[i] = 0;
+    __syncthreads();
+
+    for (;;) {
+        int s_idx = 0;
+        if (lane == 0) s_idx = atomicAdd(P.work_counter, 1);
+        s_idx = __shfl(s_idx, 0);
+        const int64_t node = P.node_begin + s_idx;
+        if (node >= P.node_end) break;
+        const int cell = P.node_cell[node];
+        const int cx = cell / P.rows, cy = cell % P.rows;
+        const double c0x = P.blx + sp * 1.0 * (double)cx, c0y = P.bly + sp * 1.0 * (double)cy;
+        if (lane < 32) { L.binc[lane] = 0; L.bfar[lane] = 0; L.bnr[lane] = 0; }
+        __syncthreads();
+
+        double tsum = 0.0, tsum2 = 0.0; // wave-uniform, reference order
+        int nsize = 0;
+        unsigned long long examined = 0;
+        int bpos = 0;        // next free run slot in stageB
+        bool failed = false;
+
+        const uint32_t own = P.cellw[cell];
+        const int own_n = cell_nseg(own), own_off = cell_seg_off(own);
+
+        for (int q = 0; q < 8; q++) {
+            // ---- depth 0: own-cell segments cropped to the quarter viewport (pointdata.cpp:1399-1450)
+            const double border = sp * 1e-10;
+            Rect vp{P.blx + sp * ((double)cx - 0.5 - 1e-10), P.bly + sp * ((double)cy - 0.5 - 1e-10),
+                    P.blx + sp * ((double)cx + 0.5 + 1e-10), P.bly + sp * ((double)cy + 0.5 + 1e-10)};
+            switch (q) {
+            case 0: vp.trx = c0x; vp.bly = c0y - border; break;
+            case 6: vp.trx = c0x + border; vp.bly = c0y; break;
+            case 1: vp.blx = c0x; vp.bly = c0y - border; break;
+            case 7: vp.blx = c0x - border; vp.bly = c0y; break;
+            case 2: vp.trx = c0x; vp.tr_y = c0y + border; break;
+            case 4: vp.trx = c0x + border; vp.tr_y = c0y; break;
+            case 3: vp.blx = c0x; vp.tr_y = c0y + border; break;
+            case 5: vp.blx = c0x - border; vp.tr_y = c0y; break;
+            }
+            if (lane == 0) { L.misc[0] = 1; L.misc[1] = 0; }
+            if (lane == 0) L.gaps[0] = make_double2(0.0, 1.0);
+            __syncthreads();
+            for (int i = lane; i < own_n; i += 64) {
+                const double* sg = P.segs + 4 * (size_t)(own_off + i);
+                Seg l = make_seg(Vec2{sg[0], sg[1]}, Vec2{sg[2], sg[3]});
+                if (clip_seg(l, vp)) {
+                    Vec2 a = l.start(), b = l.end();
+                    double ta = tanify(c0x, c0y, a.x, a.y, q), tb = tanify(c0x, c0y, b.x, b.y, q);
+                    int slot = atomicAdd(&L.misc[1], 1);
+                    if (slot < bcap)
+                        L.blocks[slot] = (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10);
+                }
+            }
+            __syncthreads();
+
+            int ng = 1;
+            int dq = 0;                 // deepest depth visited in this octant
+            int diag_n = 0, diag_min = 0, diag_max = 0;
+            int nA = 0;                 // emissions staged in this octant
+            const int q_sector = c_sector_base[q], q_axis = c_axis_bin[q], q_diag = c_diag_bin[q];
+            int depth = 0;
+            for (;;) {
+                // ---------------- collectgarbage (sparksieve2.cpp:89-132) for the previous depth
+                int nb = L.misc[1];
+                if (nb > bcap) { failed = true; if (lane == 0) atomicOr(P.error, KERR_BLOCK_CAPACITY); }
+                if (failed) break;
+                if (nb > 0) {
+                    // std::sort (start asc, end desc) + std::unique: first-occurrence flags, then
+                    // each distinct block lands at its rank among the distinct blocks
+                    for (int i = lane; i < nb; i += 64) {
+                        double2 me = L.blocks[i];
+                        int first = 1;
+                        for (int j = 0; j < i; j++) {
+                            double2 o = L.blocks[j];
+                            if (o.x == me.x && o.y == me.y) { first = 0; break; }
+                        }
+                        L.bflag[i] = first;
+                    }
+                    __syncthreads();
+                    int nu = 0;
+                    for (int i = lane; i < nb; i += 64) {
+                        if (!L.bflag[i]) continue;
+                        double2 me = L.blocks[i];
+                        int rank = 0;
+                        for (int j = 0; j < nb; j++) {
+                            double2 o = L.blocks[j];
+                            if (L.bflag[j] && zone_less(o.x, o.y, me.x, me.y)) rank++;
+                        }
+                        L.bsorted[rank] = me;
+                    }
+                    for (int base = 0; base < nb; base += 64) nu += __popcll(ballot(base + lane < nb && L.bflag[base + lane]));
+                    __syncthreads();
+                    for (int i = lane; i < nu; i += 64) L.blocks[i] = L.bsorted[i];
+                    __syncthreads();
+                    // sequential merge on lane 0: gaps -> gaps2
+                    if (lane == 0) {
+                        int gi = 0, bi = 0, no = 0;
+                        bool over = false;
+                        double2 cur = (ng > 0) ? L.gaps[0] : make_double2(0, 0);
+                        while (bi < nu && gi < ng) {
+                            double2 bk = L.blocks[bi];
+                            if (bk.y < cur.x) { bi++; continue; }
+                            bool create = true;
+                            if (bk.x <= cur.x) { create = false; if (bk.y > cur.x) cur.x = bk.y; }
+                            if (bk.y >= cur.y) { create = false; if (bk.x < cur.y) cur.y = bk.x; }
+                            if (cur.y <= cur.x + 1e-10) {
+                                gi++;
+                                if (gi < ng) cur = L.gaps[gi];
+                                continue;
+                            } else if (bk.y > cur.y) {
+                                if (no < gcap) L.gaps2[no] = cur; else over = true;
+                                no++;
+                                gi++;
+                                if (gi < ng) cur = L.gaps[gi];
+                                continue;
+                            } else if (create) {
+                                if (no < gcap) L.gaps2[no] = make_double2(cur.x, bk.x); else over = true;
+                                no++;
+                                cur.x = bk.y;
+                            }
+                            bi++;
+                        }
+                        if (gi < ng) {
+                            if (no < gcap) L.gaps2[no] = cur; else over = true;
+                            no++;
+                            for (int g = gi + 1; g < ng; g++) {
+                                if (no < gcap) L.gaps2[no] = L.gaps[g]; else over = true;
+                                no++;
+                            }
+                        }
+                        if (over) { atomicOr(P.error, KERR_GAP_CAPACITY); no = -1; }
+                        L.misc[0] = no;
+                    }
+                    __syncthreads();
+                    ng = L.misc[0];
+                    if (ng < 0) { failed = true; break; }
+                    for (int i = lane; i < ng; i += 64) L.gaps[i] = L.gaps2[i];
+                    if (lane == 0) L.misc[1] = 0;
+                    __syncthreads();
+                }
+                // loop condition: sieve.hasGaps() (pointdata.cpp:1454)
+                if (ng == 0) break;
+                depth++;
+                // ---------------- sieve2 for this depth (pointdata.cpp:1512-1565)
+                // per-gap visit ranges with the monotone firstind rule
+                int carryF = 0, carryT = 0;
+                for (int base = 0; base < ng; base += 64) {
+                    int g = base + lane;
+                    int lo = 0, b = -1;
+                    bool vis = false;
+                    if (g < ng) {
+                        double2 z = L.gaps[g];
+                        lo = (int)ceil(z.x * (depth - 0.5) - 0.5);
+                        int hi = (int)floor(z.y * (depth + 0.5) + 0.5);
+                        b = min(hi, depth);
+                        vis = (b >= lo);
+                    }
+                    int bp = vis ? b : INT_MIN;
+                    int incl = wave_incl_max(bp);
+                    int excl = __shfl_up(incl, 1);
+                    if (lane == 0) excl = INT_MIN;
+                    int F = max(carryF, max(excl, 0));
+                    int a = max(lo, F);
+                    int c = (g < ng && b >= a) ? (b - a + 1) : 0;
+                    int ci = wave_incl_sum(c);
+                    if (g < ng) { L.ga[g] = a; L.gpre[g] = carryT + ci - c; }
+                    carryT += __shfl(ci, 63);
+                    carryF = max(carryF, __shfl(incl, 63));
+                }
+                if (lane == 0) L.gpre[ng] = carryT;
+                __syncthreads();
+                const int T = carryT;
+                examined += (unsigned long long)T;
+                bool hasgaps = false;
+                int gcur = 0; // per-lane gap pointer (t increases monotonically)
+                for (int t0 = 0; t0 < T; t0 += 64) {
+                    int t = t0 + lane;
+                    bool valid = t < T;
+                    int ind = 0, hx = 0, hy = 0;
+                    double gst = 0, gen = 0;
+                    bool ingrid = false, add = false;
+                    uint32_t w = 0;
+                    if (valid) {
+                        while (L.gpre[gcur + 1] <= t) gcur++;
+                        ind = L.ga[gcur] + (t - L.gpre[gcur]);
+                        double2 z = L.gaps[gcur];
+                        gst = z.x; gen = z.y;
+                        octant_cell(q, cx, cy, depth, ind, hx, hy);
+                        ingrid = (hx >= 0 && hx < P.cols && hy >= 0 && hy < P.rows);
+                    }
+                    if (ingrid) {
+                        const int hc = hx * P.rows + hy;
+                        w = P.cellw[hc];
+                        const int nl = cell_nseg(w), off = cell_seg_off(w);
+                        const bool centregap = ((double)ind >= gst * depth && (double)ind <= gen * depth);
+                        if (centregap && cell_filled(w) &&
+                            (ind != 0 || q == 0 || q == 1 || q == 5 || q == 6) && (ind != depth || q < 4)) {
+                            // sparkSieve2::testblock (sparksieve2.cpp:45-63)
+                            const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
+                            bool blocked = false;
+                            if (P.maxdist != -1.0 || nl > 0) {
+                                Seg ray = make_seg(Vec2{c0x, c0y}, Vec2{px, py});
+                                if (P.maxdist != -1.0 && ray.length() > P.maxdist) blocked = true;
+                                const double tol = sp * 1e-10;
+                                for (int k = 0; k < nl && !blocked; k++) {
+                                    const double* sg = P.segs + 4 * (size_t)(off + k);
+                                    Seg s = make_seg(Vec2{sg[0], sg[1]}, Vec2{sg[2], sg[3]});
+                                    if (rects_touch(ray.r, s.r, tol) && segs_cross(ray, s, tol)) blocked = true;
+                                }
+                            }
+                            add = !blocked;
+                        }
+                        // sparkSieve2::block for every in-grid candidate (sparksieve2.cpp:67-87)
+                        for (int k = 0; k < nl; k++) {
+                            const double* sg = P.segs + 4 * (size_t)(off + k);
+                            double ta = tanify(c0x, c0y, sg[0], sg[1], q), tb = tanify(c0x, c0y, sg[2], sg[3], q);
+                            int slot = atomicAdd(&L.misc[1], 1);
+                            if (slot < bcap)
+                                L.blocks[slot] = (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10);
+                        }
+                    }
+                    hasgaps |= (ballot(ingrid) != 0ull);
+                    // ---- visible cells: bins, moments (reference order), run tracking
+                    unsigned long long am = ballot(add);
+                    if (am) {
+                        int bin = -1;
+                        double this_dist = 0.0;
+                        if (add) {
+                            const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
+                            bin = whichbin(px - c0x, py - c0y);
+                            const double dx = (double)(hx - cx), dy = (double)(hy - cy);
+                            this_dist = sqrt(dx * dx + dy * dy) * sp;
+                            atomicAdd(&L.binc[bin], 1u);
+                            atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
+                        }
+                        // serial sums in lane order = reference addlist order
+                        unsigned long long mm = am;
+                        while (mm) {
+                            int l = __ffsll((long long)mm) - 1;
+                            double v = __shfl(this_dist, l);
+                            tsum += v;
+                            tsum2 += v * v;
+                            mm &= mm - 1;
+                        }
+                        nsize += __popcll(am);
+                        // run tracking
+                        bool emit = false;
+                        unsigned long long rec = 0;
+                        if (add) {
+                            if (ind == depth && q < 4) { // diagonal bin: single span (ngraph.cpp:243-258)
+                                if (bin != q_diag) atomicOr(P.error, KERR_BIN_MISMATCH);
+                            } else {
+                                int slot;
+                                if (ind == 0) { slot = 3; if (bin != q_axis) atomicOr(P.error, KERR_BIN_MISMATCH); }
+                                else { slot = bin - q_sector; if (slot < 0 || slot > 2) { atomicOr(P.error, KERR_BIN_MISMATCH); slot = 0; } }
+                                uint32_t o = L.openr[ind];
+                                int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
+                                if ((o & 1u) && oslot == slot && ol == depth - 1) {
+                                    L.openr[ind] = pack_open(slot, os, depth);
+                                } else {
+                                    if (o & 1u) {
+                                        const int ci = (oslot == 3) ? AX : oslot * (D + 1) + ind;
+                                        const int k = L.cnt[ci];
+                                        L.cnt[ci] = (uint16_t)(k + 1);
+                                        emit = true;
+                                        rec = pack_emit(oslot, ind, os, ol, k);
+                                    }
+                                    L.openr[ind] = pack_open(slot, depth, depth);
+                                }
+                            }
+                        }
+                        // the diagonal cell (at most one per depth) -- wave-uniform bookkeeping
+                        unsigned long long dm = ballot(add && ind == depth && q < 4);
+                        if (dm) {
+                            if (diag_n == 0) diag_min = depth;
+                            diag_max = depth;
+                            diag_n++;
+                        }
+                        unsigned long long em = ballot(emit);
+                        if (em) {
+                            int pos = nA + prefix_popc(em);
+                            if (emit) {
+                                if (pos < P.capA) stA[pos] = rec;
+                            }
+                            nA += __popcll(em);
+                        }
+                    }
+                }
+                if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
+                if (!hasgaps) break;      // sieve2 returned false (pointdata.cpp:1458)
+                dq = depth;
+                __syncthreads();
+            }
+            if (failed) break;
+            // ---------------- flush open rows, then place this octant's runs canonically
+            __syncthreads();
+            for (int base = 0; base <= dq; base += 64) {
+                int ind = base + lane;
+                bool emit = false;
+                unsigned long long rec = 0;
+                if (ind <= dq) {
+                    uint32_t o = L.openr[ind];
+                    if (o & 1u) {
+                        int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
+                        const int ci = (oslot == 3) ? AX : oslot * (D + 1) + ind;
+                        const int k = L.cnt[ci];
+                        L.cnt[ci] = (uint16_t)(k + 1);
+                        emit = true;
+                        rec = pack_emit(oslot, ind, os, ol, k);
+                    }
+                    L.openr[ind] = 0;
+                }
+                unsigned long long em = ballot(emit);
+                if (em) {
+                    int pos = nA + prefix_popc(em);
+                    if (emit && pos < P.capA) stA[pos] = rec;
+                    nA += __popcll(em);
+                }
+            }
+            if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); break; }
+            __syncthreads();
+            // exclusive prefix over (slot, canonical row) -> pref[]
+            const int R1 = dq + 1;
+            const int nkeys = 3 * R1;
+            const int rasc = c_row_asc[q], dasc = c_d_asc[q];
+            int carry = 0;
+            for (int base = 0; base < nkeys; base += 64) {
+                int key = base + lane;
+                int c = 0;
+                if (key < nkeys) {
+                    int slot = key / R1, r = key % R1;
+                    int ind = rasc ? r : (dq - r);
+                    c = L.cnt[slot * (D + 1) + ind];
+                }
+                int ci = wave_incl_sum(c);
+                if (key < nkeys) pref[key] = carry + ci - c;
+                carry += __shfl(ci, 63);
+            }
+            const int nsector = carry;
+            const int axis_runs = L.cnt[AX];
+            if (lane == 0) pref[nkeys] = carry;
+            // per-bin run counts for the sectors
+            {
+                int s0 = 0, s1 = 0;
+                // slot boundaries in key space are multiples of R1
+                __syncthreads();
+                s0 = pref[R1];
+                s1 = pref[2 * R1];
+                if (lane == 0) {
+                    L.bnr[q_sector + 0] += s0;
+                    L.bnr[q_sector + 1] += s1 - s0;
+                    L.bnr[q_sector + 2] += nsector - s1;
+                    if (q_axis >= 0) L.bnr[q_axis] += axis_runs;
+                    if (q_diag >= 0) L.bnr[q_diag] += (diag_n > 0) ? 1 : 0;
+                }
+            }
+            const int diag_runs = (diag_n > 0) ? 1 : 0;
+            int low_n = 0;
+            if (c_axis_low[q]) low_n = axis_runs;
+            if (c_diag_low[q]) low_n = diag_runs;
+            const int seg_len = low_n + nsector + (c_axis_low[q] ? 0 : (q_axis >= 0 ? axis_runs : 0)) +
+                                (c_diag_low[q] ? 0 : diag_runs);
+            if (bpos + seg_len > P.capB) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); break; }
+            Run* seg = stB + bpos;
+            const int high_base = low_n + nsector;
+            __syncthreads();
+            for (int i = lane; i < nA; i += 64) {
+                unsigned long long rec = stA[i];
+                int slot = (int)(rec & 3ull), ind = (int)((rec >> 2) & 0x3fff), ds = (int)((rec >> 16) & 0x3fff);
+                int de = (int)((rec >> 30) & 0x3fff), k = (int)((rec >> 44) & 0x3fff);
+                int pos;
+                if (slot == 3) {
+                    int base = c_axis_low[q] ? 0 : high_base;
+                    pos = base + (dasc ? k : (axis_runs - 1 - k));
+                } else {
+                    int r = rasc ? ind : (dq - ind);
+                    int key = slot * R1 + r;
+                    pos = low_n + (dasc ? (int)pref[key] + k : (int)pref[key + 1] - 1 - k);
+                }
+                seg[pos] = make_run(q, cx, cy, ind, ds, de);
+            }
+            if (diag_runs && lane == 0) {
+                // Bin::make diagonal: first pushed pixel, replaced by the last one if it lies left/right
+                int fx, fy, lx, ly;
+                octant_cell(q, cx, cy, diag_min, diag_min, fx, fy);
+                octant_cell(q, cx, cy, diag_max, diag_max, lx, ly);
+                Run r;
+                r.x0 = fx; r.y0 = fy; r.x1 = fx; r.y1 = fy;
+                if (lx < r.x0) { r.x0 = lx; r.y0 = ly; }
+                if (lx > r.x1) { r.x1 = lx; r.y1 = ly; }
+                int pos = c_diag_low[q] ? 0 : high_base;
+                seg[pos] = r;
+            }
+            // reset the per-row counters used by this octant
+            __syncthreads();
+            for (int i = lane; i < AX; i += 64)
+                if (i % (D + 1) <= dq) L.cnt[i] = 0;
+            if (lane == 0) { L.cnt[AX] = 0; L.misc[16 + q] = bpos; L.misc[24 + q] = seg_len; }
+            bpos += seg_len;
+            __syncthreads();
+        }
+        if (failed) {
+            // leave the wave in a clean LDS state and drop this source
+            for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
+            for (int i = lane; i <= AX; i += 64) L.cnt[i] = 0;
+            __syncthreads();
+            continue;
+        }
+        // ---------------- publish: reserve pool space, copy segments in bin order 0..31
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(P.pool_cursor, (unsigned long long)bpos);
+        base = __shfl(base, 0);
+        const int64_t k = node - P.node_begin;
+        if ((int64_t)(base + bpos) > P.pool_capacity) {
+            if (lane == 0) atomicOr(P.error, KERR_POOL_CAPACITY);
+            P.node_run_start[k] = -1;
+        } else {
+            int64_t dst = (int64_t)base;
+            for (int si = 0; si < 8; si++) {
+                int q = c_seg_order[si];
+                const Run* src = stB + L.misc[16 + q];
+                const int len = L.misc[24 + q];
+                for (int i = lane; i < len; i += 64) P.pool[dst + i] = src[i];
+                dst += len;
+            }
+            if (lane == 0) P.node_run_start[k] = (int64_t)base;
+        }
+        __syncthreads();
+        if (lane < 32) {
+            P.bin_nruns[k * 32 + lane] = L.bnr[lane];
+            P.bin_count[k * 32 + lane] = (uint16_t)L.binc[lane];
+            P.bin_dist[k * 32 + lane] = __uint_as_float(L.bfar[lane]);
+        }
+        if (lane == 0) {
+            atomicAdd(&P.stats[0], examined);
+            atomicAdd(&P.stats[1], (unsigned long long)nsize);
+            P.attrs[k * 3 + 0] = (float)nsize;
+            P.attrs[k * 3 + 1] = (float)tsum;
+            P.attrs[k * 3 + 2] = (float)tsum2;
+        }
+        __syncthreads();
+    }
+}
+
+// addGridConnections (pointdata.cpp:1735-1768): bit i/4 set if the 8-neighbour in direction i is
+// covered by bin i (0,4,..,28).  One thread per node.
+__global__ void gridconn_kernel(int rows, const int32_t* node_cell, int64_t n, const int64_t* node_run_start,
+                                const int32_t* bin_nruns, const Run* pool, uint8_t* out) {
+    int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int cell = node_cell[k];
+    const int cx = cell / rows, cy = cell % rows;
+    const int nx[8] = {cx + 1, cx + 1, cx, cx - 1, cx - 1, cx - 1, cx, cx + 1};
+    const int ny[8] = {cy, cy + 1, cy + 1, cy + 1, cy, cy - 1, cy - 1, cy - 1};
+    int64_t off = node_run_start[k];
+    uint8_t gc = 0;
+    for (int b = 0; b < 32; b++) {
+        const int nr = bin_nruns[k * 32 + b];
+        if ((b & 3) == 0) {
+            const int i = b >> 2;
+            for (int r = 0; r < nr; r++) {
+                Run ru = pool[off + r];
+                bool hit;
+                if (ru.y0 == ru.y1 && ru.x0 != ru.x1) hit = (ny[i] == ru.y0 && nx[i] >= ru.x0 && nx[i] <= ru.x1);
+                else if (ru.x0 == ru.x1 && ru.y0 != ru.y1) hit = (nx[i] == ru.x0 && ny[i] >= ru.y0 && ny[i] <= ru.y1);
+                else if (ru.x0 == ru.x1) hit = (nx[i] == ru.x0 && ny[i] == ru.y0);
+                else {
+                    int dy = (ru.y1 > ru.y0) ? 1 : -1;
+                    hit = nx[i] >= ru.x0 && nx[i] <= ru.x1 && (ny[i] - ru.y0) == dy * (nx[i] - ru.x0);
+                }
+                if (hit) { gc |= (uint8_t)(1 << i); break; }
+            }
+        }
+        off += nr;
+    }
+    out[k] = gc;
+}
+
+} // namespace dmx

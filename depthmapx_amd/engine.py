@@ -1,0 +1,173 @@
+"""Python host mirror of the depthmapX VISPREP / VGA operator surface over the C ABI (include/dmx.h).
+
+    ctx = Context(0)
+    pm = PointMap(region, lines, spacing)            # MetaGraph::addNewPointMap + setGrid
+    pm.make_points(x, y)                              # PointMap::makePoints (FULLFILL)
+    g = pm.make_graph(ctx)                            # MetaGraph::makeGraph -> sparkGraph2 (GPU)
+    cols = g.vga_visual_global(radius=-1)             # VGAVisualGlobal::run (GPU)
+
+Column orders follow the reference attribute tables (see VGA_COLUMNS / MAKEGRAPH_COLUMNS).
+"""
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+MAKEGRAPH_COLUMNS = ["Connectivity", "Point First Moment", "Point Second Moment"]
+VGA_COLUMNS = ["Visual Entropy", "Visual Integration [HH]", "Visual Integration [P-value]",
+               "Visual Integration [Tekl]", "Visual Mean Depth", "Visual Node Count",
+               "Visual Relativised Entropy"]
+
+
+class Context:
+    """One HIP device (one process per GPU)."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        N.check(N.lib().dmx_ctx_create(int(device), ctypes.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            N.lib().dmx_ctx_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def last_timing(self):
+        mk, vg = ctypes.c_double(), ctypes.c_double()
+        N.check(N.lib().dmx_ctx_last_timing(self.h, ctypes.byref(mk), ctypes.byref(vg)))
+        return mk.value, vg.value
+
+    def last_stats(self):
+        out = np.zeros(8, dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 8))
+        keys = ["mk_cells_examined", "mk_visible_pairs", "mk_runs", "", "vga_runs_expanded", "", "vga_cells_reached",
+                "vga_sources"]
+        return {k: int(v) for k, v in zip(keys, out) if k}
+
+
+class PointMap:
+    """A VGA point map: grid over the drawing region, occluder pieces per cell, filled cells."""
+
+    def __init__(self, region, lines, spacing):
+        self._region = np.ascontiguousarray(region, dtype=np.float64)
+        self._lines = np.ascontiguousarray(lines, dtype=np.float64).reshape(-1, 4)
+        h = ctypes.c_void_p()
+        N.check(N.lib().dmx_pointmap_create(N.ptr(self._region), float(spacing), N.ptr(self._lines),
+                                            len(self._lines), ctypes.byref(h)))
+        self.h = h
+        self.spacing = float(spacing)
+
+    def close(self):
+        if getattr(self, "h", None):
+            N.lib().dmx_pointmap_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def info(self):
+        c, r, f = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        bx, by = ctypes.c_double(), ctypes.c_double()
+        N.check(N.lib().dmx_pointmap_info(self.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(bx),
+                                          ctypes.byref(by), ctypes.byref(f)))
+        return dict(cols=c.value, rows=r.value, bottom_left=(bx.value, by.value), filled=f.value)
+
+    @property
+    def cols(self):
+        return self.info()["cols"]
+
+    @property
+    def rows(self):
+        return self.info()["rows"]
+
+    def make_points(self, x, y):
+        """runmethods fillGraph + PointMap::makePoints; raises DmxError(DMX_ERR_OUTSIDE) like the CLI's
+        'Point outside of target region'; returns False where makePoints returns false."""
+        made = ctypes.c_int()
+        N.check(N.lib().dmx_pointmap_fill(self.h, float(x), float(y), ctypes.byref(made)))
+        return bool(made.value)
+
+    def state(self):
+        i = self.info()
+        out = np.zeros(i["cols"] * i["rows"], dtype=np.int32)
+        N.check(N.lib().dmx_pointmap_state(self.h, N.ptr(out)))
+        return out
+
+    def cell_lines(self):
+        i = self.info()
+        total = ctypes.c_int64()
+        N.check(N.lib().dmx_pointmap_cell_lines(self.h, None, None, ctypes.byref(total)))
+        counts = np.zeros(i["cols"] * i["rows"], dtype=np.int32)
+        pieces = np.zeros((max(total.value, 1), 4), dtype=np.float64)
+        N.check(N.lib().dmx_pointmap_cell_lines(self.h, N.ptr(counts), N.ptr(pieces), ctypes.byref(total)))
+        return counts, pieces[:total.value]
+
+    def make_graph(self, ctx, boundarygraph=False, maxdist=-1.0, node_begin=0, node_end=-1):
+        h = ctypes.c_void_p()
+        N.check(N.lib().dmx_makegraph(ctx.h, self.h, float(maxdist), int(bool(boundarygraph)), int(node_begin),
+                                      int(node_end), ctypes.byref(h)))
+        return Graph(h, ctx, self)
+
+    def assemble(self, ctx, blob_ptrs, blob_sizes):
+        """Whole-map graph from shard blobs living in device memory (e.g. all-gathered torch tensors)."""
+        ptrs = (ctypes.c_void_p * len(blob_ptrs))(*blob_ptrs)
+        sizes = np.ascontiguousarray(blob_sizes, dtype=np.int64)
+        h = ctypes.c_void_p()
+        N.check(N.lib().dmx_graph_assemble_device(ctx.h, self.h, ptrs, N.ptr(sizes), len(blob_ptrs),
+                                                  ctypes.byref(h)))
+        return Graph(h, ctx, self)
+
+
+class Graph:
+    """The run-length visibility graph (device resident)."""
+
+    def __init__(self, h, ctx, pm):
+        self.h, self.ctx, self.pm = h, ctx, pm
+
+    def close(self):
+        if getattr(self, "h", None):
+            N.lib().dmx_graph_free(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def info(self):
+        n, b, e, r = (ctypes.c_int64() for _ in range(4))
+        N.check(N.lib().dmx_graph_info(self.h, ctypes.byref(n), ctypes.byref(b), ctypes.byref(e), ctypes.byref(r)))
+        return dict(nnodes=n.value, node_begin=b.value, node_end=e.value, nruns=r.value)
+
+    def copy(self, runs=True):
+        i = self.info()
+        n = i["node_end"] - i["node_begin"]
+        attrs = np.zeros((n, 3), dtype=np.float32)
+        bins = np.zeros((n, 32, 4), dtype=np.int32)
+        gc = np.zeros(n, dtype=np.uint8)
+        rr = np.zeros((max(i["nruns"], 1), 4), dtype=np.int16) if runs else None
+        N.check(N.lib().dmx_graph_copy(self.h, N.ptr(attrs), N.ptr(bins), N.ptr(rr), N.ptr(gc)))
+        out = dict(attrs=attrs, bins=bins, gridconn=gc)
+        if runs:
+            out["runs"] = rr[:i["nruns"]]
+        return out
+
+    def blob_size(self):
+        b = ctypes.c_int64()
+        N.check(N.lib().dmx_graph_blob_size(self.h, ctypes.byref(b)))
+        return b.value
+
+    def write_blob_device(self, dev_ptr, nbytes):
+        N.check(N.lib().dmx_graph_blob_write_device(self.h, ctypes.c_void_p(dev_ptr), int(nbytes)))
+
+    def vga_visual_global(self, radius=-1.0, gates_only=False, src_begin=0, src_end=-1, levels=False):
+        n = self.info()["nnodes"]
+        out = np.full((n, 7), -1.0, dtype=np.float32)
+        lv = np.zeros((n, 3), dtype=np.int64) if levels else None
+        N.check(N.lib().dmx_vga_global(self.ctx.h, self.h, float(radius), int(bool(gates_only)), int(src_begin),
+                                       int(src_end), N.ptr(out), N.ptr(lv)))
+        return (out, lv) if levels else out
+
+    def vga_visual_global_device(self, out_dev_ptr, radius=-1.0, gates_only=False, src_begin=0, src_end=-1):
+        N.check(N.lib().dmx_vga_global_device(self.ctx.h, self.h, float(radius), int(bool(gates_only)),
+                                              int(src_begin), int(src_end), ctypes.c_void_p(out_dev_ptr)))

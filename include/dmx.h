@@ -1,0 +1,113 @@
+/* dmx.h -- C ABI of the MI355X visibility-graph engine (libdmx.so).
+ *
+ * Drop-in boundary for the depthmapX VISPREP makeGraph + VGA global path.  Every entry point is
+ * extern "C", takes plain pointers and sizes, never throws, and returns an int status
+ * (DMX_OK = 0, negative on error; dmx_last_error() explains).  The reference interface each one
+ * replaces is cited as file:line in orange-vertex/depthmapX.
+ *
+ * Ownership: the library owns contexts, point maps and graphs (device buffers included); callers
+ * release them with the matching *_free.  Host arrays passed in are copied; host arrays passed out
+ * are caller-allocated with the sizes the *_info calls report.  Device pointers (dmx_*_device)
+ * must be valid on the context's device.  One context per device; one process per GPU.
+ */
+#ifndef DMX_H
+#define DMX_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DMX_ABI_VERSION 1
+
+enum {
+    DMX_OK = 0,
+    DMX_ERR_ARG = -1,          /* invalid argument / handle */
+    DMX_ERR_HIP = -2,          /* HIP runtime error (no device, launch failure, OOM) */
+    DMX_ERR_CAPACITY = -3,     /* a kernel capacity was exceeded even after retries */
+    DMX_ERR_STATE = -4,        /* call sequence not allowed (e.g. makegraph on an unfilled map) */
+    DMX_ERR_UNSUPPORTED = -5,  /* feature of the reference not (yet) implemented on this path */
+    DMX_ERR_OUTSIDE = -6       /* fill point outside the region ("Point outside of target region") */
+};
+
+typedef struct dmx_ctx dmx_ctx;
+typedef struct dmx_pointmap dmx_pointmap;
+typedef struct dmx_graph dmx_graph;
+
+/* ---- library / device ------------------------------------------------------------------ */
+int dmx_abi_version(void);
+/* Thread-local message for the last failing call on this thread. */
+const char* dmx_last_error(void);
+/* Bind a context to HIP device `device` (the process-local ordinal).  No reference counterpart:
+ * salalib is single-threaded CPU code. */
+int dmx_ctx_create(int device, dmx_ctx** out);
+int dmx_ctx_free(dmx_ctx* ctx);
+/* Wall time of the kernels of the last makegraph / vga call, measured with HIP events on the
+ * context stream (seconds); kernel_ms receives per-kernel averages. */
+int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
+/* Work counters of the last calls (for roofline accounting): [0] sieve cells examined,
+ * [1] visible (source,target) pairs, [2] runs written, [4] runs expanded by the BFS,
+ * [5] reserved, [6] cells reached (sum over sources), [7] sources run. */
+int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
+
+/* ---- VISPREP preparation (host model) ----------------------------------------------------- */
+/* MetaGraph::addNewPointMap + PointMap::setGrid(spacing, (0,0)) (salalib/pointdata.cpp:122-171),
+ * with the drawing `lines` ([n][4] = x1,y1,x2,y2 as PointMap::blockLines reads them,
+ * pointdata.cpp:308-320) inside `region` (= MetaGraph::getRegion(), [4] = blx,bly,trx,try). */
+int dmx_pointmap_create(const double* region, double spacing, const double* lines, int64_t nlines,
+                        dmx_pointmap** out);
+int dmx_pointmap_free(dmx_pointmap* pm);
+/* dm_runmethods::fillGraph -> PointMap::makePoints(p, FULLFILL) (depthmapXcli/runmethods.cpp:269-277,
+ * salalib/pointdata.cpp:402-481).  DMX_ERR_OUTSIDE if the point is outside the region;
+ * *made = 0 where makePoints returns false. */
+int dmx_pointmap_fill(dmx_pointmap* pm, double x, double y, int* made);
+/* cols, rows, bottom-left cell centre, filled count. */
+int dmx_pointmap_info(const dmx_pointmap* pm, int32_t* cols, int32_t* rows, double* bl_x, double* bl_y,
+                      int64_t* filled);
+/* Point::m_state per cell, x-major (cell = x*rows + y, ColumnMatrix order, simplematrix.h:193-218). */
+int dmx_pointmap_state(const dmx_pointmap* pm, int32_t* out);
+/* Cropped occluder pieces per cell after blockLines: counts[C], pieces[total][4]. */
+int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, int64_t* total);
+
+/* ---- makeGraph (GPU) ---------------------------------------------------------------------- */
+/* MetaGraph::makeGraph(comm, boundary, maxdist) -> PointMap::sparkGraph2 (salalib/mgraph.cpp:264-284,
+ * pointdata.cpp:1246-1341).  Builds nodes [node_begin, node_end) of the filled cells in x-major
+ * order (node_end < 0: all) -- a sub-range is one rank's shard.  maxdist = -1: unrestricted. */
+int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int64_t node_begin,
+                  int64_t node_end, dmx_graph** out);
+int dmx_graph_free(dmx_graph* g);
+/* nodes in the whole map, first/last node built here, runs held. */
+int dmx_graph_info(const dmx_graph* g, int64_t* nnodes, int64_t* node_begin, int64_t* node_end, int64_t* nruns);
+/* Copies in reference layout (rows for the built range only, node order):
+ *   attrs[n][3]  Connectivity, Point First Moment, Point Second Moment (pointdata.cpp:1494-1497)
+ *   bins[n][32][4]  Bin::m_dir, m_node_count (u16), m_distance (f32 bits), runs in bin (ngraph.h:48-60)
+ *   runs[R][4]   PixelVec start.x,start.y,end.x,end.y in Bin order (ngraph.cpp:234-304)
+ *   gridconn[n]  Point::m_grid_connections (pointdata.cpp:1735-1768)
+ * Any pointer may be NULL. */
+int dmx_graph_copy(dmx_graph* g, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn);
+
+/* Shard exchange for multi-GPU runs: a graph's built range serialises into one flat blob
+ * (device memory) that another rank's dmx_graph_assemble can consume. */
+int dmx_graph_blob_size(dmx_graph* g, int64_t* bytes);
+int dmx_graph_blob_write_device(dmx_graph* g, void* dst_device, int64_t bytes);
+/* Build the whole-map graph from nshards blobs (device pointers, any order of ranges). */
+int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const* blobs, const int64_t* sizes,
+                              int nshards, dmx_graph** out);
+
+/* ---- VGA global (GPU) ----------------------------------------------------------------------- */
+/* MetaGraph::analyseGraph(OUTPUT_VISUAL, global) -> VGAVisualGlobal(radius, gates_only).run
+ * (salalib/mgraph.cpp:349-359, vgamodules/vgavisualglobal.cpp:23-216) for source nodes
+ * [src_begin, src_end) (src_end < 0: all).  radius = -1 for "n".  The graph must hold every node
+ * (dmx_graph_assemble_device for shards).  out: host [N][7] or device (dmx_vga_global_device), rows
+ * outside the range untouched, columns in table (alphabetical) order: Visual Entropy, Visual
+ * Integration [HH], [P-value], [Tekl], Visual Mean Depth, Visual Node Count, Visual Relativised
+ * Entropy.  levels (optional, host [N][3]): total nodes, total depth, BFS levels. */
+int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin, int64_t src_end,
+                   float* out, int64_t* levels);
+int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin,
+                          int64_t src_end, float* out_device);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,60 @@
+/* dmx_oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Clean-room CPU restatement (plain C) of the depthmapX VISPREP makeGraph + VGA global path, used
+ * as the parity checker for the MI355X engine and as the "port" CPU baseline in bench.py.  Only
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  Every function
+ * cites the reference file:line it restates (paths relative to orange-vertex/depthmapX).
+ *
+ * Pinned against the real reference: tests/test_oracle_golden.py compares it with the outputs of
+ * oracle/_ref/ref_probe (the reference salalib compiled from source) committed under tests/golden/.
+ */
+#ifndef DMX_ORACLE_H
+#define DMX_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dmxo_map dmxo_map;
+
+/* MetaGraph region + PointMap::setGrid(spacing, (0,0)) (pointdata.cpp:122-171), drawing lines as
+ * blockLines() sees them (pointdata.cpp:308-320). lines: [L][4] = x1,y1,x2,y2. */
+dmxo_map* dmxo_create(const double region[4], double spacing, const double* lines, int64_t nlines);
+void dmxo_free(dmxo_map* m);
+void dmxo_grid_info(const dmxo_map* m, int32_t* cols, int32_t* rows, double* bl_x, double* bl_y);
+
+/* PointMap::makePoints(seed, FULLFILL) (pointdata.cpp:402-481). Returns 1 on success, 0 if the
+ * reference would return false. */
+int dmxo_fill(dmxo_map* m, double x, double y);
+
+/* Per-cell state (x-major, cols*rows) and cropped cell lines (after blockLines). */
+void dmxo_get_state(const dmxo_map* m, int32_t* out);
+int64_t dmxo_cell_lines_count(const dmxo_map* m);
+void dmxo_get_cell_lines(const dmxo_map* m, int32_t* counts /*C*/, double* lines /*[total][4]*/);
+
+/* PointMap::sparkGraph2 (pointdata.cpp:1246-1341) for filled nodes [node_begin, node_end) in
+ * x-major order (node_end < 0: all).  nthreads > 1 runs sources in parallel (OpenMP); results are
+ * identical to the sequential order because each source is independent. */
+int dmxo_makegraph(dmxo_map* m, double maxdist, int boundary, int64_t node_begin, int64_t node_end,
+                   int nthreads);
+int64_t dmxo_num_nodes(const dmxo_map* m);
+int64_t dmxo_num_runs(const dmxo_map* m);
+/* attrs [N][3] (Connectivity, First, Second Moment); bins [N][32][4] (dir, count, dist bits, nruns);
+ * runs [R][4] int16 (x0,y0,x1,y1) in reference order; gridconn [N]. */
+void dmxo_get_graph(const dmxo_map* m, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn);
+/* Replace the graph with externally supplied bins/runs (e.g. a reference dump), same layout. */
+int dmxo_set_graph(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_t nruns);
+
+/* VGAVisualGlobal::run (vgamodules/vgavisualglobal.cpp:23-216) for source nodes
+ * [node_begin, node_end).  out [N][7] in column order: Visual Entropy, Integration [HH],
+ * Integration [P-value], Integration [Tekl], Mean Depth, Node Count, Relativised Entropy
+ * (rows outside the range are left untouched).  levels_out (optional, [N][3]) receives
+ * total_nodes, total_depth, number of levels. */
+int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t node_begin, int64_t node_end,
+                    int nthreads, float* out, int64_t* levels_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,121 @@
+"""ctypes wrapper around oracle/_build/libdmx_oracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libdmx_oracle.so")
+_lib = None
+
+
+def build():
+    """Compile the C restatement (plain gcc; no reference sources involved)."""
+    subprocess.check_call(["make", "-s", "-C", _HERE, "port"])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        vp, i64, i32, dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double
+        L.dmxo_create.restype = vp
+        L.dmxo_create.argtypes = [vp, dbl, vp, i64]
+        L.dmxo_free.argtypes = [vp]
+        L.dmxo_grid_info.argtypes = [vp, vp, vp, vp, vp]
+        L.dmxo_fill.restype = i32
+        L.dmxo_fill.argtypes = [vp, dbl, dbl]
+        L.dmxo_get_state.argtypes = [vp, vp]
+        L.dmxo_cell_lines_count.restype = i64
+        L.dmxo_cell_lines_count.argtypes = [vp]
+        L.dmxo_get_cell_lines.argtypes = [vp, vp, vp]
+        L.dmxo_makegraph.restype = i32
+        L.dmxo_makegraph.argtypes = [vp, dbl, i32, i64, i64, i32]
+        L.dmxo_num_nodes.restype = i64
+        L.dmxo_num_nodes.argtypes = [vp]
+        L.dmxo_num_runs.restype = i64
+        L.dmxo_num_runs.argtypes = [vp]
+        L.dmxo_get_graph.argtypes = [vp, vp, vp, vp, vp]
+        L.dmxo_set_graph.restype = i32
+        L.dmxo_set_graph.argtypes = [vp, vp, vp, i64]
+        L.dmxo_vga_global.restype = i32
+        L.dmxo_vga_global.argtypes = [vp, dbl, i32, i64, i64, i32, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class OracleMap:
+    """CPU restatement of one PointMap: setGrid -> fill -> makeGraph -> VGA global."""
+
+    def __init__(self, region, spacing, lines):
+        L = lib()
+        self._region = np.ascontiguousarray(region, dtype=np.float64)
+        self._lines = np.ascontiguousarray(lines, dtype=np.float64).reshape(-1, 4)
+        self.h = L.dmxo_create(_p(self._region), float(spacing), _p(self._lines), len(self._lines))
+        c, r = ctypes.c_int32(), ctypes.c_int32()
+        bx, by = ctypes.c_double(), ctypes.c_double()
+        L.dmxo_grid_info(self.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(bx), ctypes.byref(by))
+        self.cols, self.rows = c.value, r.value
+        self.bottom_left = (bx.value, by.value)
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().dmxo_free(self.h)
+            self.h = None
+
+    def fill(self, x, y):
+        return bool(lib().dmxo_fill(self.h, float(x), float(y)))
+
+    def state(self):
+        out = np.zeros(self.cols * self.rows, dtype=np.int32)
+        lib().dmxo_get_state(self.h, _p(out))
+        return out
+
+    def cell_lines(self):
+        n = lib().dmxo_cell_lines_count(self.h)
+        counts = np.zeros(self.cols * self.rows, dtype=np.int32)
+        lines = np.zeros((max(n, 1), 4), dtype=np.float64)
+        lib().dmxo_get_cell_lines(self.h, _p(counts), _p(lines))
+        return counts, lines[:n]
+
+    def make_graph(self, maxdist=-1.0, boundary=False, node_begin=0, node_end=-1, threads=1):
+        return lib().dmxo_makegraph(self.h, float(maxdist), int(boundary), node_begin, node_end, threads)
+
+    @property
+    def num_nodes(self):
+        return lib().dmxo_num_nodes(self.h)
+
+    def graph(self):
+        N = self.num_nodes
+        R = lib().dmxo_num_runs(self.h)
+        attrs = np.zeros((N, 3), dtype=np.float32)
+        bins = np.zeros((N, 32, 4), dtype=np.int32)
+        runs = np.zeros((max(R, 1), 4), dtype=np.int16)
+        gc = np.zeros(N, dtype=np.uint8)
+        lib().dmxo_get_graph(self.h, _p(attrs), _p(bins), _p(runs), _p(gc))
+        return dict(attrs=attrs, bins=bins, runs=runs[:R], gridconn=gc)
+
+    def set_graph(self, bins, runs):
+        bins = np.ascontiguousarray(bins, dtype=np.int32)
+        runs = np.ascontiguousarray(runs, dtype=np.int16)
+        rc = lib().dmxo_set_graph(self.h, _p(bins), _p(runs), len(runs))
+        if rc:
+            raise ValueError("bins/runs inconsistent")
+
+    def vga_global(self, radius=-1.0, gates_only=False, node_begin=0, node_end=-1, threads=1, levels=False):
+        N = self.num_nodes
+        out = np.full((N, 7), -1.0, dtype=np.float32)
+        lv = np.zeros((N, 3), dtype=np.int64) if levels else None
+        lib().dmxo_vga_global(self.h, float(radius), int(gates_only), node_begin, node_end, threads, _p(out),
+                              _p(lv) if lv is not None else None)
+        return (out, lv) if levels else out

@@ -1,0 +1,156 @@
+"""GPU parity: the HIP makeGraph / VGA-global path against (a) the golden fixtures produced by the
+real reference (oracle/_ref/ref_probe) and (b) the C restatement (oracle/) on seeded inputs.
+
+Bar: bit-exact for everything integer (states, bins, run lists, node counts, grid connections) and
+for the makeGraph float attributes; VGA float measures within 1e-6 relative (north_star), with the
+bit-exact fraction asserted separately to catch silent drift."""
+import numpy as np
+import pytest
+
+import depthmapx_amd as dmx
+from golden_io import case_input_lines, load_case, node_digests
+
+pytestmark = pytest.mark.gpu
+
+MK_CASES = ["kat", "syn16", "syn32", "gallery", "syn64", "barnsbury", "syn256mk"]
+VGA_CASES = ["kat", "syn16", "syn32", "gallery", "syn64", "barnsbury"]
+VGA_RTOL = 1e-6
+
+
+def _map(meta):
+    pm = dmx.PointMap(meta["region"], case_input_lines(meta), meta["spacing"])
+    for f in meta["fills"]:
+        assert pm.make_points(*f)
+    return pm
+
+
+def _assert_graph_equal(got, A, runs_full):
+    if "bins" in A:
+        np.testing.assert_array_equal(got["bins"], A["bins"])
+    np.testing.assert_array_equal(got["bins"][:, :, 3].sum(axis=1), A["nruns"] if "nruns" in A else A["bins"][:, :, 3].sum(axis=1))
+    np.testing.assert_array_equal(got["attrs"].view(np.uint32), A["attrs"].view(np.uint32))
+    np.testing.assert_array_equal(got["gridconn"], A["gridconn"])
+    if runs_full:
+        np.testing.assert_array_equal(got["runs"], A["runs"])
+    np.testing.assert_array_equal(node_digests(got["bins"], got["runs"]), A["digests"])
+
+
+def _assert_vga_close(got, want):
+    want = want.astype(np.float64)
+    got = got.astype(np.float64)
+    tol = VGA_RTOL * np.maximum(1.0, np.abs(want))
+    bad = np.abs(got - want) > tol
+    assert not bad.any(), "VGA mismatch at %d cells, first %s" % (bad.sum(), np.argwhere(bad)[:5].tolist())
+    return float((got == want).mean())
+
+
+@pytest.mark.parametrize("name", MK_CASES)
+def test_makegraph_matches_reference(ctx, name):
+    try:
+        meta, A = load_case(name)
+    except FileNotFoundError:
+        pytest.skip("fixture not generated")
+    pm = _map(meta)
+    np.testing.assert_array_equal(pm.state(), A["state"])
+    g = pm.make_graph(ctx)
+    info = g.info()
+    assert info["nnodes"] == meta["nodes"]
+    assert info["nruns"] == meta["runs"]
+    got = g.copy(runs=True)
+    _assert_graph_equal(got, A, meta["full_runs"])
+
+
+@pytest.mark.parametrize("name", VGA_CASES)
+def test_vga_global_matches_reference(ctx, name):
+    try:
+        meta, A = load_case(name)
+    except FileNotFoundError:
+        pytest.skip("fixture not generated")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    out = g.vga_visual_global(radius=-1)
+    exact = _assert_vga_close(out, A["vga"])
+    # integer columns (node count) must be bit-exact; floats nearly always are
+    np.testing.assert_array_equal(out[:, 5], A["vga"][:, 5])
+    assert exact > 0.99
+
+
+def test_vga_levels_match_oracle(ctx):
+    from pyoracle import OracleMap
+    meta, A = load_case("syn32")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    out, lv = g.vga_visual_global(levels=True)
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph()
+    ref, rlv = om.vga_global(levels=True)
+    np.testing.assert_array_equal(lv[:, :2], rlv[:, :2])
+    _assert_vga_close(out, ref)
+
+
+@pytest.mark.parametrize("seed", [3, 7, 11])
+def test_random_occluders_match_oracle(ctx, seed):
+    """Seeded random drawings (dense short occluders -> many gaps/blocks per depth)."""
+    from pyoracle import OracleMap
+    from golden.gen_synthetic import make_lines
+    W = 40
+    lines = np.array(make_lines(W, 60, seed=seed, lmin=0.02, lmax=0.3), dtype=np.float64)
+    region = [0.0, 0.0, float(W), float(W)]
+    pm = dmx.PointMap(region, lines, 1.0)
+    om = OracleMap(region, 1.0, lines)
+    assert pm.make_points(0.5, 0.5) == om.fill(0.5, 0.5)
+    np.testing.assert_array_equal(pm.state(), om.state())
+    g = pm.make_graph(ctx)
+    om.make_graph(threads=8)
+    ref = om.graph()
+    got = g.copy(runs=True)
+    np.testing.assert_array_equal(got["bins"], ref["bins"])
+    np.testing.assert_array_equal(got["runs"], ref["runs"])
+    np.testing.assert_array_equal(got["attrs"].view(np.uint32), ref["attrs"].view(np.uint32))
+    np.testing.assert_array_equal(got["gridconn"], ref["gridconn"])
+    _assert_vga_close(g.vga_visual_global(), om.vga_global(threads=8))
+
+
+def test_maxdist_and_radius_match_oracle(ctx):
+    from pyoracle import OracleMap
+    meta, _ = load_case("syn32")
+    lines = case_input_lines(meta)
+    pm = _map(meta)
+    om = OracleMap(meta["region"], meta["spacing"], lines)
+    for f in meta["fills"]:
+        om.fill(*f)
+    g = pm.make_graph(ctx, maxdist=9.5)
+    om.make_graph(maxdist=9.5)
+    ref = om.graph()
+    got = g.copy()
+    np.testing.assert_array_equal(got["bins"], ref["bins"])
+    np.testing.assert_array_equal(got["runs"], ref["runs"])
+    for r in (1, 2, 3):
+        _assert_vga_close(g.vga_visual_global(radius=r), om.vga_global(radius=r))
+
+
+def test_shards_assemble_to_whole_graph(ctx):
+    """Source-range shards (one per rank in multi-GPU runs) reassembled == one-shot graph."""
+    import torch
+    meta, A = load_case("gallery")
+    pm = _map(meta)
+    n = meta["nodes"]
+    cuts = [0, n // 3, (2 * n) // 3, n]
+    shards = [pm.make_graph(ctx, node_begin=cuts[i], node_end=cuts[i + 1]) for i in range(3)]
+    blobs = []
+    for s in shards:
+        t = torch.empty(s.blob_size(), dtype=torch.uint8, device="cuda:0")
+        s.write_blob_device(t.data_ptr(), t.numel())
+        blobs.append(t)
+    torch.cuda.synchronize()
+    g = pm.assemble(ctx, [b.data_ptr() for b in blobs[::-1]], [b.numel() for b in blobs[::-1]])
+    got = g.copy()
+    _assert_graph_equal(got, A, True)
+    out = torch.full((n, 7), -1.0, dtype=torch.float32, device="cuda:0")
+    g.vga_visual_global_device(out.data_ptr(), src_begin=100, src_end=900)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    _assert_vga_close(o[100:900], A["vga"][100:900])
+    assert (o[:100] == -1).all() and (o[900:] == -1).all()
