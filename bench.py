@@ -1,0 +1,241 @@
+#!/usr/bin/env python3
+"""Headline benchmark: grid cells/s for VISPREP makeGraph + VGA global (radius n) on a synthetic
+N x N open-plan grid with 50 random occluders (BASELINE.json metric).
+
+One step = the whole hot path for every filled cell of the grid:
+  makeGraph (sparkGraph2) over this rank's source-cell shard -> [N>1: RCCL all-gather of the
+  run-length graph shards] -> VGA global BFS + measures over this rank's source shard ->
+  [N>1: RCCL all-gather of the 7 float columns].
+Inputs (grid state + occluder pieces) are resident in HBM before the timed region; value =
+filled cells / step time (all ranks), i.e. source cells carried through makeGraph + VGA per
+second.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 256]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def load_lines(W, occluders):
+    p = os.path.join(REPO, "tests", "golden", "inputs", "syn%d.csv" % W)
+    if occluders == 50 and os.path.exists(p):
+        from tests.golden_io import read_csv_lines
+        return read_csv_lines(p)
+    sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+    from gen_synthetic import make_lines
+    return np.array(make_lines(W, occluders, seed=1), dtype=np.float64)
+
+
+def shard_range(n, rank, world):
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+def load_traffic(workload):
+    """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/pmc_traffic.json)."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get(workload)
+    except Exception:
+        return None
+
+
+def cpu_baseline(region, lines, spacing, fill, graph_np, budget_s):
+    """The C restatement (oracle/, bit-exact vs the reference) timed single-threaded on a bounded
+    sample of the same workload: makeGraph on a contiguous block of sources, then VGA global BFS
+    on a block of sources over the full graph (imported from the GPU result, identical bits)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from pyoracle import OracleMap
+    om = OracleMap(region, spacing, lines)
+    om.fill(*fill)
+    N = graph_np["bins"].shape[0]
+    mid = N // 2
+    # makeGraph sample: grow until ~40% of the budget
+    k, t_mk = 8, 0.0
+    while True:
+        t0 = time.perf_counter()
+        om.make_graph(node_begin=mid, node_end=min(N, mid + k), threads=1)
+        t_mk = time.perf_counter() - t0
+        if t_mk > 0.4 * budget_s or mid + k >= N:
+            break
+        k = min(N - mid, max(k * 2, int(k * 0.4 * budget_s / max(t_mk, 1e-3))))
+    mk_per_src = t_mk / min(k, N - mid)
+    om.set_graph(graph_np["bins"], graph_np["runs"])
+    kv, t_v = 1, 0.0
+    while True:
+        t0 = time.perf_counter()
+        om.vga_global(node_begin=mid, node_end=min(N, mid + kv), threads=1)
+        t_v = time.perf_counter() - t0
+        if t_v > 0.4 * budget_s or mid + kv >= N:
+            break
+        kv = min(N - mid, max(kv * 2, int(kv * 0.4 * budget_s / max(t_v, 1e-3))))
+    vga_per_src = t_v / min(kv, N - mid)
+    value = 1.0 / (mk_per_src + vga_per_src)
+    return {"value": value, "unit": "cells/s", "cores": 1, "kind": "port",
+            "sample": "oracle/dmx_oracle.c single thread: makeGraph on %d sources (%.2f s) + VGA global BFS "
+                      "on %d sources (%.2f s) from node %d; per-source times extrapolated to cells/s"
+                      % (min(k, N - mid), t_mk, min(kv, N - mid), t_v, mid),
+            "makegraph_s_per_source": mk_per_src, "vga_s_per_source": vga_per_src}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--grid", type=int, default=256, help="W: region [0,W]^2 at spacing 1 -> (W+1)^2 cells")
+    ap.add_argument("--occluders", type=int, default=50)
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline sampling")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import depthmapx_amd as dmx
+
+    W = args.grid
+    lines = load_lines(W, args.occluders)
+    region = [0.0, 0.0, float(W), float(W)]
+    fill = (0.5, 0.5)
+    ctx = dmx.Context(local)
+    pm = dmx.PointMap(region, lines, 1.0)
+    assert pm.make_points(*fill)
+    info = pm.info()
+    N = info["filled"]
+    b, e = shard_range(N, rank, world)
+    workload = "synthetic-%d/%d-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + VGA -vm visibility -vg -vr n" % (
+        W, args.occluders)
+
+    out_full = torch.full((N, 7), -1.0, dtype=torch.float32, device=dev)
+    kt = {"makegraph_s": 0.0, "vga_s": 0.0, "n": 0}
+    stats = {}
+
+    def step(record):
+        shard = pm.make_graph(ctx, node_begin=b, node_end=e)
+        t_mk = ctx.last_timing()[0]
+        st = dict(ctx.last_stats())
+        if world > 1:
+            sz = torch.tensor([shard.blob_size()], dtype=torch.int64, device=dev)
+            sizes = [torch.zeros_like(sz) for _ in range(world)]
+            dist.all_gather(sizes, sz)
+            mx = int(max(int(s.item()) for s in sizes))
+            mine = torch.zeros(mx, dtype=torch.uint8, device=dev)
+            shard.write_blob_device(mine.data_ptr(), mx)
+            allb = torch.empty(world * mx, dtype=torch.uint8, device=dev)
+            dist.all_gather_into_tensor(allb, mine)
+            torch.cuda.synchronize()
+            ptrs = [allb.data_ptr() + i * mx for i in range(world)]
+            g = pm.assemble(ctx, ptrs, [int(s.item()) for s in sizes])
+            del allb, mine
+        else:
+            g = shard
+        g.vga_visual_global_device(out_full.data_ptr(), src_begin=b, src_end=e)
+        t_vga = ctx.last_timing()[1]
+        st.update({k: v for k, v in ctx.last_stats().items() if k.startswith("vga")})
+        if world > 1:
+            per = (N + world - 1) // world
+            mine = torch.zeros((per, 7), dtype=torch.float32, device=dev)
+            mine[: e - b] = out_full[b:e]
+            gathered = torch.empty((world * per, 7), dtype=torch.float32, device=dev)
+            dist.all_gather_into_tensor(gathered, mine)
+            for r in range(world):
+                rb, re_ = shard_range(N, r, world)
+                out_full[rb:re_] = gathered[r * per: r * per + (re_ - rb)]
+        if record:
+            kt["makegraph_s"] += t_mk
+            kt["vga_s"] += t_vga
+            kt["n"] += 1
+            stats.update(st)
+        return g
+
+    for _ in range(args.warmup):
+        g = step(False)
+        del g
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g = step(True)
+        if _ != args.steps - 1:
+            del g
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    if rank == 0:
+        steps = max(args.steps, 1)
+        mk_s = kt["makegraph_s"] / max(kt["n"], 1)
+        vga_s = kt["vga_s"] / max(kt["n"], 1)
+        nr_shard = stats.get("mk_runs", 0)
+        # algorithmic bytes (DESIGN.md "Roofline accounting"), per launch on this rank
+        tw, th = (info["cols"] + 7) // 8, (info["rows"] + 7) // 8
+        nsrc = e - b
+        mk_bytes = 8 * nr_shard + 4 * stats.get("mk_cells_examined", 0)
+        vga_bytes = 8 * stats.get("vga_runs_expanded", 0) + 8 * tw * th * nsrc + 8 * stats.get("vga_cells_reached", 0)
+        dominant = "vga_global_kernel" if vga_s >= mk_s else "makegraph_kernel"
+        dom_bytes, dom_s = (vga_bytes, vga_s) if vga_s >= mk_s else (mk_bytes, mk_s)
+        achieved = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
+        traffic = load_traffic(workload)
+        tr = traffic.get(dominant) if isinstance(traffic, dict) else None
+        rec = {
+            "metric": "grid cells/sec for VISPREP makeGraph + VGA global on N×N grid",
+            "value": N * steps / elapsed,
+            "unit": "cells/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (committed occluder CSV, seed 1)",
+            "config": {"workload": workload, "grid": "%dx%d" % (info["cols"], info["rows"]), "filled_cells": N,
+                       "runs": int(g.info()["nruns"]), "parallelism": "source-shard x%d" % world},
+            "kernels": {"makegraph_s": mk_s, "vga_s": vga_s,
+                        "makegraph_cells_per_s": nsrc / mk_s if mk_s else None,
+                        "visible_pairs": stats.get("mk_visible_pairs"),
+                        "vga_runs_read": stats.get("vga_runs_expanded"),
+                        "vga_kernel": stats.get("vga_kernel"),
+                        "vga_levels_bottom_up": stats.get("vga_bottom_up_levels"),
+                        "vga_levels_top_down": stats.get("vga_top_down_levels"),
+                        "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc},
+            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": tr},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            gn = g.copy(runs=True)
+            rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, gn, args.cpu_budget)
+            rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

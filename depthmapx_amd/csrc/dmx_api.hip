@@ -19,6 +19,7 @@
 #include "host/pointmap.hpp"
 #include "kernels/makegraph.hip"
 #include "kernels/vga.hip"
+#include "kernels/vga_do.hip"
 
 using namespace dmx;
 
@@ -77,6 +78,7 @@ struct dmx_pointmap {
     DevBuf<int32_t> d_cell_node;
     DevBuf<uint8_t> d_node_flags;
     DevBuf<unsigned long long> d_seed_tiles;
+    DevBuf<unsigned long long> d_nonexp_tiles;  // contextfilled cells with odd x or y
 };
 
 struct dmx_graph {
@@ -94,7 +96,12 @@ struct dmx_graph {
     DevBuf<uint8_t> gridconn;
     // VGA early-exit universe
     DevBuf<unsigned long long> uf_tiles;
+    DevBuf<unsigned long long> notuf_tiles;
     int64_t uf_count = -1;
+    int64_t r_universe = 0;
+    int symmetric = -1;   // -1 unknown, 0 top-down only, 1 bottom-up allowed (with corrections)
+    int nspecial = 0;
+    DevBuf<int32_t> spec_index, extra_off, extra, missing_off, missing;
 };
 
 namespace {
@@ -125,11 +132,14 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     pm->nnodes = (int64_t)pm->node_cell.size();
     // seed bitmap for the BFS: 1 = not a filled cell (or padding), 8x8 tiles
     const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
-    std::vector<unsigned long long> seed((size_t)tw * th, ~0ull);
+    std::vector<unsigned long long> seed((size_t)tw * th, ~0ull), nonexp((size_t)tw * th, 0ull);
     for (int x = 0; x < h.cols(); x++)
-        for (int y = 0; y < h.rows(); y++)
-            if (st[h.index(x, y)] & CELL_FILLED)
-                seed[(size_t)(y >> 3) * tw + (x >> 3)] &= ~(1ull << ((y & 7) * 8 + (x & 7)));
+        for (int y = 0; y < h.rows(); y++) {
+            const int32_t sv = st[h.index(x, y)];
+            const unsigned long long bit = 1ull << ((y & 7) * 8 + (x & 7));
+            if (sv & CELL_FILLED) seed[(size_t)(y >> 3) * tw + (x >> 3)] &= ~bit;
+            if ((sv & CELL_CONTEXTFILLED) && !((x % 2) == 0 && (y % 2) == 0)) nonexp[(size_t)(y >> 3) * tw + (x >> 3)] |= bit;
+        }
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(pm->d_cellw.alloc(C));
     HIPCHK(pm->d_segs.alloc(std::max<size_t>(h.segs().size(), 4)));
@@ -137,6 +147,8 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     HIPCHK(pm->d_cell_node.alloc(C));
     HIPCHK(pm->d_node_flags.alloc(std::max<int64_t>(pm->nnodes, 1)));
     HIPCHK(pm->d_seed_tiles.alloc(seed.size()));
+    HIPCHK(pm->d_nonexp_tiles.alloc(nonexp.size()));
+    HIPCHK(hipMemcpyAsync(pm->d_nonexp_tiles.p, nonexp.data(), nonexp.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(pm->d_cellw.p, cellw.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
     if (!h.segs().empty())
         HIPCHK(hipMemcpyAsync(pm->d_segs.p, h.segs().data(), h.segs().size() * 8, hipMemcpyHostToDevice, ctx->stream));
@@ -619,12 +631,127 @@ static int prepare_uf(dmx_graph* g) {
     HIPCHK(hipMemcpyAsync(seed.data(), g->pm->d_seed_tiles.p, seed.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     int64_t cnt = 0;
+    std::vector<unsigned long long> notuf(uf.size());
     for (size_t i = 0; i < uf.size(); i++) {
         uf[i] &= ~seed[i];
+        notuf[i] = ~uf[i];
         cnt += __builtin_popcountll(uf[i]);
     }
     HIPCHK(hipMemcpy(g->uf_tiles.p, uf.data(), uf.size() * 8, hipMemcpyHostToDevice));
+    HIPCHK(g->notuf_tiles.alloc(uf.size()));
+    HIPCHK(hipMemcpy(g->notuf_tiles.p, notuf.data(), notuf.size() * 8, hipMemcpyHostToDevice));
     g->uf_count = cnt;
+    // run mass of the discoverable universe
+    std::vector<int32_t> nr((size_t)std::max<int64_t>(g->nnodes, 1));
+    if (g->nnodes) HIPCHK(hipMemcpy(nr.data(), g->node_nruns.p, g->nnodes * 4, hipMemcpyDeviceToHost));
+    int64_t ru = 0;
+    for (int64_t k = 0; k < g->nnodes; k++) {
+        const int c = g->pm->node_cell[k];
+        const int x = c / h.rows(), y = c % h.rows();
+        if (uf[(size_t)(y >> 3) * tw + (x >> 3)] & (1ull << ((y & 7) * 8 + (x & 7)))) ru += nr[k];
+    }
+    g->r_universe = ru;
+    return DMX_OK;
+}
+
+// In-set corrections for bottom-up BFS (vga_do.hip, "symmetry / in-set corrections").
+static int prepare_symmetry(dmx_graph* g) {
+    if (g->symmetric >= 0) return DMX_OK;
+    const char* force = getenv("DMX_VGA_KERNEL");
+    if (force && std::string(force) == "topdown") { g->symmetric = 0; return DMX_OK; }
+    dmx_ctx* ctx = g->ctx;
+    hipStream_t s = ctx->stream;
+    PointMapHost& h = *g->pm->host;
+    const int cols = h.cols(), rows = h.rows();
+    const int64_t C = (int64_t)cols * rows, N = g->nnodes;
+    const int kSpecLimit = 4096;
+    DevBuf<unsigned long long> prefix, diff, ho;
+    DevBuf<int32_t> flist;
+    DevBuf<int> fcount;
+    HIPCHK(prefix.alloc((size_t)4 * C));
+    HIPCHK(diff.alloc((size_t)4 * C));
+    HIPCHK(ho.alloc(std::max<int64_t>(N, 1)));
+    HIPCHK(flist.alloc(kSpecLimit));
+    HIPCHK(fcount.alloc(1));
+    HIPCHK(hipMemsetAsync(diff.p, 0, (size_t)4 * C * 8, s));
+    HIPCHK(hipMemsetAsync(fcount.p, 0, 4, s));
+    const int maxlines = cols + rows;
+    hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
+                       g->pm->d_cell_node.p, prefix.p, 0);
+    HIPCHK(hipGetLastError());
+    if (N) {
+        hipLaunchKernelGGL(sym_scatter_kernel, dim3((unsigned)std::min<int64_t>(N, 4096)), dim3(256), 0, s, cols, rows,
+                           g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, prefix.p, diff.p,
+                           ho.p);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
+                       g->pm->d_cell_node.p, diff.p, 1);
+    HIPCHK(hipGetLastError());
+    if (N) {
+        hipLaunchKernelGGL(sym_flag_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rows,
+                           g->pm->d_node_cell.p, N, C, diff.p, ho.p, fcount.p, flist.p, kSpecLimit);
+        HIPCHK(hipGetLastError());
+    }
+    int nspec = 0;
+    HIPCHK(hipMemcpyAsync(&nspec, fcount.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    g->nspecial = nspec;
+    if (nspec == 0) { g->symmetric = 1; return DMX_OK; }
+    if (nspec > kSpecLimit) { g->symmetric = 0; return DMX_OK; }
+    std::vector<int32_t> specs((size_t)nspec);
+    HIPCHK(hipMemcpy(specs.data(), flist.p, nspec * 4, hipMemcpyDeviceToHost));
+    std::sort(specs.begin(), specs.end());
+    std::vector<uint8_t> is_spec((size_t)N, 0);
+    std::vector<int32_t> sidx((size_t)N, -1);
+    for (int i = 0; i < nspec; i++) { is_spec[specs[i]] = 1; sidx[specs[i]] = i; }
+    DevBuf<uint8_t> d_is;
+    DevBuf<int32_t> d_specs, d_out;
+    DevBuf<int> d_outn;
+    HIPCHK(d_is.alloc(N));
+    HIPCHK(d_specs.alloc(nspec));
+    HIPCHK(d_out.alloc((size_t)nspec * nspec));
+    HIPCHK(d_outn.alloc(nspec));
+    HIPCHK(hipMemcpy(d_is.p, is_spec.data(), N, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(d_specs.p, specs.data(), nspec * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemset(d_outn.p, 0, nspec * 4));
+    hipLaunchKernelGGL(sym_special_out_kernel, dim3(nspec), dim3(256), 0, s, rows, d_specs.p, nspec,
+                       g->pm->d_node_cell.p, g->pm->d_cell_node.p, d_is.p, g->node_run_start.p, g->node_nruns.p,
+                       g->pool.p, d_out.p, d_outn.p, nspec);
+    HIPCHK(hipGetLastError());
+    std::vector<int32_t> outn((size_t)nspec), out((size_t)nspec * nspec);
+    HIPCHK(hipMemcpyAsync(outn.data(), d_outn.p, nspec * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(out.data(), d_out.p, (size_t)nspec * nspec * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    // A[a][b] = b in cells(a), over special nodes (asymmetric pairs only involve special nodes)
+    std::vector<std::vector<char>> A((size_t)nspec, std::vector<char>((size_t)nspec, 0));
+    for (int a = 0; a < nspec; a++)
+        for (int j = 0; j < std::min(outn[a], nspec); j++) A[a][sidx[out[(size_t)a * nspec + j]]] = 1;
+    std::vector<std::vector<int32_t>> extra((size_t)nspec), missing((size_t)nspec);
+    for (int a = 0; a < nspec; a++)
+        for (int b = 0; b < nspec; b++)
+            if (A[a][b] && !A[b][a]) {          // b in cells(a), a not in cells(b)
+                extra[b].push_back(specs[a]);   // a is an in-neighbour of b outside cells(b)
+                missing[a].push_back(specs[b]); // b sits in cells(a) but is not an in-neighbour of a
+            }
+    std::vector<int32_t> eoff(1, 0), moff(1, 0), ev, mv;
+    for (int i = 0; i < nspec; i++) {
+        ev.insert(ev.end(), extra[i].begin(), extra[i].end());
+        mv.insert(mv.end(), missing[i].begin(), missing[i].end());
+        eoff.push_back((int32_t)ev.size());
+        moff.push_back((int32_t)mv.size());
+    }
+    HIPCHK(g->spec_index.alloc(N));
+    HIPCHK(g->extra_off.alloc(eoff.size()));
+    HIPCHK(g->missing_off.alloc(moff.size()));
+    HIPCHK(g->extra.alloc(std::max<size_t>(ev.size(), 1)));
+    HIPCHK(g->missing.alloc(std::max<size_t>(mv.size(), 1)));
+    HIPCHK(hipMemcpy(g->spec_index.p, sidx.data(), N * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g->extra_off.p, eoff.data(), eoff.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(g->missing_off.p, moff.data(), moff.size() * 4, hipMemcpyHostToDevice));
+    if (!ev.empty()) HIPCHK(hipMemcpy(g->extra.p, ev.data(), ev.size() * 4, hipMemcpyHostToDevice));
+    if (!mv.empty()) HIPCHK(hipMemcpy(g->missing.p, mv.data(), mv.size() * 4, hipMemcpyHostToDevice));
+    g->symmetric = 1;
     return DMX_OK;
 }
 
@@ -639,13 +766,19 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     if (sb < 0 || sb > se) return fail(DMX_ERR_ARG, "bad source range");
     int rc = prepare_uf(g);
     if (rc) return rc;
+    rc = prepare_symmetry(g);
+    if (rc) return rc;
     PointMapHost& h = *g->pm->host;
     const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
     const int maxlev = 4096;
-    const size_t lds = (size_t)tw * th * 8 + (maxlev + 4) * 4 + 64;
+    const size_t lds_do = (size_t)tw * th * 8 * 3 + (maxlev + 4) * 4 + 64;
+    const char* force = getenv("DMX_VGA_KERNEL");
+    const bool use_do = lds_do <= 160 * 1024 && !(force && std::string(force) == "v1");
+    const size_t lds = use_do ? lds_do : (size_t)tw * th * 8 + (maxlev + 4) * 4 + 64;
     if (lds > 160 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the LDS visited bitmap (v1 limit)");
     int occ = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_global_kernel, VGA_THREADS, lds));
+    if (use_do) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_do_kernel, DO_THREADS, lds));
+    else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_global_kernel, VGA_THREADS, lds));
     if (occ < 1) occ = 1;
     const int64_t nsrc = se - sb;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cu * occ, nsrc));
@@ -671,9 +804,28 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     P.frontier = frontier.p; P.nnodes = N; P.maxlev = maxlev;
     P.out = outp; P.levels_out = levels ? d_lv.p : nullptr;
     P.stats = ctx->stats.p;
+    VgaDoParams Q;
+    Q.cols = h.cols(); Q.rows = h.rows(); Q.tw = tw; Q.th = th;
+    Q.seed_tiles = g->notuf_tiles.p; Q.uf_tiles = g->uf_tiles.p; Q.nonexp_tiles = g->pm->d_nonexp_tiles.p;
+    Q.node_cell = P.node_cell; Q.cell_node = P.cell_node; Q.node_flags = P.node_flags;
+    Q.node_run_start = P.node_run_start; Q.node_nruns = P.node_nruns; Q.pool = P.pool;
+    Q.src_begin = sb; Q.src_end = se; Q.radius = P.radius; Q.gates_only = gates_only;
+    Q.uf_count = g->uf_count; Q.r_universe = g->r_universe; Q.symmetric = g->symmetric;
+    const bool corr = g->symmetric == 1 && g->nspecial > 0;
+    Q.spec_index = corr ? g->spec_index.p : nullptr;
+    Q.extra_off = corr ? g->extra_off.p : nullptr;
+    Q.extra = corr ? g->extra.p : nullptr;
+    Q.missing_off = corr ? g->missing_off.p : nullptr;
+    Q.missing = corr ? g->missing.p : nullptr;
+    Q.alpha = 15; Q.kshort = 16;
+    if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
+    if (const char* k = getenv("DMX_VGA_KSHORT")) Q.kshort = atoi(k);
+    Q.work_counter = P.work_counter; Q.scratch = frontier.p; Q.nnodes = N; Q.maxlev = maxlev;
+    Q.out = outp; Q.levels_out = P.levels_out; Q.error = P.error; Q.stats = P.stats;
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (nsrc > 0) {
-        hipLaunchKernelGGL(vga_global_kernel, dim3((unsigned)blocks), dim3(VGA_THREADS), lds, ctx->stream, P);
+        if (use_do) hipLaunchKernelGGL(vga_do_kernel, dim3((unsigned)blocks), dim3(DO_THREADS), lds, ctx->stream, Q);
+        else hipLaunchKernelGGL(vga_global_kernel, dim3((unsigned)blocks), dim3(VGA_THREADS), lds, ctx->stream, P);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
@@ -684,10 +836,11 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     int hc[2];
     HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level/frontier capacity");
-    unsigned long long st[3];
+    unsigned long long st[5];
     HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+    ctx->last_stats[3] = (long long)(use_do ? (g->symmetric ? 2 : 1) : 0) | ((long long)g->nspecial << 8);
     ctx->last_stats[4] = (long long)st[0];
-    ctx->last_stats[5] = (long long)st[1];
+    ctx->last_stats[5] = (long long)(st[3] | (st[4] << 32));                 // bottom-up | top-down levels
     ctx->last_stats[6] = (long long)st[2];
     ctx->last_stats[7] = nsrc;
     if (!out_on_device && nsrc > 0)

@@ -44,9 +44,15 @@ class Context:
     def last_stats(self):
         out = np.zeros(8, dtype=np.int64)
         N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 8))
-        keys = ["mk_cells_examined", "mk_visible_pairs", "mk_runs", "", "vga_runs_expanded", "", "vga_cells_reached",
-                "vga_sources"]
-        return {k: int(v) for k, v in zip(keys, out) if k}
+        keys = ["mk_cells_examined", "mk_visible_pairs", "mk_runs", "vga_kernel", "vga_runs_expanded", "vga_levels",
+                "vga_cells_reached", "vga_sources"]
+        d = {k: int(v) for k, v in zip(keys, out)}
+        lv = d.pop("vga_levels")
+        d["vga_bottom_up_levels"], d["vga_top_down_levels"] = lv & 0xFFFFFFFF, lv >> 32
+        d["vga_special_nodes"] = d["vga_kernel"] >> 8
+        d["vga_kernel"] = ["topdown-v1", "direction-optimizing(top-down only)",
+                           "direction-optimizing"][d["vga_kernel"] & 0xFF]
+        return d
 
 
 class PointMap:

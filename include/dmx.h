@@ -46,8 +46,11 @@ int dmx_ctx_free(dmx_ctx* ctx);
  * context stream (seconds); kernel_ms receives per-kernel averages. */
 int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
 /* Work counters of the last calls (for roofline accounting): [0] sieve cells examined,
- * [1] visible (source,target) pairs, [2] runs written, [4] runs expanded by the BFS,
- * [5] reserved, [6] cells reached (sum over sources), [7] sources run. */
+ * [1] visible (source,target) pairs, [2] runs written, [3] VGA kernel used (0 top-down v1,
+ * 1 direction-optimising restricted to top-down, 2 direction-optimising) | nodes needing exact
+ * in-set corrections << 8, [4] runs read by the
+ * BFS, [5] bottom-up levels | top-down levels << 32, [6] cells reached (sum over sources),
+ * [7] sources run. */
 int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
 
 /* ---- VISPREP preparation (host model) ----------------------------------------------------- */

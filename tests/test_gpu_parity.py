@@ -154,3 +154,42 @@ def test_shards_assemble_to_whole_graph(ctx):
     o = out.cpu().numpy()
     _assert_vga_close(o[100:900], A["vga"][100:900])
     assert (o[:100] == -1).all() and (o[900:] == -1).all()
+
+
+@pytest.mark.parametrize("kernel", ["v1", "topdown"])
+def test_vga_kernels_agree(ctx, kernel, monkeypatch):
+    """The direction-optimising BFS, its top-down-only mode and the v1 top-down kernel agree
+    bit-for-bit (levels and measures)."""
+    meta, A = load_case("gallery")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    out_do, lv_do = g.vga_visual_global(levels=True)
+    assert ctx.last_stats()["vga_kernel"] == "direction-optimizing"
+    monkeypatch.setenv("DMX_VGA_KERNEL", kernel)
+    g2 = pm.make_graph(ctx)
+    out2, lv2 = g2.vga_visual_global(levels=True)
+    np.testing.assert_array_equal(lv_do, lv2)
+    np.testing.assert_array_equal(out_do.view(np.uint32), out2.view(np.uint32))
+
+
+def test_vga_asymmetric_graph_corrections(ctx, monkeypatch):
+    """syn256 has 2 asymmetric visibility pairs (found by an exhaustive check): the bottom-up BFS
+    must route the 4 nodes involved through exact in-set corrections and still agree bit-for-bit
+    with the pure top-down kernel on sources around them."""
+    lines = np.loadtxt(__import__("os").path.join(__import__("golden_io").GOLDEN, "inputs", "syn256.csv"),
+                       delimiter=",", skiprows=1)
+    pm = dmx.PointMap([0.0, 0.0, 256.0, 256.0], lines, 1.0)
+    assert pm.make_points(0.5, 0.5)
+    g = pm.make_graph(ctx)
+    ranges = [(21900, 22100), (34000, 34200), (48050, 48200)]
+    outs = []
+    for (b, e) in ranges:
+        outs.append(g.vga_visual_global(src_begin=b, src_end=e, levels=True))
+    st = ctx.last_stats()
+    assert st["vga_kernel"] == "direction-optimizing" and st["vga_special_nodes"] == 4
+    monkeypatch.setenv("DMX_VGA_KERNEL", "v1")
+    g2 = pm.make_graph(ctx)
+    for (b, e), (o, lv) in zip(ranges, outs):
+        o2, lv2 = g2.vga_visual_global(src_begin=b, src_end=e, levels=True)
+        np.testing.assert_array_equal(lv[b:e], lv2[b:e])
+        np.testing.assert_array_equal(o[b:e].view(np.uint32), o2[b:e].view(np.uint32))
