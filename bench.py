@@ -37,10 +37,6 @@ def load_lines(W, occluders):
     return np.array(make_lines(W, occluders, seed=1), dtype=np.float64)
 
 
-def shard_range(n, rank, world):
-    return (n * rank) // world, (n * (rank + 1)) // world
-
-
 def load_traffic(workload):
     """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/pmc_traffic.json)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -111,6 +107,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     import depthmapx_amd as dmx
+    from depthmapx_amd.sharded import allgather_blobs, allgather_rows, shard_range
 
     W = args.grid
     lines = load_lines(W, args.occluders)
@@ -130,36 +127,27 @@ def main():
     stats = {}
 
     def step(record):
+        # 1. makeGraph for this rank's sources
         shard = pm.make_graph(ctx, node_begin=b, node_end=e)
         t_mk = ctx.last_timing()[0]
         st = dict(ctx.last_stats())
         if world > 1:
-            sz = torch.tensor([shard.blob_size()], dtype=torch.int64, device=dev)
-            sizes = [torch.zeros_like(sz) for _ in range(world)]
-            dist.all_gather(sizes, sz)
-            mx = int(max(int(s.item()) for s in sizes))
-            mine = torch.zeros(mx, dtype=torch.uint8, device=dev)
-            shard.write_blob_device(mine.data_ptr(), mx)
-            allb = torch.empty(world * mx, dtype=torch.uint8, device=dev)
-            dist.all_gather_into_tensor(allb, mine)
+            # 2. all-gather the run-length graph shards (RCCL), assemble the whole graph
+            blob = torch.empty(shard.blob_size(), dtype=torch.uint8, device=dev)
+            shard.write_blob_device(blob.data_ptr(), blob.numel())
+            flat, mx, sizes = allgather_blobs(blob, dist)
             torch.cuda.synchronize()
-            ptrs = [allb.data_ptr() + i * mx for i in range(world)]
-            g = pm.assemble(ctx, ptrs, [int(s.item()) for s in sizes])
-            del allb, mine
+            g = pm.assemble(ctx, [flat.data_ptr() + i * mx for i in range(world)], sizes)
+            del flat, blob
         else:
             g = shard
+        # 3. VGA global for this rank's sources
         g.vga_visual_global_device(out_full.data_ptr(), src_begin=b, src_end=e)
         t_vga = ctx.last_timing()[1]
         st.update({k: v for k, v in ctx.last_stats().items() if k.startswith("vga")})
+        # 4. all-gather the 7 float columns
         if world > 1:
-            per = (N + world - 1) // world
-            mine = torch.zeros((per, 7), dtype=torch.float32, device=dev)
-            mine[: e - b] = out_full[b:e]
-            gathered = torch.empty((world * per, 7), dtype=torch.float32, device=dev)
-            dist.all_gather_into_tensor(gathered, mine)
-            for r in range(world):
-                rb, re_ = shard_range(N, r, world)
-                out_full[rb:re_] = gathered[r * per: r * per + (re_ - rb)]
+            allgather_rows(out_full, N, dist)
         if record:
             kt["makegraph_s"] += t_mk
             kt["vga_s"] += t_vga

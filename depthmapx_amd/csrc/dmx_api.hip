@@ -98,7 +98,10 @@ struct dmx_graph {
     DevBuf<unsigned long long> uf_tiles;
     DevBuf<unsigned long long> notuf_tiles;
     int64_t uf_count = -1;
-    int64_t r_universe = 0;
+    // bottom-up scan order: runs of each node longest-first, indexed by cell
+    DevBuf<Run> scan_pool;
+    DevBuf<int64_t> cell_scan_start;
+    DevBuf<int32_t> cell_nruns;
     int symmetric = -1;   // -1 unknown, 0 top-down only, 1 bottom-up allowed (with corrections)
     int nspecial = 0;
     DevBuf<int32_t> spec_index, extra_off, extra, missing_off, missing;
@@ -615,42 +618,58 @@ int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const*
 }
 
 // ---------------------------------------------------------------- VGA global
+// U_f (filled cells that appear in some run: the early-exit universe of every BFS) by range counts,
+// plus the longest-first scan pool.  O(runs) with a few line-prefix passes.
 static int prepare_uf(dmx_graph* g) {
     if (g->uf_count >= 0) return DMX_OK;
     dmx_ctx* ctx = g->ctx;
+    hipStream_t s = ctx->stream;
     PointMapHost& h = *g->pm->host;
-    const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
+    const int cols = h.cols(), rows = h.rows();
+    const int tw = (cols + 7) / 8, th = (rows + 7) / 8;
+    const int64_t C = (int64_t)cols * rows, N = g->nnodes;
+    DevBuf<int> cov;
+    DevBuf<unsigned long long> cnt;
+    HIPCHK(cov.alloc((size_t)4 * C));
+    HIPCHK(cnt.alloc(1));
     HIPCHK(g->uf_tiles.alloc((size_t)tw * th));
-    HIPCHK(hipMemsetAsync(g->uf_tiles.p, 0, (size_t)tw * th * 8, ctx->stream));
-    if (g->nnodes)
-        hipLaunchKernelGGL(mark_runs_kernel, dim3((unsigned)g->nnodes), dim3(64), 0, ctx->stream, tw,
-                           g->node_run_start.p, g->node_nruns.p, g->pool.p, g->nnodes, g->uf_tiles.p);
+    HIPCHK(g->notuf_tiles.alloc((size_t)tw * th));
+    HIPCHK(hipMemsetAsync(cov.p, 0, (size_t)4 * C * 4, s));
+    HIPCHK(hipMemsetAsync(cnt.p, 0, 8, s));
+    if (N) {
+        hipLaunchKernelGGL(cov_scatter_kernel, dim3((unsigned)std::min<int64_t>(N, 4096)), dim3(256), 0, s, cols, rows, N,
+                           g->node_run_start.p, g->node_nruns.p, g->pool.p, cov.p);
+        HIPCHK(hipGetLastError());
+    }
+    hipLaunchKernelGGL(cov_lines_kernel, dim3((cols + rows + 127) / 128, 4), dim3(128), 0, s, cols, rows, cov.p);
     HIPCHK(hipGetLastError());
-    std::vector<unsigned long long> uf((size_t)tw * th), seed((size_t)tw * th);
-    HIPCHK(hipMemcpyAsync(uf.data(), g->uf_tiles.p, uf.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(seed.data(), g->pm->d_seed_tiles.p, seed.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    int64_t cnt = 0;
-    std::vector<unsigned long long> notuf(uf.size());
-    for (size_t i = 0; i < uf.size(); i++) {
-        uf[i] &= ~seed[i];
-        notuf[i] = ~uf[i];
-        cnt += __builtin_popcountll(uf[i]);
+    hipLaunchKernelGGL(cov_tiles_kernel, dim3((tw * th + 255) / 256), dim3(256), 0, s, cols, rows, tw, th,
+                       g->pm->d_cell_node.p, cov.p, g->uf_tiles.p, g->notuf_tiles.p, cnt.p);
+    HIPCHK(hipGetLastError());
+    // scan pool (node order, runs longest-first inside each node)
+    std::vector<int32_t> nr((size_t)std::max<int64_t>(N, 1));
+    if (N) HIPCHK(hipMemcpyAsync(nr.data(), g->node_nruns.p, N * 4, hipMemcpyDeviceToHost, s));
+    unsigned long long ufc = 0;
+    HIPCHK(hipMemcpyAsync(&ufc, cnt.p, 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    std::vector<int64_t> ss((size_t)std::max<int64_t>(N, 1));
+    int64_t acc = 0;
+    for (int64_t k = 0; k < N; k++) { ss[k] = acc; acc += nr[k]; }
+    DevBuf<int64_t> d_ss;
+    HIPCHK(d_ss.alloc(std::max<int64_t>(N, 1)));
+    HIPCHK(g->scan_pool.alloc(std::max<int64_t>(acc, 1)));
+    HIPCHK(g->cell_scan_start.alloc(C));
+    HIPCHK(g->cell_nruns.alloc(C));
+    HIPCHK(hipMemsetAsync(g->cell_nruns.p, 0, C * 4, s));
+    if (N) {
+        HIPCHK(hipMemcpyAsync(d_ss.p, ss.data(), N * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(scan_pool_kernel, dim3((unsigned)std::min<int64_t>(N, 8192)), dim3(256), 0, s, rows,
+                           g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, d_ss.p,
+                           g->scan_pool.p, g->cell_scan_start.p, g->cell_nruns.p);
+        HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipMemcpy(g->uf_tiles.p, uf.data(), uf.size() * 8, hipMemcpyHostToDevice));
-    HIPCHK(g->notuf_tiles.alloc(uf.size()));
-    HIPCHK(hipMemcpy(g->notuf_tiles.p, notuf.data(), notuf.size() * 8, hipMemcpyHostToDevice));
-    g->uf_count = cnt;
-    // run mass of the discoverable universe
-    std::vector<int32_t> nr((size_t)std::max<int64_t>(g->nnodes, 1));
-    if (g->nnodes) HIPCHK(hipMemcpy(nr.data(), g->node_nruns.p, g->nnodes * 4, hipMemcpyDeviceToHost));
-    int64_t ru = 0;
-    for (int64_t k = 0; k < g->nnodes; k++) {
-        const int c = g->pm->node_cell[k];
-        const int x = c / h.rows(), y = c % h.rows();
-        if (uf[(size_t)(y >> 3) * tw + (x >> 3)] & (1ull << ((y & 7) * 8 + (x & 7)))) ru += nr[k];
-    }
-    g->r_universe = ru;
+    HIPCHK(hipStreamSynchronize(s));
+    g->uf_count = (int64_t)ufc;
     return DMX_OK;
 }
 
@@ -809,8 +828,9 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     Q.seed_tiles = g->notuf_tiles.p; Q.uf_tiles = g->uf_tiles.p; Q.nonexp_tiles = g->pm->d_nonexp_tiles.p;
     Q.node_cell = P.node_cell; Q.cell_node = P.cell_node; Q.node_flags = P.node_flags;
     Q.node_run_start = P.node_run_start; Q.node_nruns = P.node_nruns; Q.pool = P.pool;
+    Q.cell_scan_start = g->cell_scan_start.p; Q.cell_nruns = g->cell_nruns.p; Q.scan_pool = g->scan_pool.p;
     Q.src_begin = sb; Q.src_end = se; Q.radius = P.radius; Q.gates_only = gates_only;
-    Q.uf_count = g->uf_count; Q.r_universe = g->r_universe; Q.symmetric = g->symmetric;
+    Q.uf_count = g->uf_count; Q.symmetric = g->symmetric;
     const bool corr = g->symmetric == 1 && g->nspecial > 0;
     Q.spec_index = corr ? g->spec_index.p : nullptr;
     Q.extra_off = corr ? g->extra_off.p : nullptr;

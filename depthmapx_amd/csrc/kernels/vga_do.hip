@@ -10,9 +10,10 @@
 //
 // Per workgroup (one source at a time, persistent grid): three LDS bitmaps tiled 8x8 cells per
 // 64-bit word -- V (seen, pre-seeded with cells that can never be discovered), F (expandable
-// frontier) and X (next level).  Per level the direction is chosen with Beamer's test
-// (m_f * alpha > m_u: frontier run mass vs unvisited run mass).  Bottom-up cells scan at most
-// `kshort` runs on their own lane; the rest go to a hard list scanned 64 runs at a time per wave.
+// frontier) and X (next level).  Per level the direction is chosen with Beamer's test on cell
+// counts (n_frontier * alpha > n_unvisited).  Bottom-up cells scan their runs longest-first (the
+// scan pool) on their own lane for at most `kshort` runs; the rest go to a hard list scanned 64
+// runs at a time per wave.
 #include "common.hpp"
 
 namespace dmx {
@@ -28,10 +29,12 @@ struct VgaDoParams {
     const int64_t* node_run_start;
     const int32_t* node_nruns;
     const Run* pool;
+    const int64_t* cell_scan_start;  // [C] start of the cell's runs in scan_pool (longest first)
+    const int32_t* cell_nruns;       // [C] (0 for non-filled cells)
+    const Run* scan_pool;
     int64_t src_begin, src_end;
     int radius, gates_only;
     int64_t uf_count;       // |U_f|
-    int64_t r_universe;     // sum of runs over U_f
     int symmetric;          // bottom-up allowed
     // exact in-set corrections for the few nodes whose visibility is not symmetric
     const int32_t* spec_index;    // [N] node -> special index or -1
@@ -151,7 +154,7 @@ __device__ __forceinline__ int run_push(unsigned long long* V, unsigned long lon
 
 struct DoShared {
     int list_n, hard_n, item, pad;
-    unsigned long long cnt, mass;   // next-level count and run mass
+    unsigned long long cnt, mass;   // next-level count and its expandable part
     unsigned long long tdnew;       // cells discovered so far in a top-down level
 };
 
@@ -197,8 +200,8 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
         if (tid == 0) { hist[0] = 1; S->cnt = 0; S->mass = 0; S->list_n = 0; S->hard_n = 0; S->item = 0; S->tdnew = 0; }
         const bool s_in_uf = (P.uf_tiles[stile] & sbit) != 0;
         const long long target = P.uf_count - (s_in_uf ? 1 : 0); // cells still to discover
-        const long long rs_src = P.node_nruns[src];
-        long long m_f = rs_src, m_u = P.r_universe - (s_in_uf ? rs_src : 0);
+        // Beamer's direction test on cell counts: frontier size vs cells still unvisited
+        long long m_f = 1, m_u = target;
         long long discovered = 0;
         int level = 0, nlev = 1;
         bool overflow = false;
@@ -226,17 +229,16 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                 // ---- phase 1: one lane per cell, at most kshort runs
                 for (int i = tid; i < nl; i += DO_THREADS) {
                     const int c = list[i];
-                    const int node = P.cell_node[c];
-                    if (P.spec_index && P.spec_index[node] >= 0) { // exact path (phase 2)
+                    if (P.spec_index && P.spec_index[P.cell_node[c]] >= 0) { // exact path (phase 2)
                         hard[atomicAdd(&S->hard_n, 1)] = -1 - c;
                         continue;
                     }
-                    const int64_t rs = P.node_run_start[node];
-                    const int nr = P.node_nruns[node];
+                    const int64_t rs = P.cell_scan_start[c];
+                    const int nr = P.cell_nruns[c];
                     const int lim = min(nr, P.kshort);
                     bool hit = false;
                     int r = 0;
-                    for (; r < lim && !hit; r++) hit = run_hits(F, tw, P.pool[rs + r]);
+                    for (; r < lim && !hit; r++) hit = run_hits(F, tw, P.scan_pool[rs + r]);
                     runs_read += r;
                     if (hit) {
                         const int x = c / rows, y = c % rows;
@@ -292,9 +294,10 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                         found = __ballot(h) != 0ull;
                         if (lane == 0) runs_read += (unsigned long long)nr;
                     }
+                    const int64_t srs = P.cell_scan_start[c];
                     for (int base = P.kshort; base < nr && !found && !special; base += 64) {
                         const int r = base + lane;
-                        const bool h = (r < nr) && run_hits(F, tw, P.pool[rs + r]);
+                        const bool h = (r < nr) && run_hits(F, tw, P.scan_pool[srs + r]);
                         found = __ballot(h) != 0ull;
                         if (lane == 0) runs_read += (unsigned long long)min(64, nr - base);
                     }
@@ -328,11 +331,11 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                     it = __shfl(it, 0);
                     // everything discoverable already found -> the rest of the level adds nothing
                     if (it >= nl || discovered + (long long)*(volatile unsigned long long*)&S->tdnew >= target) break;
-                    const int node = P.cell_node[list[it]];
-                    const int64_t rs = P.node_run_start[node];
-                    const int nr = P.node_nruns[node];
+                    const int c = list[it];
+                    const int64_t rs = P.cell_scan_start[c];
+                    const int nr = P.cell_nruns[c];
                     int nnew = 0;
-                    for (int r = lane; r < nr; r += 64) nnew += run_push(V, X, tw, P.pool[rs + r]);
+                    for (int r = lane; r < nr; r += 64) nnew += run_push(V, X, tw, P.scan_pool[rs + r]);
                     for (int off = 32; off >= 1; off >>= 1) nnew += __shfl_xor(nnew, off);
                     if (lane == 0) {
                         runs_read += (unsigned long long)nr;
@@ -343,20 +346,14 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                 if (tid == 0) { S->list_n = 0; S->item = 0; S->tdnew = 0; }
             }
             __syncthreads();
-            // ---- level bookkeeping: count + run mass of X, next frontier
+            // ---- level bookkeeping: count of X, next (expandable) frontier
             unsigned long long c_loc = 0, m_loc = 0;
             for (int i = tid; i < nt; i += DO_THREADS) {
                 unsigned long long x = X[i];
                 if (x) {
                     c_loc += (unsigned long long)__popcll(x);
-                    const int tx = i % tw, ty = i / tw;
-                    unsigned long long u = x;
-                    while (u) {
-                        const int b = __ffsll((long long)u) - 1;
-                        u &= u - 1;
-                        m_loc += (unsigned long long)P.node_nruns[P.cell_node[(tx * 8 + (b & 7)) * rows + ty * 8 + (b >> 3)]];
-                    }
                     if (P.radius != -1) x &= ~P.nonexp_tiles[i];
+                    m_loc += (unsigned long long)__popcll(x);  // expandable part of the next frontier
                 }
                 F[i] = x;
                 X[i] = 0ull;
@@ -374,7 +371,7 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
             if (level + 1 >= P.maxlev) { overflow = true; break; }
             if (tid == 0) hist[level + 1] = (int)cnt;
             discovered += cnt;
-            m_u -= mass;
+            m_u -= cnt;
             m_f = mass;
             level++;
             nlev = level + 1;
@@ -504,6 +501,96 @@ __global__ void sym_flag_kernel(int rows, const int32_t* node_cell, int64_t n, i
     if (hi != ho[k]) {
         const int pos = atomicAdd(count, 1);
         if (pos < cap) list[pos] = (int32_t)k;
+    }
+}
+
+// Coverage counts: range-add 1 per run into int difference arrays (4 directions); after the line
+// prefix pass a filled cell with a non-zero total appears in some run (it is in U_f).
+__global__ void cov_scatter_kernel(int cols, int rows, int64_t n, const int64_t* node_run_start, const int32_t* node_nruns,
+                                   const Run* pool, int* diff) {
+    const int64_t C = (int64_t)cols * rows;
+    for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
+        const int64_t rs = node_run_start[k];
+        const int nr = node_nruns[k];
+        for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+            const Run ru = pool[rs + r];
+            const int dir = run_dir(ru);
+            int dx, dy;
+            dir_step(dir, dx, dy);
+            const int ex = ru.x1 + dx, ey = ru.y1 + dy;
+            int* D = diff + (int64_t)dir * C;
+            atomicAdd(&D[(int64_t)ru.x0 * rows + ru.y0], 1);
+            if (ex >= 0 && ex < cols && ey >= 0 && ey < rows) atomicAdd(&D[(int64_t)ex * rows + ey], -1);
+        }
+    }
+}
+__global__ void cov_lines_kernel(int cols, int rows, int* arr) {
+    const int64_t C = (int64_t)cols * rows;
+    const int dir = blockIdx.y;
+    const int line = blockIdx.x * blockDim.x + threadIdx.x;
+    int x, y, dx, dy;
+    if (!line_start(dir, line, cols, rows, x, y)) return;
+    dir_step(dir, dx, dy);
+    int* A = arr + (int64_t)dir * C;
+    int acc = 0;
+    for (; x >= 0 && x < cols && y >= 0 && y < rows; x += dx, y += dy) {
+        const int64_t c = (int64_t)x * rows + y;
+        acc += A[c];
+        A[c] = acc;
+    }
+}
+// U_f tiles (filled & covered), their complement, and the count
+__global__ void cov_tiles_kernel(int cols, int rows, int tw, int th, const int32_t* cell_node, const int* cov,
+                                 unsigned long long* uf, unsigned long long* notuf, unsigned long long* count) {
+    const int64_t C = (int64_t)cols * rows;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= tw * th) return;
+    const int tx = t % tw, ty = t / tw;
+    unsigned long long w = 0;
+    for (int b = 0; b < 64; b++) {
+        const int x = tx * 8 + (b & 7), y = ty * 8 + (b >> 3);
+        if (x >= cols || y >= rows) continue;
+        const int64_t c = (int64_t)x * rows + y;
+        if (cell_node[c] >= 0 && (cov[c] + cov[C + c] + cov[2 * C + c] + cov[3 * C + c]) > 0) w |= 1ull << b;
+    }
+    uf[t] = w;
+    notuf[t] = ~w;
+    if (w) atomicAdd(count, (unsigned long long)__popcll(w));
+}
+
+// Scan pool: each node's runs bucketed longest-first (bucket = floor(log2(cells)), 16 buckets), so a
+// bottom-up cell tests its most likely hits first.  One workgroup per node; also fills the
+// cell-indexed start / count arrays.
+__global__ void scan_pool_kernel(int rows, const int32_t* node_cell, int64_t n, const int64_t* node_run_start,
+                                 const int32_t* node_nruns, const Run* pool, const int64_t* scan_start, Run* scan_pool,
+                                 int64_t* cell_scan_start, int32_t* cell_nruns) {
+    __shared__ int cnt[16], cur[16];
+    for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
+        const int64_t rs = node_run_start[k], ss = scan_start[k];
+        const int nr = node_nruns[k];
+        if (threadIdx.x < 16) cnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+            const Run ru = pool[rs + r];
+            const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+            atomicAdd(&cnt[15 - min(15, 31 - __clz(len))], 1);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int acc = 0;
+            for (int b = 0; b < 16; b++) { cur[b] = acc; acc += cnt[b]; }
+            const int c = node_cell[k];
+            cell_scan_start[c] = ss;
+            cell_nruns[c] = nr;
+        }
+        __syncthreads();
+        for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+            const Run ru = pool[rs + r];
+            const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+            const int pos = atomicAdd(&cur[15 - min(15, 31 - __clz(len))], 1);
+            scan_pool[ss + pos] = ru;
+        }
+        __syncthreads();
     }
 }
 

@@ -1,0 +1,62 @@
+"""Multi-GPU choreography for the hot path (one process per GPU, torch.distributed over RCCL).
+
+The units are source cells: rank r owns the contiguous x-major node range shard_range(N, r, W).
+Per step
+  1. makeGraph for the owned sources (no communication);
+  2. all-gather of the run-length graph shards (ragged byte blobs, padded to the largest) so every
+     rank holds the whole graph -- VGA BFS from any source can reach any node;
+  3. VGA global for the owned sources;
+  4. all-gather of the owned rows of the 7 float columns.
+Only 2 and 4 are collectives.  The helpers below take any torch.distributed backend, so the same
+code is exercised with gloo on CPU tensors in tests/test_sharded_gloo.py.
+"""
+import torch
+
+
+def shard_range(n, rank, world):
+    """Contiguous, balanced split of n units over `world` ranks."""
+    return (n * rank) // world, (n * (rank + 1)) // world
+
+
+def allgather_blobs(blob, dist, device=None):
+    """All-gather ragged 1-D uint8 tensors.  Returns (flat tensor of world*maxlen bytes, sizes):
+    rank i's blob occupies flat[i*maxlen : i*maxlen + sizes[i]]."""
+    world = dist.get_world_size()
+    device = device if device is not None else blob.device
+    sz = torch.tensor([blob.numel()], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(sz) for _ in range(world)]
+    dist.all_gather(sizes, sz)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    mine = torch.zeros(mx, dtype=torch.uint8, device=device)
+    mine[: blob.numel()] = blob
+    flat = torch.empty(world * mx, dtype=torch.uint8, device=device)
+    if hasattr(dist, "all_gather_into_tensor") and device.type == "cuda":
+        dist.all_gather_into_tensor(flat, mine)
+    else:
+        parts = list(flat.view(world, mx).unbind(0))
+        dist.all_gather(parts, mine)
+        flat = torch.stack(parts).reshape(-1)
+    return flat, mx, sizes
+
+
+def allgather_rows(full, n, dist):
+    """full: [n, k] tensor where this rank filled rows shard_range(n, rank, world); afterwards every
+    rank holds all rows."""
+    world, rank = dist.get_world_size(), dist.get_rank()
+    b, e = shard_range(n, rank, world)
+    per = (n + world - 1) // world
+    k = full.shape[1]
+    mine = torch.zeros((per, k), dtype=full.dtype, device=full.device)
+    mine[: e - b] = full[b:e]
+    if hasattr(dist, "all_gather_into_tensor") and full.device.type == "cuda":
+        gathered = torch.empty((world * per, k), dtype=full.dtype, device=full.device)
+        dist.all_gather_into_tensor(gathered, mine)
+    else:
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        gathered = torch.cat(parts)
+    for r in range(world):
+        rb, re_ = shard_range(n, r, world)
+        full[rb:re_] = gathered[r * per: r * per + (re_ - rb)]
+    return full

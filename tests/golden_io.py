@@ -54,3 +54,27 @@ def node_digests(bins, runs):
         out[k] = np.frombuffer(h.digest(), dtype=np.uint64)[0]
         ro += nr
     return out
+
+
+def roundtrip_runs(bins, runs):
+    """Apply the .graph write/read round trip to a run list: inside each H/V bin,
+    run i>0 is stored as (primary coordinate, ShiftLength{shift:4, runlength:12}) relative to run
+    i-1 (ngraph.cpp:536-583), so row/column jumps > 15 wrap on re-read and the error propagates.
+    Diagonal bins keep their single span.  Returns the runs VGA sees after VISPREP -> file -> VGA."""
+    out = runs.astype(np.int32).copy()
+    ro = 0
+    for k in range(len(bins)):
+        for b in range(32):
+            d, n = int(bins[k, b, 0]), int(bins[k, b, 3])
+            if n and d in (1, 2):
+                for i in range(ro + 1, ro + n):
+                    if d == 1:  # HORIZONTAL: primary x, shift in y, length in x
+                        y = out[i - 1, 1] + ((int(runs[i, 1]) - int(runs[i - 1, 1])) & 15)
+                        x0 = int(runs[i, 0])
+                        out[i] = (x0, y, x0 + ((int(runs[i, 2]) - x0) & 4095), y)
+                    else:       # VERTICAL: primary y, shift in x, length in y
+                        x = out[i - 1, 0] + ((int(runs[i, 0]) - int(runs[i - 1, 0])) & 15)
+                        y0 = int(runs[i, 1])
+                        out[i] = (x, y0, x, y0 + ((int(runs[i, 3]) - y0) & 4095))
+            ro += n
+    return out.astype(np.int16)

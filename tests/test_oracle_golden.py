@@ -1,0 +1,121 @@
+"""The C restatement (oracle/) against the REAL reference's outputs (tests/golden/, produced by
+oracle/_ref/ref_probe = salalib compiled from source).  This pins the oracle before it is trusted
+as the GPU checker."""
+import numpy as np
+import pytest
+
+from golden_io import case_input_lines, load_case, node_digests, roundtrip_runs
+from pyoracle import OracleMap
+
+CASES = ["kat", "syn16", "syn32", "gallery", "syn64", "barnsbury"]
+
+
+def _oracle(meta, threads=8):
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    assert (om.cols, om.rows) == (meta["cols"], meta["rows"])
+    assert np.allclose(om.bottom_left, meta["bottom_left"])
+    for f in meta["fills"]:
+        assert om.fill(*f)
+    return om
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_prep_matches_reference(name):
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    counts, pieces = om.cell_lines()
+    np.testing.assert_array_equal(counts, A["celllines_n"])
+    np.testing.assert_array_equal(pieces, A["celllines"])
+    np.testing.assert_array_equal(om.state(), A["state"])
+
+
+@pytest.mark.parametrize("name", CASES + ["syn256mk"])
+def test_makegraph_matches_reference(name):
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    assert om.num_nodes == meta["nodes"]
+    g = om.graph()
+    assert len(g["runs"]) == meta["runs"]
+    np.testing.assert_array_equal(g["attrs"].view(np.uint32), A["attrs"].view(np.uint32))
+    np.testing.assert_array_equal(g["gridconn"], A["gridconn"])
+    if "bins" in A:
+        np.testing.assert_array_equal(g["bins"], A["bins"])
+        np.testing.assert_array_equal(g["runs"], A["runs"])
+    np.testing.assert_array_equal(g["bins"][:, :, 3].sum(axis=1), A["nruns"])
+    np.testing.assert_array_equal(node_digests(g["bins"], g["runs"]), A["digests"])
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "gallery", "syn64"])
+def test_vga_global_matches_reference_bitexact(name):
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    out = om.vga_global(threads=8)
+    np.testing.assert_array_equal(out.view(np.uint32), A["vga"].view(np.uint32))
+
+
+@pytest.mark.slow
+def test_vga_global_barnsbury_bitexact():
+    meta, A = load_case("barnsbury")
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    out = om.vga_global(threads=8)
+    np.testing.assert_array_equal(out.view(np.uint32), A["vga"].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["syn32", "gallery", "syn64"])
+def test_graph_file_roundtrip_quirk(name):
+    """VGA in the CLI pipeline runs on the re-read .graph whose runs went through the lossy 4-bit
+    row shift; the reference's post-round-trip VGA columns (vga_rt) are reproduced by
+    applying that transform to the runs."""
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    g = om.graph()
+    rt = roundtrip_runs(g["bins"], g["runs"])
+    om.set_graph(g["bins"], rt)
+    out = om.vga_global(threads=8)
+    np.testing.assert_array_equal(out.view(np.uint32), A["vga_rt"].view(np.uint32))
+
+
+def test_kat_connections_from_reference_test():
+    """salaTest/testpointmap.cpp:400-451: node iteration order of the 2x2 KAT (PixelRef ints)."""
+    expected = {65537: [131073, 131074, 65538], 65538: [131074, 65537, 131073],
+                131073: [131074, 65538, 65537], 131074: [65538, 65537, 131073]}
+    meta, _ = load_case("kat")
+    om = _oracle(meta)
+    om.make_graph()
+    g = om.graph()
+    ro = 0
+    st = om.state()
+    nodes = [c for c in range(len(st)) if st[c] & 2]
+    for k, c in enumerate(nodes):
+        x, y = divmod(c, om.rows)
+        conn = []
+        for b in range(32):
+            for r in g["runs"][ro:ro + g["bins"][k, b, 3]]:
+                x0, y0, x1, y1 = map(int, r)
+                dx = 1 if x1 > x0 else 0
+                dy = 0 if y0 == y1 else (1 if x0 == x1 else (1 if y1 > y0 else -1))
+                px, py = x0, y0
+                while True:
+                    conn.append((px << 16) | py)
+                    if (px, py) == (x1, y1):
+                        break
+                    px += dx
+                    py += dy
+            ro += g["bins"][k, b, 3]
+        assert conn == expected[(x << 16) | y]
+
+
+def test_reference_gallery_attributes_file():
+    """testdata/gallery_graph_vga.txt (the reference's own expected Connectivity / moments for
+    gallery_empty.graph -pg 0.04 -pp 1.32,7.24) vs the golden probe dump."""
+    import os
+    from golden_io import GOLDEN
+    meta, A = load_case("gallery")
+    rows = np.loadtxt(os.path.join(GOLDEN, "gallery_graph_vga.txt"), skiprows=1)
+    assert len(rows) == meta["nodes"]
+    np.testing.assert_array_equal(rows[:, 3], A["attrs"][:, 0])
+    np.testing.assert_allclose(rows[:, 4:6], A["attrs"][:, 1:3], rtol=1e-6)

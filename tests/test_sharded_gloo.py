@@ -1,0 +1,105 @@
+"""world_size-2 gloo run of the multi-GPU choreography (depthmapx_amd/sharded.py) on CPU.
+
+Each rank builds the makeGraph shard for its source range, the shards are all-gathered as ragged
+byte blobs and reassembled, each rank runs VGA global for its sources, and the 7 columns are
+all-gathered.  The per-rank compute here is the C restatement (no GPU in this container); the
+collectives, sharding and reassembly are exactly the code bench.py runs over RCCL."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from golden_io import case_input_lines, load_case
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _pack(g, n):
+    bins = np.ascontiguousarray(g["bins"], dtype=np.int32)
+    runs = np.ascontiguousarray(g["runs"], dtype=np.int16)
+    hdr = np.array([n, len(runs)], dtype=np.int64)
+    return np.concatenate([hdr.view(np.uint8), bins.view(np.uint8).ravel(), runs.view(np.uint8).ravel()])
+
+
+def _unpack(buf):
+    n, nr = np.frombuffer(buf[:16].tobytes(), dtype=np.int64)
+    bins = np.frombuffer(buf[16:16 + n * 32 * 16].tobytes(), dtype=np.int32).reshape(n, 32, 4)
+    runs = np.frombuffer(buf[16 + n * 32 * 16:16 + n * 32 * 16 + nr * 8].tobytes(), dtype=np.int16).reshape(nr, 4)
+    return bins, runs
+
+
+def _worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle")):
+        sys.path.insert(0, p)
+    from depthmapx_amd.sharded import allgather_blobs, allgather_rows, shard_range
+    from pyoracle import OracleMap
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    meta, _ = load_case("syn16")
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    om.fill(*meta["fills"][0])
+    om.make_graph()                       # index nodes
+    N = om.num_nodes
+    b, e = shard_range(N, rank, world)
+    om.make_graph(node_begin=b, node_end=e)
+    full = om.graph()
+    ro = int(full["bins"][:b, :, 3].sum())
+    nr = int(full["bins"][b:e, :, 3].sum())
+    blob = torch.from_numpy(_pack(dict(bins=full["bins"][b:e], runs=full["runs"][ro:ro + nr]), e - b))
+    flat, mx, sizes = allgather_blobs(blob, dist, device=torch.device("cpu"))
+    parts = [_unpack(flat[i * mx:i * mx + sizes[i]].numpy()) for i in range(world)]
+    bins = np.concatenate([p[0] for p in parts])
+    runs = np.concatenate([p[1] for p in parts])
+    om.set_graph(bins, runs)
+    out = torch.full((N, 7), -1.0)
+    out[b:e] = torch.from_numpy(om.vga_global(node_begin=b, node_end=e)[b:e])
+    allgather_rows(out, N, dist)
+    q.put((rank, bins, runs, out.numpy()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_matches_single_process():
+    from pyoracle import OracleMap
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    meta, A = load_case("syn16")
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    om.fill(*meta["fills"][0])
+    om.make_graph()
+    g = om.graph()
+    ref = om.vga_global()
+    for _, bins, runs, out in res:
+        np.testing.assert_array_equal(bins, g["bins"])
+        np.testing.assert_array_equal(runs, g["runs"])
+        np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
+        np.testing.assert_array_equal(out.view(np.uint32), A["vga"].view(np.uint32))
+
+
+@pytest.mark.parametrize("n,world", [(0, 2), (1, 2), (7, 3), (65025, 8)])
+def test_shard_ranges_partition(n, world):
+    from depthmapx_amd.sharded import shard_range
+    r = [shard_range(n, i, world) for i in range(world)]
+    assert r[0][0] == 0 and r[-1][1] == n
+    assert all(r[i][1] == r[i + 1][0] for i in range(world - 1))
+    assert max(e - b for b, e in r) - min(e - b for b, e in r) <= 1
