@@ -20,6 +20,7 @@
 #include "kernels/makegraph.hip"
 #include "kernels/vga.hip"
 #include "kernels/vga_do.hip"
+#include "kernels/vga_tile.hip"
 
 using namespace dmx;
 
@@ -56,13 +57,14 @@ template <typename T> struct DevBuf {
 
 struct dmx_ctx {
     int device = 0;
+    bool tile_disabled = false;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int num_cu = 0;
     double last_mk_s = 0, last_vga_s = 0;
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
-    long long last_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long last_stats[16] = {};
 };
 
 struct dmx_pointmap {
@@ -102,9 +104,17 @@ struct dmx_graph {
     DevBuf<Run> scan_pool;
     DevBuf<int64_t> cell_scan_start;
     DevBuf<int32_t> cell_nruns;
+    DevBuf<int64_t> scan_start;   // [N] start of each node's runs in scan_pool
     int symmetric = -1;   // -1 unknown, 0 top-down only, 1 bottom-up allowed (with corrections)
     int nspecial = 0;
+    std::vector<int32_t> special_nodes;
     DevBuf<int32_t> spec_index, extra_off, extra, missing_off, missing;
+    // tile-resolved BFS (vga_tile.hip)
+    bool tiles_ready = false;
+    DevBuf<int64_t> tscan_start;
+    DevBuf<int32_t> tnruns;
+    DevBuf<Run> heads, cr;
+    DevBuf<unsigned long long> regular_tiles;
 };
 
 namespace {
@@ -236,7 +246,7 @@ int dmx_ctx_free(dmx_ctx* c) {
 
 int dmx_ctx_last_stats(dmx_ctx* c, int64_t* out, int n) {
     if (!c || !out) return fail(DMX_ERR_ARG, "bad arguments");
-    for (int i = 0; i < n && i < 8; i++) out[i] = c->last_stats[i];
+    for (int i = 0; i < n && i < 16; i++) out[i] = c->last_stats[i];
     return DMX_OK;
 }
 
@@ -655,7 +665,7 @@ static int prepare_uf(dmx_graph* g) {
     std::vector<int64_t> ss((size_t)std::max<int64_t>(N, 1));
     int64_t acc = 0;
     for (int64_t k = 0; k < N; k++) { ss[k] = acc; acc += nr[k]; }
-    DevBuf<int64_t> d_ss;
+    DevBuf<int64_t>& d_ss = g->scan_start;
     HIPCHK(d_ss.alloc(std::max<int64_t>(N, 1)));
     HIPCHK(g->scan_pool.alloc(std::max<int64_t>(acc, 1)));
     HIPCHK(g->cell_scan_start.alloc(C));
@@ -664,7 +674,7 @@ static int prepare_uf(dmx_graph* g) {
     if (N) {
         HIPCHK(hipMemcpyAsync(d_ss.p, ss.data(), N * 8, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(scan_pool_kernel, dim3((unsigned)std::min<int64_t>(N, 8192)), dim3(256), 0, s, rows,
-                           g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, d_ss.p,
+                           g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->bin_nruns.p, g->pool.p, d_ss.p,
                            g->scan_pool.p, g->cell_scan_start.p, g->cell_nruns.p);
         HIPCHK(hipGetLastError());
     }
@@ -721,6 +731,7 @@ static int prepare_symmetry(dmx_graph* g) {
     std::vector<int32_t> specs((size_t)nspec);
     HIPCHK(hipMemcpy(specs.data(), flist.p, nspec * 4, hipMemcpyDeviceToHost));
     std::sort(specs.begin(), specs.end());
+    g->special_nodes = specs;
     std::vector<uint8_t> is_spec((size_t)N, 0);
     std::vector<int32_t> sidx((size_t)N, -1);
     for (int i = 0; i < nspec; i++) { is_spec[specs[i]] = 1; sidx[specs[i]] = i; }
@@ -774,6 +785,158 @@ static int prepare_symmetry(dmx_graph* g) {
     return DMX_OK;
 }
 
+// Tile-ordered per-cell arrays, head runs and tile-common runs for vga_tile_kernel (O(runs)).
+static int prepare_tiles(dmx_graph* g) {
+    if (g->tiles_ready) return DMX_OK;
+    dmx_ctx* ctx = g->ctx;
+    hipStream_t s = ctx->stream;
+    PointMapHost& h = *g->pm->host;
+    const int cols = h.cols(), rows = h.rows();
+    const int tw = (cols + 7) / 8, th = (rows + 7) / 8, nt = tw * th;
+    const int64_t N = g->nnodes, Ct = (int64_t)nt * 64;
+    HIPCHK(g->tscan_start.alloc(Ct));
+    HIPCHK(g->tnruns.alloc(Ct));
+    HIPCHK(g->heads.alloc((size_t)KH * Ct));
+    HIPCHK(g->cr.alloc((size_t)CRK * nt));
+    HIPCHK(g->regular_tiles.alloc(nt));
+    HIPCHK(hipMemsetAsync(g->tnruns.p, 0, Ct * 4, s));
+    HIPCHK(hipMemsetAsync(g->tscan_start.p, 0, Ct * 8, s));
+    HIPCHK(hipMemsetAsync(g->heads.p, 0xFF, (size_t)KH * Ct * sizeof(Run), s));
+    // regular = U_f minus the special (asymmetric) nodes
+    std::vector<unsigned long long> uf((size_t)nt);
+    HIPCHK(hipMemcpyAsync(uf.data(), g->uf_tiles.p, nt * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int32_t k : g->special_nodes) {
+        const int c = g->pm->node_cell[k];
+        const int x = c / rows, y = c % rows;
+        uf[(size_t)(y >> 3) * tw + (x >> 3)] &= ~(1ull << ((y & 7) * 8 + (x & 7)));
+    }
+    HIPCHK(hipMemcpyAsync(g->regular_tiles.p, uf.data(), nt * 8, hipMemcpyHostToDevice, s));
+    if (N) {
+        hipLaunchKernelGGL(tile_heads_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rows, tw,
+                           g->pm->d_node_cell.p, N, g->node_nruns.p, g->scan_pool.p, g->scan_start.p,
+                           g->tscan_start.p, g->tnruns.p, g->heads.p, (size_t)Ct);
+        HIPCHK(hipGetLastError());
+    }
+    const int dmax = std::max(cols, rows);
+    const size_t lds = (size_t)8 * (dmax + 2) * 4;
+    if (lds > 150 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the tile-common-run pass");
+    hipLaunchKernelGGL(tile_cr_kernel, dim3((unsigned)std::min<int64_t>(nt, (int64_t)ctx->num_cu * 8)), dim3(CR_THREADS),
+                       lds, s, cols, rows, tw, th, g->regular_tiles.p, g->pm->d_cell_node.p, g->node_run_start.p,
+                       g->node_nruns.p, g->scan_start.p, g->scan_pool.p, g->pool.p, dmax, g->cr.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    g->tiles_ready = true;
+    return DMX_OK;
+}
+
+extern "C++" template <int NT>
+static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_t lds, int64_t* blocks_out,
+                       DevBuf<unsigned long long>& xg, DevBuf<int4>& queue, DevBuf<int32_t>& list) {
+    int occ = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT>, NT, lds));
+    if (occ < 1) occ = 1;
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cu * occ, nsrc));
+    const int64_t nt = (int64_t)Q.tw * Q.th;
+    HIPCHK(xg.alloc((size_t)blocks * 2 * nt));
+    HIPCHK(queue.alloc((size_t)blocks * nt));
+    HIPCHK(list.alloc((size_t)blocks * nt * 64));
+    VgaTileParams P = Q;
+    P.xg = xg.p;
+    P.queue = queue.p;
+    P.list = list.p;
+    HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+    hipLaunchKernelGGL((vga_tile_kernel<NT>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
+    HIPCHK(hipGetLastError());
+    *blocks_out = blocks;
+    return DMX_OK;
+}
+
+static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
+                         bool out_on_device, int64_t* levels, int tw, int th) {
+    int rc = prepare_tiles(g);
+    if (rc) return rc;
+    PointMapHost& h = *g->pm->host;
+    const int64_t N = g->nnodes, nsrc = se - sb;
+    const int nt = tw * th;
+    const int maxlev = 1024;
+    DevBuf<float> d_out;
+    float* outp = out;
+    if (!out_on_device) {
+        HIPCHK(d_out.alloc(std::max<int64_t>(N, 1) * 7));
+        outp = d_out.p;
+    }
+    DevBuf<int64_t> d_lv;
+    if (levels) HIPCHK(d_lv.alloc(std::max<int64_t>(N, 1) * 3));
+    HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    VgaTileParams Q;
+    Q.cols = h.cols(); Q.rows = h.rows(); Q.tw = tw; Q.th = th;
+    Q.seed_tiles = g->notuf_tiles.p; Q.regular_tiles = g->regular_tiles.p; Q.nonexp_tiles = g->pm->d_nonexp_tiles.p;
+    Q.cr = g->cr.p; Q.heads = g->heads.p; Q.tscan_start = g->tscan_start.p; Q.tnruns = g->tnruns.p;
+    Q.scan_pool = g->scan_pool.p;
+    Q.node_cell = g->pm->d_node_cell.p; Q.cell_node = g->pm->d_cell_node.p; Q.node_flags = g->pm->d_node_flags.p;
+    Q.node_run_start = g->node_run_start.p; Q.node_nruns = g->node_nruns.p; Q.pool = g->pool.p;
+    const bool corr = g->nspecial > 0;
+    Q.spec_index = corr ? g->spec_index.p : nullptr;
+    Q.extra_off = corr ? g->extra_off.p : nullptr;
+    Q.extra = corr ? g->extra.p : nullptr;
+    Q.missing_off = corr ? g->missing_off.p : nullptr;
+    Q.missing = corr ? g->missing.p : nullptr;
+    Q.src_begin = sb; Q.src_end = se; Q.radius = (int)radius; Q.gates_only = gates_only;
+    Q.uf_count = g->uf_count;
+    Q.alpha = 15;
+    if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
+    Q.work_counter = ctx->counters.p + 0; Q.error = ctx->counters.p + 1;
+    DevBuf<int32_t> d_hist, d_nlev;
+    HIPCHK(d_hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));
+    HIPCHK(d_nlev.alloc(std::max<int64_t>(N, 1)));
+    Q.maxlev = maxlev; Q.hist_out = d_hist.p; Q.nlev_out = d_nlev.p; Q.stats = ctx->stats.p;
+    const size_t lds = (size_t)nt * 8 + (size_t)VGA_HMAX * 4;
+    DevBuf<unsigned long long> xg;
+    DevBuf<int4> queue;
+    DevBuf<int32_t> list;
+    int64_t blocks = 0;
+    int kt = 0, ntpb = 0;
+    (void)kt;
+    if (nsrc > 0) {
+        if (nt <= 4096) { rc = launch_tile<256>(ctx, Q, nsrc, lds, &blocks, xg, queue, list); ntpb = 256; }
+        else { rc = launch_tile<1024>(ctx, Q, nsrc, lds, &blocks, xg, queue, list); ntpb = 1024; }
+        if (rc) return rc;
+        hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsrc + 255) / 256)), dim3(256), 0, ctx->stream, sb, se,
+                           d_hist.p, d_nlev.p, outp, levels ? d_lv.p : nullptr, ctx->stats.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+    } else {
+        HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+        HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_vga_s = ms * 1e-3;
+    int hc[2];
+    HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+    if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level capacity");
+    unsigned long long st[8];
+    HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+    ctx->last_stats[3] = 3 | ((long long)g->nspecial << 8);
+    ctx->last_stats[4] = (long long)st[0];
+    ctx->last_stats[5] = (long long)(st[3] | (st[4] << 32));
+    ctx->last_stats[6] = (long long)st[2];
+    ctx->last_stats[7] = nsrc;
+    ctx->last_stats[8] = (long long)st[5];
+    ctx->last_stats[9] = (long long)st[6];
+    ctx->last_stats[10] = 0;
+    ctx->last_stats[11] = (long long)st[7];
+    ctx->last_stats[12] = blocks | ((long long)kt << 32) | ((long long)ntpb << 40);
+    if (!out_on_device && nsrc > 0)
+        HIPCHK(hipMemcpy(out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
+    if (levels && nsrc > 0)
+        HIPCHK(hipMemcpy(levels + sb * 3, d_lv.p + sb * 3, nsrc * 3 * 8, hipMemcpyDeviceToHost));
+    return DMX_OK;
+}
+
 static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
                     bool out_on_device, int64_t* levels) {
     if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");
@@ -790,19 +953,33 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     PointMapHost& h = *g->pm->host;
     const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
     const int maxlev = 4096;
+    {
+        const char* fk = getenv("DMX_VGA_KERNEL");
+        const bool forced_other = fk && (std::string(fk) == "v1" || std::string(fk) == "do" || std::string(fk) == "topdown");
+        const int nt = tw * th;
+        if (!forced_other && g->symmetric == 1 && nt <= 16 * 1024 && !ctx->tile_disabled) {
+            int rc2 = vga_tile_impl(ctx, g, radius, gates_only, sb, se, out, out_on_device, levels, tw, th);
+            if (rc2 != DMX_ERR_CAPACITY) return rc2;   // capacity (level histogram): retry with vga_do
+        }
+    }
     const size_t lds_do = (size_t)tw * th * 8 * 3 + (maxlev + 4) * 4 + 64;
     const char* force = getenv("DMX_VGA_KERNEL");
-    const bool use_do = lds_do <= 160 * 1024 && !(force && std::string(force) == "v1");
-    const size_t lds = use_do ? lds_do : (size_t)tw * th * 8 + (maxlev + 4) * 4 + 64;
+    const bool want_v1 = force && std::string(force) == "v1";
+    const bool gbm = !want_v1 && lds_do > 160 * 1024;   // bitmaps in HBM
+    const bool use_do = !want_v1;
+    const size_t lds = gbm ? (size_t)(maxlev + 4) * 4 + 64 : use_do ? lds_do : (size_t)tw * th * 8 + (maxlev + 4) * 4 + 64;
     if (lds > 160 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the LDS visited bitmap (v1 limit)");
     int occ = 0;
-    if (use_do) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_do_kernel, DO_THREADS, lds));
+    if (gbm) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_do_kernel<true>, DO_THREADS, lds));
+    else if (use_do) HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_do_kernel<false>, DO_THREADS, lds));
     else HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_global_kernel, VGA_THREADS, lds));
     if (occ < 1) occ = 1;
     const int64_t nsrc = se - sb;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cu * occ, nsrc));
     DevBuf<int32_t> frontier;
     HIPCHK(frontier.alloc((size_t)blocks * 2 * std::max<int64_t>(N, 1)));
+    DevBuf<unsigned long long> gbm_buf;
+    if (gbm) HIPCHK(gbm_buf.alloc((size_t)blocks * 3 * tw * th));
     DevBuf<float> d_out;
     float* outp = out;
     if (!out_on_device) {
@@ -842,9 +1019,11 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     if (const char* k = getenv("DMX_VGA_KSHORT")) Q.kshort = atoi(k);
     Q.work_counter = P.work_counter; Q.scratch = frontier.p; Q.nnodes = N; Q.maxlev = maxlev;
     Q.out = outp; Q.levels_out = P.levels_out; Q.error = P.error; Q.stats = P.stats;
+    Q.gbm = gbm ? gbm_buf.p : nullptr;
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (nsrc > 0) {
-        if (use_do) hipLaunchKernelGGL(vga_do_kernel, dim3((unsigned)blocks), dim3(DO_THREADS), lds, ctx->stream, Q);
+        if (gbm) hipLaunchKernelGGL(vga_do_kernel<true>, dim3((unsigned)blocks), dim3(DO_THREADS), lds, ctx->stream, Q);
+        else if (use_do) hipLaunchKernelGGL(vga_do_kernel<false>, dim3((unsigned)blocks), dim3(DO_THREADS), lds, ctx->stream, Q);
         else hipLaunchKernelGGL(vga_global_kernel, dim3((unsigned)blocks), dim3(VGA_THREADS), lds, ctx->stream, P);
         HIPCHK(hipGetLastError());
     }
@@ -856,8 +1035,11 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     int hc[2];
     HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level/frontier capacity");
-    unsigned long long st[5];
+    unsigned long long st[8];
     HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+    ctx->last_stats[8] = (long long)st[5];   // bottom-up cells that scanned all their runs without a hit
+    ctx->last_stats[9] = (long long)st[6];   // runs read by those
+    ctx->last_stats[10] = gbm ? 1 : 0;
     ctx->last_stats[3] = (long long)(use_do ? (g->symmetric ? 2 : 1) : 0) | ((long long)g->nspecial << 8);
     ctx->last_stats[4] = (long long)st[0];
     ctx->last_stats[5] = (long long)(st[3] | (st[4] << 32));                 // bottom-up | top-down levels

@@ -50,7 +50,9 @@ struct VgaDoParams {
     float* out;
     int64_t* levels_out;
     int* error;
-    unsigned long long* stats;  // [0] runs read, [2] cells reached, [3] bottom-up levels, [4] top-down levels
+    unsigned long long* stats;  // [0] runs read, [2] cells reached, [3] bottom-up levels, [4] top-down levels,
+                                // [5] bottom-up cells that scanned every run without a hit, [6] their runs
+    unsigned long long* gbm;    // GBM variant: per workgroup 3*tw*th words (V, F, X) in HBM
 };
 
 constexpr int DO_THREADS = 256;
@@ -58,7 +60,7 @@ constexpr int DO_THREADS = 256;
 __device__ __forceinline__ double do_plog2(double a) { return log(a) * 1.4426950408889634073599246810019; }
 
 // VGAVisualGlobal measures (vgavisualglobal.cpp:131-193) from the level histogram.
-__device__ void vga_measures(const int* hist, int nlev, float* o, long long& tn, long long& td) {
+__device__ __noinline__ void vga_measures(const int* hist, int nlev, float* o, long long& tn, long long& td) {
     long long total_nodes = 0, total_depth = 0;
     for (int l = 0; l < nlev; l++) { total_nodes += hist[l]; total_depth += (long long)l * hist[l]; }
     float r[7];
@@ -158,20 +160,22 @@ struct DoShared {
     unsigned long long tdnew;       // cells discovered so far in a top-down level
 };
 
+// GBM = false: V/F/X bitmaps in LDS (grids up to ~1.7e5 cells); true: in HBM (per-workgroup slice).
+template <bool GBM>
 __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nt = P.tw * P.th;
-    unsigned long long* V = (unsigned long long*)smem;
+    unsigned long long* V = GBM ? P.gbm + (size_t)blockIdx.x * 3 * nt : (unsigned long long*)smem;
     unsigned long long* F = V + nt;
     unsigned long long* X = F + nt;
-    int* hist = (int*)(X + nt);
+    int* hist = GBM ? (int*)smem : (int*)(X + nt);
     DoShared* S = (DoShared*)(hist + P.maxlev + 4);
     __shared__ int s_src;
     const int tid = threadIdx.x, lane = tid & 63;
     int32_t* list = P.scratch + (size_t)blockIdx.x * 2 * P.nnodes;
     int32_t* hard = list + P.nnodes;
     const int rows = P.rows, tw = P.tw;
-    unsigned long long runs_read = 0;
+    unsigned long long runs_read = 0, fail_cells = 0, fail_runs = 0;
 
     for (;;) {
         if (tid == 0) s_src = atomicAdd(P.work_counter, 1);
@@ -245,6 +249,9 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                         atomicOr(&X[(y >> 3) * tw + (x >> 3)], 1ull << ((y & 7) * 8 + (x & 7)));
                     } else if (nr > lim) {
                         hard[atomicAdd(&S->hard_n, 1)] = c;
+                    } else {
+                        fail_cells++;
+                        fail_runs += nr;
                     }
                 }
                 __syncthreads();
@@ -305,6 +312,7 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                         const int x = c / rows, y = c % rows;
                         atomicOr(&X[(y >> 3) * tw + (x >> 3)], 1ull << ((y & 7) * 8 + (x & 7)));
                     }
+                    if (!found && lane == 0) { fail_cells++; fail_runs += nr; }
                 }
                 __syncthreads();
                 for (int i = tid; i < nt; i += DO_THREADS) V[i] |= X[i];
@@ -395,8 +403,13 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
         }
         __syncthreads();
     }
-    for (int off = 32; off >= 1; off >>= 1) runs_read += __shfl_xor(runs_read, off);
+    for (int off = 32; off >= 1; off >>= 1) {
+        runs_read += __shfl_xor(runs_read, off);
+        fail_cells += __shfl_xor(fail_cells, off);
+        fail_runs += __shfl_xor(fail_runs, off);
+    }
     if (lane == 0 && runs_read) atomicAdd(&P.stats[0], runs_read);
+    if (lane == 0 && fail_cells) { atomicAdd(&P.stats[5], fail_cells); atomicAdd(&P.stats[6], fail_runs); }
 }
 
 // ---------------------------------------------------------------- symmetry / in-set corrections
@@ -558,37 +571,55 @@ __global__ void cov_tiles_kernel(int cols, int rows, int tw, int th, const int32
     if (w) atomicAdd(count, (unsigned long long)__popcll(w));
 }
 
-// Scan pool: each node's runs bucketed longest-first (bucket = floor(log2(cells)), 16 buckets), so a
-// bottom-up cell tests its most likely hits first.  One workgroup per node; also fills the
-// cell-indexed start / count arrays.
+// Scan pool: each node's runs in bottom-up scan order.  Runs are split into the 8 angular groups of
+// 4 bins (bins 4g..4g+3), ordered longest-first inside a group (16 log2-length buckets), and the
+// groups are interleaved round-robin: the first 8 entries are the longest run of each direction, so
+// a cell hidden from the frontier in some directions still finds a hit early.  One workgroup per
+// node; also fills the cell-indexed start / count arrays.
 __global__ void scan_pool_kernel(int rows, const int32_t* node_cell, int64_t n, const int64_t* node_run_start,
-                                 const int32_t* node_nruns, const Run* pool, const int64_t* scan_start, Run* scan_pool,
-                                 int64_t* cell_scan_start, int32_t* cell_nruns) {
-    __shared__ int cnt[16], cur[16];
+                                 const int32_t* node_nruns, const int32_t* bin_nruns, const Run* pool,
+                                 const int64_t* scan_start, Run* scan_pool, int64_t* cell_scan_start, int32_t* cell_nruns) {
+    __shared__ int cnt[8][16], cur[8][16], ng[8], pre[33];
     for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
         const int64_t rs = node_run_start[k], ss = scan_start[k];
         const int nr = node_nruns[k];
-        if (threadIdx.x < 16) cnt[threadIdx.x] = 0;
+        if (threadIdx.x < 128) cnt[threadIdx.x >> 4][threadIdx.x & 15] = 0;
+        if (threadIdx.x < 32) pre[threadIdx.x + 1] = bin_nruns[k * 32 + threadIdx.x];
+        if (threadIdx.x == 0) pre[0] = 0;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int b = 1; b <= 32; b++) pre[b] += pre[b - 1];
         __syncthreads();
         for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+            int b = 0;
+            while (pre[b + 1] <= r) b++;
             const Run ru = pool[rs + r];
             const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
-            atomicAdd(&cnt[15 - min(15, 31 - __clz(len))], 1);
+            atomicAdd(&cnt[b >> 2][15 - min(15, 31 - __clz(len))], 1);
         }
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (threadIdx.x < 8) {
+            const int g = threadIdx.x;
             int acc = 0;
-            for (int b = 0; b < 16; b++) { cur[b] = acc; acc += cnt[b]; }
+            for (int b = 0; b < 16; b++) { cur[g][b] = acc; acc += cnt[g][b]; }
+            ng[g] = acc;
+        }
+        if (threadIdx.x == 0) {
             const int c = node_cell[k];
             cell_scan_start[c] = ss;
             cell_nruns[c] = nr;
         }
         __syncthreads();
         for (int r = threadIdx.x; r < nr; r += blockDim.x) {
+            int b = 0;
+            while (pre[b + 1] <= r) b++;
+            const int g = b >> 2;
             const Run ru = pool[rs + r];
             const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
-            const int pos = atomicAdd(&cur[15 - min(15, 31 - __clz(len))], 1);
-            scan_pool[ss + pos] = ru;
+            const int p = atomicAdd(&cur[g][15 - min(15, 31 - __clz(len))], 1);   // position inside group g
+            int idx = 0;
+            for (int h = 0; h < 8; h++) idx += min(p, ng[h]) + ((h < g && ng[h] > p) ? 1 : 0);
+            scan_pool[ss + idx] = ru;
         }
         __syncthreads();
     }

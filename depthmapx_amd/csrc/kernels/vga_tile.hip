@@ -1,0 +1,581 @@
+// vga_tile.hip -- K3 v3: tile-resolved, direction-optimising VGA global BFS (+ K4 measures).
+//
+// Same result as VGAVisualGlobal::run (salalib/vgamodules/vgavisualglobal.cpp:23-216; set
+// semantics as in vga.hip / vga_do.hip), organised so that one source costs O(tiles) rather than
+// O(cells) of memory traffic on open plans:
+//   * one workgroup per source (persistent grid); the frontier F is an LDS bitmap in 8x8-cell
+//     tiles (fits 1024x1024-cell grids), while the visited set V and the next level X live in the
+//     registers of the thread that owns each tile (thread tid owns tiles tid + k*NT);
+//   * level 1 is top-down: the source's runs are rasterised into F with LDS atomic ORs;
+//   * later levels are bottom-up (valid because visibility is symmetric; the few asymmetric nodes
+//     are routed through exact in-set corrections, see vga_do.hip):
+//       A. tile level: the owner tests the tile's precomputed common runs CR(t) -- runs whose cells
+//          are visible from EVERY regular cell of the tile -- against F; one hit discovers all of
+//          the tile's unvisited regular cells at once (64 cells per test);
+//       B. cell level: the remaining cells test their KH "head" runs (the longest run of each of
+//          8 angular groups, longest first), a wave per tile, lane = cell, coalesced loads;
+//       C. hard cells scan their whole run list longest-first, 64 runs per wave step (coalesced),
+//          stopping at the first hit.
+//   * top-down is used again only when Beamer's test on cell counts prefers it (small frontier).
+// Prep kernels below build the tile-ordered per-cell arrays, the head runs and CR(t) from the
+// run-length graph in O(runs).
+#include "common.hpp"
+
+namespace dmx {
+
+constexpr int KH = 8;        // head runs per cell (first KH entries of its scan order)
+constexpr int CRK = 4;       // tile-common runs per tile
+constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
+
+struct VgaTileParams {
+    int cols, rows, tw, th;
+    const unsigned long long* seed_tiles;     // cells never discoverable (non-filled, outside U_f, padding)
+    const unsigned long long* regular_tiles;  // U_f cells that are not special (asymmetric)
+    const unsigned long long* nonexp_tiles;   // contextfilled odd cells (radius != -1)
+    const Run* cr;                            // [nt][CRK] tile-common runs, longest first (x0 < 0: none)
+    const Run* heads;                         // [KH][nt*64] tile-ordered head runs (x0 < 0: none)
+    const int64_t* tscan_start;               // [nt*64] start in scan_pool (tile order)
+    const int32_t* tnruns;                    // [nt*64]
+    const Run* scan_pool;
+    const int32_t* node_cell;
+    const int32_t* cell_node;
+    const uint8_t* node_flags;
+    const int64_t* node_run_start;
+    const int32_t* node_nruns;
+    const Run* pool;
+    const int32_t* spec_index;
+    const int32_t* extra_off;
+    const int32_t* extra;
+    const int32_t* missing_off;
+    const int32_t* missing;
+    int64_t src_begin, src_end;
+    int radius, gates_only;
+    int64_t uf_count;
+    int alpha;
+    int* work_counter;
+    unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
+    int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
+    int32_t* list;            // per workgroup [nt*64]: hard cells / frontier cells
+    int maxlev;
+    int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
+    int32_t* nlev_out;        // [N] levels (0: source skipped)
+    int* error;
+    unsigned long long* stats;  // [0] runs tested, [2] cells reached, [3] BU levels, [4] TD levels,
+                                // [5] hard cells without a hit, [6] their runs, [7] tiles resolved by CR
+};
+
+__device__ __forceinline__ int tile_id_of(int x, int y, int tw) {
+    return (((y >> 3) * tw + (x >> 3)) << 6) | ((y & 7) << 3) | (x & 7);
+}
+__device__ __forceinline__ void xy_of_tile_id(int id, int tw, int& x, int& y) {
+    const int t = id >> 6, b = id & 63;
+    x = (t % tw) * 8 + (b & 7);
+    y = (t / tw) * 8 + (b >> 3);
+}
+
+// OR all cells of run `ru` into the tiled bitmap `bm` (LDS or HBM, atomic).
+__device__ __forceinline__ void run_or(unsigned long long* bm, int tw, Run ru) {
+    if (ru.y0 == ru.y1 && ru.x0 != ru.x1) {
+        const int y = ru.y0, rowoff = (y >> 3) * tw, sh = (y & 7) * 8;
+        for (int tx = ru.x0 >> 3; tx <= (ru.x1 >> 3); tx++) {
+            const int lo = max((int)ru.x0, tx * 8) & 7, hi = min((int)ru.x1, tx * 8 + 7) & 7;
+            atomicOr(&bm[rowoff + tx], (unsigned long long)((0xFFu >> (7 - hi)) & (0xFFu << lo) & 0xFFu) << sh);
+        }
+    } else if (ru.x0 == ru.x1 && ru.y0 != ru.y1) {
+        const int x = ru.x0, tx = x >> 3;
+        const unsigned long long col = 0x0101010101010101ull << (x & 7);
+        for (int ty = ru.y0 >> 3; ty <= (ru.y1 >> 3); ty++) {
+            const int lo = max((int)ru.y0, ty * 8) & 7, hi = min((int)ru.y1, ty * 8 + 7) & 7;
+            atomicOr(&bm[ty * tw + tx], col & (~0ull >> (8 * (7 - hi))) & (~0ull << (8 * lo)));
+        }
+    } else {
+        const int dy = (ru.y1 > ru.y0) ? 1 : ((ru.y1 < ru.y0) ? -1 : 0);
+        int y = ru.y0;
+        for (int x = ru.x0; x <= ru.x1; x++, y += dy) atomicOr(&bm[(y >> 3) * tw + (x >> 3)], 1ull << ((y & 7) * 8 + (x & 7)));
+    }
+}
+
+// Xg is written with plain stores by its owner thread and with atomics (performed at L2) by any
+// wave of the workgroup; reads after such phases bypass the CU's L1.
+__device__ __forceinline__ unsigned long long ld_l2(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sync_global() {
+    __threadfence();
+    __syncthreads();
+}
+
+struct TileShared {
+    int src, qn, hn, item;
+    unsigned long long cnt, mass;
+};
+
+// Exact bottom-up test for a node with asymmetric visibility (rare): hit iff some frontier cell u
+// is an in-neighbour, i.e. u in Extra(v), or u in cells(v) and u not in Missing(v).  Whole wave.
+__device__ __forceinline__ bool special_hit(const VgaTileParams& P, const unsigned long long* F, int x, int y, int* nr_out) {
+    const int lane = threadIdx.x & 63;
+    const int tw = P.tw, rows = P.rows;
+    const int node = P.cell_node[x * rows + y];
+    const int si = P.spec_index[node];
+    const int64_t rs = P.node_run_start[node];
+    const int nr = P.node_nruns[node];
+    const int e0 = P.extra_off[si], e1 = P.extra_off[si + 1];
+    const int m0 = P.missing_off[si], m1 = P.missing_off[si + 1];
+    bool h = false;
+    for (int j = e0 + lane; j < e1; j += 64) {
+        const int uc = P.node_cell[P.extra[j]];
+        const int ux = uc / rows, uy = uc % rows;
+        if (F[(uy >> 3) * tw + (ux >> 3)] & (1ull << ((uy & 7) * 8 + (ux & 7)))) h = true;
+    }
+    for (int r = lane; r < nr && !h; r += 64) {
+        const Run ru = P.pool[rs + r];
+        const int dx = (ru.x1 > ru.x0) ? 1 : 0;
+        const int dy = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
+        int cx = ru.x0, cy = ru.y0;
+        for (;;) {
+            if (F[(cy >> 3) * tw + (cx >> 3)] & (1ull << ((cy & 7) * 8 + (cx & 7)))) {
+                const int un = P.cell_node[cx * rows + cy];
+                bool miss = false;
+                for (int j = m0; j < m1; j++) miss |= (P.missing[j] == un);
+                if (!miss) { h = true; break; }
+            }
+            if (cx == ru.x1 && cy == ru.y1) break;
+            cx += dx;
+            cy += dy;
+        }
+    }
+    *nr_out = nr;
+    return __ballot(h) != 0ull;
+}
+
+// V (visited) and X (next level) are per-workgroup bitmaps in HBM (they stay in the L2/MALL; a
+// source touches each word a few times), F (frontier, read by every run test) is in LDS.
+template <int NT>
+__global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long F[];
+    __shared__ TileShared S;
+    constexpr int NW = NT / 64;
+    const int nt = P.tw * P.th;
+    int* hist = (int*)(F + nt);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tw = P.tw, rows = P.rows;
+    unsigned long long* Vg = P.xg + (size_t)blockIdx.x * 2 * nt;
+    unsigned long long* Xg = Vg + nt;
+    int4* Q = P.queue + (size_t)blockIdx.x * nt;
+    int32_t* L = P.list + (size_t)blockIdx.x * nt * 64;
+    const size_t hstride = (size_t)nt * 64;
+    unsigned long long runs_tested = 0, fail_cells = 0, fail_runs = 0, cr_tiles = 0;
+
+    if (tid == 0) { S.qn = 0; S.hn = 0; S.item = 0; S.cnt = 0; S.mass = 0; }
+    for (;;) {
+        if (tid == 0) S.src = atomicAdd(P.work_counter, 1);
+        __syncthreads();
+        const int64_t src = P.src_begin + S.src;
+        __syncthreads();
+        if (src >= P.src_end) break;
+        const int scell = P.node_cell[src];
+        const int sx = scell / rows, sy = scell % rows;
+        // VGAVisualGlobal::run: context-filled odd sources and gates_only are skipped (:72-75)
+        if (((P.node_flags[src] & 1) && !((sx % 2) == 0 && (sy % 2) == 0)) || P.gates_only) {
+            if (tid == 0) P.nlev_out[src] = 0;
+            continue;
+        }
+        const int stile = (sy >> 3) * tw + (sx >> 3);
+        const unsigned long long sbit = 1ull << ((sy & 7) * 8 + (sx & 7));
+        for (int t = tid; t < nt; t += NT) {
+            Vg[t] = P.seed_tiles[t] | (t == stile ? sbit : 0ull);
+            Xg[t] = 0ull;
+            F[t] = 0ull;
+        }
+        for (int i = tid; i < VGA_HMAX; i += NT) hist[i] = 0;
+        const bool s_in_uf = !(P.seed_tiles[stile] & sbit);
+        const long long target = P.uf_count - (s_in_uf ? 1 : 0);
+        long long m_f = 1, m_u = target, discovered = 0;
+        int level = 0, nlev = 1;
+        bool overflow = false;
+        __syncthreads();
+        if (tid == 0) hist[0] = 1;
+        for (;;) {
+            if (P.radius != -1 && level >= P.radius) break;
+            if (discovered >= target) break;
+            const bool bottom_up = level > 0 && (m_f * (long long)P.alpha > m_u);
+            if (level == 0) {
+                // ---- level 1: rasterise the source's runs (top-down from {s})
+                const int64_t rs = P.node_run_start[src];
+                const int nr = P.node_nruns[src];
+                for (int r = tid; r < nr; r += NT) run_or(F, tw, P.pool[rs + r]);
+                if (tid < nr) runs_tested += (unsigned long long)((nr - tid + NT - 1) / NT);
+                sync_global();
+                for (int t = tid; t < nt; t += NT) Xg[t] = F[t] & ~Vg[t];
+            } else if (bottom_up) {
+                // ---- A: tile-common runs
+                for (int t0 = 0; t0 < nt; t0 += NT) {
+                    const int t = t0 + tid;
+                    unsigned long long U = 0ull;
+                    if (t < nt) {
+                        U = ~Vg[t];
+                        const unsigned long long R = U & P.regular_tiles[t];
+                        if (R) {
+                            bool hit = false;
+                            for (int j = 0; j < CRK && !hit; j++) {
+                                const Run c = P.cr[CRK * t + j];
+                                if (c.x0 < 0) break;
+                                runs_tested++;
+                                hit = run_hits(F, tw, c);
+                            }
+                            if (hit) { Xg[t] = R; U &= ~R; cr_tiles++; }
+                        }
+                    }
+                    const unsigned long long want = __ballot(U != 0ull);
+                    if (want) {
+                        int base = 0;
+                        if (lane == 0) base = atomicAdd(&S.qn, __popcll(want));
+                        base = __shfl(base, 0);
+                        if (U) {
+                            const int pos = base + __popcll(want & ((1ull << lane) - 1ull));
+                            Q[pos] = make_int4(t, 0, (int)(unsigned)(U & 0xFFFFFFFFull), (int)(unsigned)(U >> 32));
+                        }
+                    }
+                }
+                sync_global();
+                const int qn = S.qn;
+                // ---- B: head runs, one wave per queued tile, lane = cell
+                for (int it = wave; it < qn; it += NW) {
+                    const int4 e = Q[it];
+                    const int t = e.x;
+                    const unsigned long long mask = (unsigned long long)(unsigned)e.z | ((unsigned long long)(unsigned)e.w << 32);
+                    bool hit = false, to_hard = false;
+                    int hard_val = 0;
+                    if ((mask >> lane) & 1ull) {
+                        const int id = (t << 6) | lane;
+                        if (!((P.regular_tiles[t] >> lane) & 1ull)) {
+                            to_hard = true;
+                            hard_val = -1 - id;   // special node: exact path
+                        } else {
+                            int h = 0;
+                            for (; h < KH; h++) {
+                                const Run hr = P.heads[h * hstride + id];
+                                if (hr.x0 < 0) break;
+                                if (run_hits(F, tw, hr)) { hit = true; h++; break; }
+                            }
+                            runs_tested += h;
+                            if (!hit) {
+                                const int nr = P.tnruns[id];
+                                if (nr > h) { to_hard = true; hard_val = id; }
+                                else { fail_cells++; fail_runs += nr; }
+                            }
+                        }
+                    }
+                    const unsigned long long hm = __ballot(hit);
+                    if (lane == 0 && hm) atomicOr(&Xg[t], hm);
+                    const unsigned long long hw = __ballot(to_hard);
+                    if (hw) {
+                        int base = 0;
+                        if (lane == 0) base = atomicAdd(&S.hn, __popcll(hw));
+                        base = __shfl(base, 0);
+                        if (to_hard) L[base + __popcll(hw & ((1ull << lane) - 1ull))] = hard_val;
+                    }
+                }
+                sync_global();
+                const int hn = S.hn;
+                // ---- C: hard cells, a wave scans 64 runs at a time (dynamic work counter)
+                for (;;) {
+                    int it = 0;
+                    if (lane == 0) it = atomicAdd(&S.item, 1);
+                    it = __shfl(it, 0);
+                    if (it >= hn) break;
+                    int id = L[it];
+                    const bool special = id < 0;
+                    if (special) id = -1 - id;
+                    bool found = false;
+                    int nr = 0;
+                    if (special) {
+                        int x, y;
+                        xy_of_tile_id(id, tw, x, y);
+                        found = special_hit(P, F, x, y, &nr);
+                        if (lane == 0) runs_tested += (unsigned long long)nr;
+                    } else {
+                        const int64_t rs = P.tscan_start[id];
+                        nr = P.tnruns[id];
+                        int base = KH;   // the first KH runs (the heads) were tested in phase B
+                        for (; base < nr && !found; base += 64) {
+                            const int r = base + lane;
+                            const bool h = (r < nr) && run_hits(F, tw, P.scan_pool[rs + r]);
+                            found = __ballot(h) != 0ull;
+                        }
+                        if (lane == 0) runs_tested += (unsigned long long)(min(base, nr) - KH);
+                    }
+                    if (lane == 0) {
+                        if (found) atomicOr(&Xg[id >> 6], 1ull << (id & 63));
+                        else { fail_cells++; fail_runs += (unsigned long long)nr; }
+                    }
+                }
+            } else {
+                // ---- top-down from the frontier F (small frontier): push runs into Xg, mask with V
+                for (int t = tid; t < nt; t += NT) {
+                    unsigned long long f = F[t];
+                    const int c = __popcll(f);
+                    int pos = c ? atomicAdd(&S.hn, c) : 0;
+                    while (f) {
+                        const int b = __ffsll((long long)f) - 1;
+                        f &= f - 1;
+                        L[pos++] = (t << 6) | b;
+                    }
+                }
+                sync_global();
+                const int fn = S.hn;
+                for (;;) {
+                    int it = 0;
+                    if (lane == 0) it = atomicAdd(&S.item, 1);
+                    it = __shfl(it, 0);
+                    if (it >= fn) break;
+                    int x, y;
+                    xy_of_tile_id(L[it], tw, x, y);
+                    const int node = P.cell_node[x * rows + y];
+                    const int64_t rs = P.node_run_start[node];
+                    const int nr = P.node_nruns[node];
+                    for (int r = lane; r < nr; r += 64) run_or(Xg, tw, P.pool[rs + r]);
+                    if (lane == 0) runs_tested += (unsigned long long)nr;
+                }
+                sync_global();
+                __threadfence();
+                for (int t = tid; t < nt; t += NT) Xg[t] = ld_l2(&Xg[t]) & ~Vg[t];
+            }
+            sync_global();
+            __threadfence();
+            // ---- level bookkeeping: count X, publish the expandable part as the next frontier
+            unsigned long long c_loc = 0, m_loc = 0;
+            for (int t = tid; t < nt; t += NT) {
+                unsigned long long x = ld_l2(&Xg[t]);
+                if (x) {
+                    c_loc += (unsigned long long)__popcll(x);
+                    Vg[t] |= x;
+                    Xg[t] = 0ull;
+                    if (P.radius != -1) x &= ~P.nonexp_tiles[t];
+                    m_loc += (unsigned long long)__popcll(x);
+                }
+                F[t] = x;
+            }
+            for (int off = 32; off >= 1; off >>= 1) {
+                c_loc += __shfl_xor(c_loc, off);
+                m_loc += __shfl_xor(m_loc, off);
+            }
+            if (lane == 0 && c_loc) { atomicAdd(&S.cnt, c_loc); atomicAdd(&S.mass, m_loc); }
+            sync_global();
+            const long long cnt = (long long)S.cnt, mass = (long long)S.mass;
+            __syncthreads();
+            if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; }
+            if (cnt == 0) break;
+            if (level + 1 >= VGA_HMAX) { overflow = true; break; }
+            if (tid == 0) hist[level + 1] = (int)cnt;
+            discovered += cnt;
+            m_u -= cnt;
+            m_f = mass;
+            level++;
+            nlev = level + 1;
+            if (tid == 0) atomicAdd(&P.stats[bottom_up ? 3 : 4], 1ull);
+        }
+        __syncthreads();
+        if (overflow) {
+            if (tid == 0) atomicOr(P.error, KERR_LEVELS);
+            continue;
+        }
+        for (int l = tid; l < nlev; l += NT) P.hist_out[src * VGA_HMAX + l] = hist[l];
+        if (tid == 0) P.nlev_out[src] = nlev;
+        __syncthreads();
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        runs_tested += __shfl_xor(runs_tested, off);
+        fail_cells += __shfl_xor(fail_cells, off);
+        fail_runs += __shfl_xor(fail_runs, off);
+        cr_tiles += __shfl_xor(cr_tiles, off);
+    }
+    if (lane == 0) {
+        if (runs_tested) atomicAdd(&P.stats[0], runs_tested);
+        if (fail_cells) { atomicAdd(&P.stats[5], fail_cells); atomicAdd(&P.stats[6], fail_runs); }
+        if (cr_tiles) atomicAdd(&P.stats[7], cr_tiles);
+    }
+}
+
+// ---------------------------------------------------------------- prep: tile-ordered cell arrays
+__device__ __forceinline__ int run_len(Run ru) {
+    return max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+}
+
+// Tile-ordered scan start / run count per cell, and its KH head runs (the first KH entries of its
+// scan order: the longest run of each angular group).  One thread per node.
+__global__ void tile_heads_kernel(int rows, int tw, const int32_t* node_cell, int64_t n, const int32_t* node_nruns,
+                                  const Run* scan_pool, const int64_t* scan_start, int64_t* tscan_start, int32_t* tnruns,
+                                  Run* heads, size_t hstride) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int c = node_cell[k];
+    const int id = tile_id_of(c / rows, c % rows, tw);
+    const int64_t ss = scan_start[k];
+    const int nr = node_nruns[k];
+    tscan_start[id] = ss;
+    tnruns[id] = nr;
+    for (int h = 0; h < KH && h < nr; h++) heads[h * hstride + id] = scan_pool[ss + h];
+}
+
+// Lattice segment: cells (x0 + p*dx, y0 + p*dy), p = 0..len-1 (dx in {0,1}, dy in {-1,0,1}).
+struct LSeg {
+    int x0, y0, dx, dy, len;
+};
+__device__ __forceinline__ LSeg lseg_of(Run ru) {
+    LSeg s;
+    s.x0 = ru.x0;
+    s.y0 = ru.y0;
+    if (ru.y0 == ru.y1) { s.dx = 1; s.dy = 0; s.len = ru.x1 - ru.x0 + 1; }
+    else if (ru.x0 == ru.x1) { s.dx = 0; s.dy = 1; s.len = ru.y1 - ru.y0 + 1; }
+    else { s.dx = 1; s.dy = (ru.y1 > ru.y0) ? 1 : -1; s.len = ru.x1 - ru.x0 + 1; }
+    return s;
+}
+// Positions [*pa, *pb] of candidate `c` covered by segment `s` (empty if *pa > *pb).
+__device__ __forceinline__ void lseg_overlap(const LSeg& c, const LSeg& s, int* pa, int* pb) {
+    *pa = 1;
+    *pb = 0;
+    const int ux = s.x0 - c.x0, uy = s.y0 - c.y0;
+    const int det = -c.dx * s.dy + s.dx * c.dy;
+    if (det == 0) {
+        // parallel: same lattice line iff (ux, uy) is collinear with (dx, dy)
+        if (ux * c.dy - uy * c.dx != 0) return;
+        const int a = c.dx ? ux : uy;
+        *pa = max(a, 0);
+        *pb = min(a + s.len - 1, c.len - 1);
+        return;
+    }
+    // p*c.d - q*s.d = u  (Cramer)
+    const int pn = -ux * s.dy + s.dx * uy, qn = c.dx * uy - c.dy * ux;
+    if (pn % det != 0 || qn % det != 0) return;
+    const int p = pn / det, q = qn / det;
+    if (p < 0 || p >= c.len || q < 0 || q >= s.len) return;
+    *pa = p;
+    *pb = p;
+}
+
+// CR(t): up to two runs whose cells are visible from every regular cell of tile t.  Candidates are
+// the group-longest runs of the tile's most central regular cell; every regular cell's runs are
+// intersected with them through LDS difference arrays (O(runs) per tile).
+constexpr int CR_THREADS = 256;
+__global__ void __launch_bounds__(CR_THREADS) tile_cr_kernel(int cols, int rows, int tw, int th,
+                                                             const unsigned long long* regular_tiles,
+                                                             const int32_t* cell_node, const int64_t* node_run_start,
+                                                             const int32_t* node_nruns, const int64_t* scan_start,
+                                                             const Run* scan_pool, const Run* pool, int dmax, Run* cr) {
+    extern __shared__ __attribute__((aligned(16))) int diff[];   // [8][dmax + 2]
+    __shared__ LSeg cand[8];
+    __shared__ int bestlen[8], beststart[8];
+    const int nt = tw * th;
+    const int tid = threadIdx.x;
+    const int stride = dmax + 2;
+    for (int t = blockIdx.x; t < nt; t += gridDim.x) {
+        const unsigned long long R = regular_tiles[t];
+        const int tx = t % tw, ty = t / tw;
+        if (R == 0ull) {
+            if (tid < CRK) { Run z; z.x0 = z.y0 = z.x1 = z.y1 = -1; cr[CRK * t + tid] = z; }
+            continue;
+        }
+        const int nreg = __popcll(R);
+        // most central regular cell (ties: lowest bit); its first 8 scan entries are the candidates
+        int cb = 0, cd = 1 << 30;
+        for (int b = 0; b < 64; b++)
+            if ((R >> b) & 1ull) {
+                const int d = (2 * (b & 7) - 7) * (2 * (b & 7) - 7) + (2 * (b >> 3) - 7) * (2 * (b >> 3) - 7);
+                if (d < cd) { cd = d; cb = b; }
+            }
+        const int ck = cell_node[(tx * 8 + (cb & 7)) * rows + ty * 8 + (cb >> 3)];
+        for (int i = tid; i < 8 * stride; i += CR_THREADS) diff[i] = 0;
+        if (tid < 8) {
+            const int nrc = node_nruns[ck];
+            if (tid < nrc) cand[tid] = lseg_of(scan_pool[scan_start[ck] + tid]);
+            else cand[tid].len = 0;
+        }
+        __syncthreads();
+        // coverage counts: every regular cell's runs against the 8 candidates (difference arrays;
+        // one cell's runs are disjoint, so a position counts each regular cell at most once)
+        for (int b = 0; b < 64; b++) {
+            if (!((R >> b) & 1ull)) continue;
+            const int wk = cell_node[(tx * 8 + (b & 7)) * rows + ty * 8 + (b >> 3)];
+            const int64_t rs = node_run_start[wk];
+            const int nr = node_nruns[wk];
+            for (int r = tid; r < nr; r += CR_THREADS) {
+                const LSeg s = lseg_of(pool[rs + r]);
+                for (int g = 0; g < 8; g++) {
+                    const LSeg c = cand[g];
+                    if (c.len == 0) continue;
+                    int pa, pb;
+                    lseg_overlap(c, s, &pa, &pb);
+                    if (pa <= pb) {
+                        atomicAdd(&diff[g * stride + pa], 1);
+                        atomicAdd(&diff[g * stride + pb + 1], -1);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < 8) {
+            const LSeg c = cand[tid];
+            int bl = 0, bs = 0, cur = 0, run = 0, rstart = 0;
+            for (int p = 0; p < c.len; p++) {
+                cur += diff[tid * stride + p];
+                if (cur == nreg) {
+                    if (run == 0) rstart = p;
+                    run++;
+                    if (run > bl) { bl = run; bs = rstart; }
+                } else {
+                    run = 0;
+                }
+            }
+            bestlen[tid] = bl;
+            beststart[tid] = bs;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            // the CRK longest common intervals, longest first
+            int used = 0;
+            for (int j = 0; j < CRK; j++) {
+                int pick = -1;
+                for (int g = 0; g < 8; g++)
+                    if (bestlen[g] > 0 && !((used >> g) & 1) && (pick < 0 || bestlen[g] > bestlen[pick])) pick = g;
+                Run z;
+                z.x0 = z.y0 = z.x1 = z.y1 = -1;
+                if (pick >= 0) {
+                    used |= 1 << pick;
+                    const LSeg c = cand[pick];
+                    const int pa = beststart[pick], pb = pa + bestlen[pick] - 1;
+                    z.x0 = (int16_t)(c.x0 + pa * c.dx);
+                    z.y0 = (int16_t)(c.y0 + pa * c.dy);
+                    z.x1 = (int16_t)(c.x0 + pb * c.dx);
+                    z.y1 = (int16_t)(c.y0 + pb * c.dy);
+                }
+                cr[CRK * t + j] = z;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// K4: the 7 VGA measures per source from its level histogram (vgavisualglobal.cpp:131-193).
+__global__ void vga_measures_kernel(int64_t sb, int64_t se, const int32_t* hist_all, const int32_t* nlev_all, float* out,
+                                    int64_t* levels_out, unsigned long long* stats) {
+    const int64_t src = sb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (src >= se) return;
+    const int nlev = nlev_all[src];
+    float* o = out + src * 7;
+    if (nlev == 0) {   // skipped source (context-filled odd cell / gates_only)
+        for (int i = 0; i < 7; i++) o[i] = -1.0f;
+        if (levels_out) { levels_out[src * 3] = 0; levels_out[src * 3 + 1] = 0; levels_out[src * 3 + 2] = 0; }
+        return;
+    }
+    long long tn, td;
+    vga_measures(hist_all + src * VGA_HMAX, nlev, o, tn, td);
+    if (levels_out) {
+        levels_out[src * 3 + 0] = tn;
+        levels_out[src * 3 + 1] = td;
+        levels_out[src * 3 + 2] = nlev;
+    }
+    atomicAdd(&stats[2], (unsigned long long)tn);
+}
+
+} // namespace dmx

@@ -42,16 +42,17 @@ class Context:
         return mk.value, vg.value
 
     def last_stats(self):
-        out = np.zeros(8, dtype=np.int64)
-        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 8))
+        out = np.zeros(16, dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 16))
         keys = ["mk_cells_examined", "mk_visible_pairs", "mk_runs", "vga_kernel", "vga_runs_expanded", "vga_levels",
-                "vga_cells_reached", "vga_sources"]
+                "vga_cells_reached", "vga_sources", "vga_fail_cells", "vga_fail_runs", "vga_hbm_bitmaps",
+                "vga_cr_tiles", "vga_launch"]
         d = {k: int(v) for k, v in zip(keys, out)}
         lv = d.pop("vga_levels")
         d["vga_bottom_up_levels"], d["vga_top_down_levels"] = lv & 0xFFFFFFFF, lv >> 32
         d["vga_special_nodes"] = d["vga_kernel"] >> 8
         d["vga_kernel"] = ["topdown-v1", "direction-optimizing(top-down only)",
-                           "direction-optimizing"][d["vga_kernel"] & 0xFF]
+                           "direction-optimizing", "tile-resolved"][d["vga_kernel"] & 0xFF]
         return d
 
 

@@ -15,6 +15,7 @@
 #endif
 
 #define M_1_LN2_ 1.4426950408889634073599246810019
+#define M_PI_ 3.14159265358979323846
 
 /* Point::m_state bits (salalib/point.h:32-38) */
 enum { ST_EMPTY = 0x1, ST_FILLED = 0x2, ST_BLOCKED = 0x4, ST_CONTEXTFILLED = 0x8, ST_EDGE = 0x20 };
@@ -973,5 +974,137 @@ int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t nb, int6
         for (int i = 0; i < 4096; i++) free(levels[i].p);
         free(miscs); free(extx); free(exty); free(dist);
     }
+    return 0;
+}
+
+/* ---------------------------------------------------------------- VGA metric step depth */
+/* MetricTriple (salalib/pointdata.h:377-399): std::set ordered by (dist, pixel); two triples with
+ * equal dist and pixel are the same key, so a second insert keeps the first lastpixel. */
+typedef struct { float dist; int32_t pix; int32_t last; } MTrip;
+static int mt_less(const MTrip* a, const MTrip* b) {
+    return a->dist < b->dist || (a->dist == b->dist && a->pix < b->pix);
+}
+typedef struct { MTrip* a; int64_t n, cap; } MHeap;
+static void mh_push(MHeap* h, MTrip t) {
+    if (h->n == h->cap) { h->cap = h->cap ? 2 * h->cap : 1024; h->a = (MTrip*)realloc(h->a, h->cap * sizeof(MTrip)); }
+    int64_t i = h->n++;
+    while (i > 0) {
+        int64_t p = (i - 1) / 2;
+        if (!mt_less(&t, &h->a[p])) break;
+        h->a[i] = h->a[p];
+        i = p;
+    }
+    h->a[i] = t;
+}
+static MTrip mh_pop(MHeap* h) {
+    MTrip top = h->a[0], last = h->a[--h->n];
+    int64_t i = 0;
+    for (;;) {
+        int64_t c = 2 * i + 1;
+        if (c >= h->n) break;
+        if (c + 1 < h->n && mt_less(&h->a[c + 1], &h->a[c])) c++;
+        if (!mt_less(&h->a[c], &last)) break;
+        h->a[i] = h->a[c];
+        i = c;
+    }
+    if (h->n) h->a[i] = last;
+    return top;
+}
+static inline int32_t pix_int(int x, int y) { return (int32_t)(((uint32_t)x << 16) + ((uint32_t)y & 0xffff)); } /* pixelref.h:81 */
+static inline double pix_dist(int ax, int ay, int bx, int by) { /* pixelref.h:116-119 */
+    int dx = ax - bx, dy = ay - by;
+    return sqrt((double)(dx * dx + dy * dy));
+}
+static inline double pix_angle(int ax, int ay, int bx, int by, int cx, int cy) { /* pixelref.h:121-131 */
+    return acos((double)((ax - bx) * (bx - cx) + (ay - by) * (by - cy)) /
+                (sqrt((double)((ax - bx) * (ax - bx) + (ay - by) * (ay - by))) *
+                     sqrt((double)((bx - cx) * (bx - cx) + (by - cy) * (by - cy))) + 1e-12));
+}
+/* PointMap::blockedAdjacent (pointdata.cpp:1016-1068) */
+static int blocked_adjacent(const dmxo_map* m, int x, int y) {
+    static const int dx[8] = {1, 1, 0, -1, -1, -1, 0, 1}, dy[8] = {0, 1, 1, 1, 0, -1, -1, -1};
+    for (int i = 0; i < 8; i++) {
+        int nx = x + dx[i], ny = y + dy[i];
+        if (incl(m, nx, ny) && (m->state[cidx(m, nx, ny)] & ST_BLOCKED)) return 1;
+    }
+    return 0;
+}
+
+int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out) {
+    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
+    for (int64_t i = 0; i < 3 * N; i++) out[i] = -1.0f;
+    if (nsel <= 0) return -1;
+    float* mdist = (float*)malloc(C * sizeof(float));
+    float* cum = (float*)calloc(C, sizeof(float));
+    int32_t* misc = (int32_t*)calloc(C, sizeof(int32_t));
+    Vec* ins = (Vec*)calloc(C, sizeof(Vec)); /* dists inserted per cell (std::set key dedupe) */
+    for (int64_t c = 0; c < C; c++) mdist[c] = -1.0f;
+    MHeap h = {0, 0, 0};
+    /* std::set<int> getSelSet() order; every selected cell enters at dist 0 (vgametricdepth.cpp:45-47) */
+    int32_t sx0 = 0, sy0 = 0;
+    for (int64_t i = 0; i < nsel; i++) {
+        int32_t c = sel_cells[i];
+        int x = c / m->rows, y = c % m->rows;
+        if (i == 0) { sx0 = x; sy0 = y; }
+        MTrip t = {0.0f, pix_int(x, y), -1};
+        float* d = (float*)vec_push(&ins[c], sizeof(float));
+        *d = 0.0f;
+        mh_push(&h, t);
+    }
+    while (h.n) {
+        MTrip here = mh_pop(&h);
+        int hx = here.pix >> 16, hy = here.pix & 0xffff;
+        int64_t hc = cidx(m, hx, hy);
+        if (!(m->state[hc] & ST_FILLED) || misc[hc] == ~0) continue;
+        if (here.dist == 0.0f || (m->state[hc] & ST_BLOCKED) || blocked_adjacent(m, hx, hy)) {
+            /* Node::extractMetric / Bin::extractMetric (ngraph.cpp:67-76, :330-345) */
+            const NodeG* nd = &m->nodes[m->node_of_cell[hc]];
+            const Run* r = nd->runs;
+            int lx = here.last >> 16, ly = here.last & 0xffff;
+            for (int b = 0; b < 32; b++) {
+                char dir = nd->dir[b];
+                for (int k = 0; k < nd->nruns[b]; k++, r++) {
+                    int px = r->x0, py = r->y0;
+                    int endc = (dir & D_V) ? r->y1 : r->x1;
+                    for (;;) {
+                        int col = (dir & D_V) ? py : px;
+                        if (col > endc) break;
+                        int64_t pc = cidx(m, px, py);
+                        /* non-filled cells (diagonal gaps) can be queued but never resolve */
+                        if ((m->state[pc] & ST_FILLED) && misc[pc] == 0) {
+                            double dd = pix_dist(px, py, hx, hy);
+                            if (mdist[pc] == -1.0 || (double)here.dist + dd < (double)mdist[pc]) {
+                                mdist[pc] = here.dist + (float)dd;
+                                cum[pc] = cum[hc] + (here.last == -1 ? 0.0f
+                                                                     : (float)(pix_angle(px, py, hx, hy, lx, ly) / (M_PI_ * 0.5)));
+                                int dup = 0;
+                                for (int64_t q = 0; q < ins[pc].n; q++)
+                                    if (((float*)ins[pc].p)[q] == mdist[pc]) { dup = 1; break; }
+                                if (!dup) {
+                                    float* d = (float*)vec_push(&ins[pc], sizeof(float));
+                                    *d = mdist[pc];
+                                    MTrip t = {mdist[pc], pix_int(px, py), here.pix};
+                                    mh_push(&h, t);
+                                }
+                            }
+                        }
+                        switch (dir) {
+                        case D_PD: px++; py++; break;
+                        case D_ND: px++; py--; break;
+                        case D_H: px++; break;
+                        case D_V: py++; break;
+                        }
+                    }
+                }
+            }
+        }
+        misc[hc] = ~0;
+        float* o = out + 3 * m->node_of_cell[hc];
+        o[0] = cum[hc];
+        o[1] = (float)(m->spacing * here.dist);
+        if (nsel == 1) o[2] = (float)(m->spacing * pix_dist(hx, hy, sx0, sy0));
+    }
+    for (int64_t c = 0; c < C; c++) free(ins[c].p);
+    free(ins); free(h.a); free(mdist); free(cum); free(misc);
     return 0;
 }

@@ -54,6 +54,12 @@ int dmxo_set_graph(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_
 int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t node_begin, int64_t node_end,
                     int nthreads, float* out, int64_t* levels_out);
 
+/* VGAMetricDepth::run (vgamodules/vgametricdepth.cpp:23-92) from the selected cells (x-major cell
+ * indices, in std::set<int> PixelRef order, all FILLED).  out [N][3]: Metric Step Shortest-Path
+ * Angle, Metric Step Shortest-Path Length, Metric Straight-Line Distance (single selection only;
+ * otherwise -1); unreached cells keep -1.  Returns -1 for an empty selection. */
+int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -44,6 +44,8 @@ def lib():
         L.dmxo_get_graph.argtypes = [vp, vp, vp, vp, vp]
         L.dmxo_set_graph.restype = i32
         L.dmxo_set_graph.argtypes = [vp, vp, vp, i64]
+        L.dmxo_metric_stepdepth.restype = i32
+        L.dmxo_metric_stepdepth.argtypes = [vp, vp, i64, vp]
         L.dmxo_vga_global.restype = i32
         L.dmxo_vga_global.argtypes = [vp, dbl, i32, i64, i64, i32, vp, vp]
         _lib = L
@@ -119,3 +121,11 @@ class OracleMap:
         lib().dmxo_vga_global(self.h, float(radius), int(gates_only), node_begin, node_end, threads, _p(out),
                               _p(lv) if lv is not None else None)
         return (out, lv) if levels else out
+
+    def metric_stepdepth(self, sel_cells):
+        """VGAMetricDepth::run from x-major cell indices (std::set<int> PixelRef order).  [N][3]:
+        Shortest-Path Angle, Shortest-Path Length, Straight-Line Distance (single selection)."""
+        sel = np.ascontiguousarray(sel_cells, dtype=np.int32)
+        out = np.full((self.num_nodes, 3), -1.0, dtype=np.float32)
+        lib().dmxo_metric_stepdepth(self.h, _p(sel), len(sel), _p(out))
+        return out

@@ -75,7 +75,7 @@ int main(int argc, char** argv) {
     double spacing = -1, maxdist = -1, radius = -1;
     bool boundary = false, vga = false, roundtrip = false;
     long sources = 0;
-    std::vector<Point2f> fills;
+    std::vector<Point2f> fills, stepPoints;
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() { if (i + 1 >= argc) { fprintf(stderr, "missing arg for %s\n", a.c_str()); exit(2);} return std::string(argv[++i]); };
@@ -91,6 +91,7 @@ int main(int argc, char** argv) {
         else if (a == "--out") outDir = next();
         else if (a == "--write-graph") writeGraph = next();
         else if (a == "--sources") sources = atol(next().c_str());
+        else if (a == "--stepdepth") { std::string p = next(); double x, y; sscanf(p.c_str(), "%lf,%lf", &x, &y); stepPoints.push_back(Point2f(x, y)); }
         else { fprintf(stderr, "unknown arg %s\n", a.c_str()); return 2; }
     }
     MetaGraph mg;
@@ -206,6 +207,34 @@ int main(int argc, char** argv) {
     dump(outDir + "/runs.bin", runs);
     dump(outDir + "/gridconn.bin", gconn);
 
+    double tsd = 0;
+    if (!stepPoints.empty()) {
+        // dm_runmethods::runStepDepth (depthmapXcli/runmethods.cpp:735-778), metric step type
+        for (auto& p : stepPoints) {
+            if (!reg.contains(p)) { fprintf(stderr, "Point outside of target region\n"); return 1; }
+            QtRegion r(p, p);
+            mg.setCurSel(r, true);
+        }
+        std::vector<int> sel(pm.getSelSet().begin(), pm.getSelSet().end());
+        dump(outDir + "/stepdepth_sel.bin", sel);
+        Options opt;
+        opt.global = 0;
+        opt.point_depth_selection = 2;
+        auto a = std::chrono::steady_clock::now();
+        bool done = mg.analyseGraph(nullptr, opt, false);
+        auto b = std::chrono::steady_clock::now();
+        tsd = std::chrono::duration<double>(b - a).count();
+        std::vector<float> sd;
+        const char* names[3] = {"Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length",
+                                "Metric Straight-Line Distance"};
+        std::vector<int> cols3;
+        for (auto n : names) cols3.push_back(done && at.hasColumn(n) ? (int)at.getColumnIndex(n) : -1);
+        for (auto it = at.begin(); it != at.end(); ++it)
+            for (int c : cols3) sd.push_back(c >= 0 ? it->getRow().getValue(c) : -1.0f);
+        dump(outDir + "/stepdepth.bin", sd);
+        pm.clearSel();
+    }
+
     double tv = 0, tvrt = 0;
     if (vga) {
         Options opt;
@@ -246,8 +275,8 @@ int main(int argc, char** argv) {
     fprintf(f, "region %.17g %.17g %.17g %.17g\n", reg.bottom_left.x, reg.bottom_left.y, reg.top_right.x,
             reg.top_right.y);
     fprintf(f, "filled %d\nnodes %ld\nruns %zu\n", pm.m_filled_point_count, nodes, runs.size() / 4);
-    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\n", std::chrono::duration<double>(t1 - t0).count(), tv,
-            tvrt);
+    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\nt_stepdepth %.6f\n",
+            std::chrono::duration<double>(t1 - t0).count(), tv, tvrt, tsd);
     fclose(f);
     printf("ok nodes %ld runs %zu t_makegraph %.3f t_vga %.3f\n", nodes, runs.size() / 4,
            std::chrono::duration<double>(t1 - t0).count(), tv);

@@ -1,0 +1,42 @@
+"""GPU probe: makeGraph + VGA global on a contiguous block of sources of the synthetic W x W grid;
+prints timings and the BFS work counters.  python scripts/probe_big.py W nsources [kernel]"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import depthmapx_amd as dmx  # noqa: E402
+from bench import load_lines  # noqa: E402
+
+W = int(sys.argv[1])
+ns = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+if len(sys.argv) > 3:
+    os.environ["DMX_VGA_KERNEL"] = sys.argv[3]
+ctx = dmx.Context(0)
+pm = dmx.PointMap([0.0, 0.0, float(W), float(W)], load_lines(W, 50), 1.0)
+assert pm.make_points(0.5, 0.5)
+N = pm.info()["filled"]
+t0 = time.time()
+g = pm.make_graph(ctx)
+t1 = time.time()
+print(json.dumps({"W": W, "N": N, "runs": g.info()["nruns"], "makegraph_kernel_s": ctx.last_timing()[0],
+                  "makegraph_wall_s": t1 - t0}), flush=True)
+b = max(0, N // 2 - ns // 2)
+e = min(N, b + ns)
+t0 = time.time()
+g.vga_visual_global(src_begin=b, src_end=b + 1)   # prep (uf, symmetry, tiles)
+t1 = time.time()
+out = g.vga_visual_global(src_begin=b, src_end=e)
+t2 = time.time()
+st = ctx.last_stats()
+nsrc = e - b
+tk = ctx.last_timing()[1]
+print(json.dumps({"prep_wall_s": t1 - t0, "vga_sources": nsrc, "vga_kernel_s": tk, "vga_wall_s": t2 - t1,
+                  "vga_s_per_source": tk / nsrc, "est_full_vga_s": tk / nsrc * N,
+                  "runs_read_per_src": st["vga_runs_expanded"] / nsrc, "fail_cells_per_src": st["vga_fail_cells"] / nsrc,
+                  "fail_runs_per_src": st["vga_fail_runs"] / nsrc, "cr_tiles_per_src": st["vga_cr_tiles"] / nsrc,
+                  "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc,
+                  "levels_td_per_src": st["vga_top_down_levels"] / nsrc, "kernel": st["vga_kernel"],
+                  "launch": st["vga_launch"]}), flush=True)

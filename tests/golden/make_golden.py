@@ -32,6 +32,16 @@ CASES = {
     "syn256mk": ("inputs/syn256.csv", 1.0, ["0.5,0.5"], False, False, False),
 }
 
+# metric step depth selections per case (STEPDEPTH -sdt metric -sdp x,y [-sdp ...])
+STEPDEPTH = {
+    "kat": ["0.25,0.25"],
+    "syn16": ["8.5,8.5"],
+    "syn32": ["16.5,16.5"],
+    "syn64": ["32.5,32.5", "10.5,50.5"],
+    "gallery": ["1.32,7.24"],
+    "barnsbury": ["531000,184000"],
+}
+
 
 def node_digests(bins, runs):
     """64-bit blake2b per node over its 32 bin records (int32 x4) and its runs (int16 x4)."""
@@ -68,6 +78,8 @@ def run_case(name):
             cmd += ["--vga"]
         if rt:
             cmd += ["--roundtrip"]
+        for p in STEPDEPTH.get(name, []):
+            cmd += ["--stepdepth", p]
         print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         g = parse_grid(os.path.join(d, "grid.txt"))
@@ -92,13 +104,17 @@ def run_case(name):
             arrays["vga"] = rd("vga.bin", np.float32).reshape(N, 7)
         if rt:
             arrays["vga_rt"] = rd("vga_rt.bin", np.float32).reshape(N, 7)
+        if name in STEPDEPTH:
+            arrays["stepdepth"] = rd("stepdepth.bin", np.float32).reshape(N, 3)
+            arrays["stepdepth_sel"] = rd("stepdepth_sel.bin", np.int32)
     lines_npy = name + "_lines.npy"
     np.save(os.path.join(HERE, lines_npy), lines)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
     meta = dict(source=os.path.basename(src), spacing=spacing, fills=[[float(v) for v in p.split(",")] for p in fills],
                 region=g["region"], cols=int(g["cols"]), rows=int(g["rows"]), bottom_left=g["bottom_left"],
                 nodes=N, runs=int(g["runs"]), lines_npy=lines_npy, vga=vga, roundtrip=rt, full_runs=keep,
-                ref_seconds=dict(makegraph=g["t_makegraph"], vga=g["t_vga"]))
+                stepdepth=STEPDEPTH.get(name, []),
+                ref_seconds=dict(makegraph=g["t_makegraph"], vga=g["t_vga"], stepdepth=g.get("t_stepdepth", 0.0)))
     return meta
 
 

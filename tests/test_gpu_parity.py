@@ -156,15 +156,15 @@ def test_shards_assemble_to_whole_graph(ctx):
     assert (o[:100] == -1).all() and (o[900:] == -1).all()
 
 
-@pytest.mark.parametrize("kernel", ["v1", "topdown"])
+@pytest.mark.parametrize("kernel", ["v1", "topdown", "do"])
 def test_vga_kernels_agree(ctx, kernel, monkeypatch):
-    """The direction-optimising BFS, its top-down-only mode and the v1 top-down kernel agree
-    bit-for-bit (levels and measures)."""
+    """The tile-resolved BFS (default), the direction-optimising BFS, its top-down-only mode and
+    the v1 top-down kernel agree bit-for-bit (levels and measures)."""
     meta, A = load_case("gallery")
     pm = _map(meta)
     g = pm.make_graph(ctx)
     out_do, lv_do = g.vga_visual_global(levels=True)
-    assert ctx.last_stats()["vga_kernel"] == "direction-optimizing"
+    assert ctx.last_stats()["vga_kernel"] == "tile-resolved"
     monkeypatch.setenv("DMX_VGA_KERNEL", kernel)
     g2 = pm.make_graph(ctx)
     out2, lv2 = g2.vga_visual_global(levels=True)
@@ -186,7 +186,7 @@ def test_vga_asymmetric_graph_corrections(ctx, monkeypatch):
     for (b, e) in ranges:
         outs.append(g.vga_visual_global(src_begin=b, src_end=e, levels=True))
     st = ctx.last_stats()
-    assert st["vga_kernel"] == "direction-optimizing" and st["vga_special_nodes"] == 4
+    assert st["vga_kernel"] == "tile-resolved" and st["vga_special_nodes"] == 4
     monkeypatch.setenv("DMX_VGA_KERNEL", "v1")
     g2 = pm.make_graph(ctx)
     for (b, e), (o, lv) in zip(ranges, outs):
