@@ -37,6 +37,9 @@ SIGNATURES = {
     "dmx_graph_assemble_device": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp]),
     "dmx_vga_global": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp, _vp]),
     "dmx_vga_global_device": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp]),
+    "dmx_metric_stepdepth": (_i32, [_vp, _vp, _vp, _i64, _vp]),
+    "dmx_ctx_last_stepdepth": (_i32, [_vp, _vp, _vp, _vp]),
+    "dmx_ctx_last_phase_cycles": (_i32, [_vp, _vp]),
 }
 
 

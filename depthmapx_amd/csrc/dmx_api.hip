@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -21,11 +22,24 @@
 #include "kernels/vga.hip"
 #include "kernels/vga_do.hip"
 #include "kernels/vga_tile.hip"
+#include "kernels/stepdepth.hip"
 
 using namespace dmx;
 
 namespace {
 thread_local std::string g_err;
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+bool verbose() {
+    static int v = -1;
+    if (v < 0) v = getenv("DMX_VERBOSE") ? 1 : 0;
+    return v == 1;
+}
+#define VLOG(...)                                      \
+    do {                                               \
+        if (verbose()) fprintf(stderr, "[dmx] " __VA_ARGS__); \
+    } while (0)
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -61,7 +75,9 @@ struct dmx_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int num_cu = 0;
-    double last_mk_s = 0, last_vga_s = 0;
+    double last_mk_s = 0, last_vga_s = 0, last_sd_s = 0;
+    long long last_sd_stats[3] = {0, 0, 0};
+    long long phase_cycles[5] = {0, 0, 0, 0, 0};   // tile BFS: level 1, A, B, C, bookkeeping (sum over workgroups)
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
     long long last_stats[16] = {};
@@ -227,7 +243,7 @@ int dmx_ctx_create(int device, dmx_ctx** out) {
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(c->counters.alloc(16));
-    HIPCHK(c->stats.alloc(8));
+    HIPCHK(c->stats.alloc(16));
     *out = c;
     return DMX_OK;
 }
@@ -317,11 +333,13 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
                   dmx_graph** out) {
     if (!ctx || !pm || !out) return fail(DMX_ERR_ARG, "bad arguments");
     HIPCHK(hipSetDevice(ctx->device));
+    const double t_start = now_s();
     PointMapHost& h = *pm->host;
     if (!h.lines_blocked()) h.block_lines();
     if (boundary) { h.keep_edges_only(); pm->version++; }
     int rc = upload_pointmap(ctx, pm);
     if (rc) return rc;
+    VLOG("makegraph: host prep + upload %.3f s\n", now_s() - t_start);
     const int64_t N = pm->nnodes;
     if (node_end < 0 || node_end > N) node_end = N;
     if (node_begin < 0 || node_begin > node_end) return fail(DMX_ERR_ARG, "bad node range");
@@ -361,7 +379,10 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         const size_t pool_bytes_max = free_b > stage_bytes + (1ull << 30) ? (free_b - stage_bytes - (1ull << 30)) : 0;
         if ((size_t)pool_cap * sizeof(Run) > pool_bytes_max) pool_cap = (int64_t)(pool_bytes_max / sizeof(Run));
         if (pool_cap <= 0) return fail(DMX_ERR_HIP, "not enough device memory for the run pool");
+        double ta = now_s();
         HIPCHK(g->pool.alloc(pool_cap));
+        VLOG("makegraph: pool alloc %.3f GB %.3f s\n", pool_cap * 8.0 / 1e9, now_s() - ta);
+        ta = now_s();
         DevBuf<unsigned long long> stA;
         DevBuf<Run> stB;
         DevBuf<uint32_t> pref;
@@ -369,7 +390,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         HIPCHK(stB.alloc((size_t)waves * capB));
         HIPCHK(pref.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
         HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
-        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), ctx->stream));
         MakeGraphParams P;
         P.cols = h.cols(); P.rows = h.rows();
         P.spacing = h.spacing(); P.blx = h.bottom_left().x; P.bly = h.bottom_left().y;
@@ -385,6 +406,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         P.stageA = stA.p; P.stageB = stB.p; P.prefix = pref.p;
         P.capA = (int)capA; P.capB = (int)capB; P.gcap = gcap; P.bcap = bcap; P.dmax = D;
         P.stats = ctx->stats.p;
+        VLOG("makegraph: stage alloc %.3f s\n", now_s() - ta);
         HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
         if (n > 0) {
             hipLaunchKernelGGL(makegraph_kernel, dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
@@ -414,6 +436,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             ctx->last_stats[2] = (long long)used;
             ctx->last_mk_s = ms * 1e-3;
             g->nruns = (int64_t)used;
+            VLOG("makegraph: kernels %.3f s, total %.3f s\n", ms * 1e-3, now_s() - t_start);
             *out = g.release();
             return DMX_OK;
         }
@@ -841,13 +864,21 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     HIPCHK(xg.alloc((size_t)blocks * 2 * nt));
     HIPCHK(queue.alloc((size_t)blocks * nt));
     HIPCHK(list.alloc((size_t)blocks * nt * 64));
+    DevBuf<uint16_t> hint;
+    HIPCHK(hint.alloc((size_t)nt * 64));
+    HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 2, ctx->stream));
     VgaTileParams P = Q;
     P.xg = xg.p;
     P.queue = queue.p;
     P.list = list.p;
+    P.hint = hint.p;
+    // chunks of consecutive sources per workgroup, small enough to balance the tail
+    P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
+    if (const char* c = getenv("DMX_VGA_CHUNK")) P.chunk = std::max(1, atoi(c));
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     hipLaunchKernelGGL((vga_tile_kernel<NT>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // hint freed on return
     *blocks_out = blocks;
     return DMX_OK;
 }
@@ -869,7 +900,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     DevBuf<int64_t> d_lv;
     if (levels) HIPCHK(d_lv.alloc(std::max<int64_t>(N, 1) * 3));
     HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), ctx->stream));
     VgaTileParams Q;
     Q.cols = h.cols(); Q.rows = h.rows(); Q.tw = tw; Q.th = th;
     Q.seed_tiles = g->notuf_tiles.p; Q.regular_tiles = g->regular_tiles.p; Q.nonexp_tiles = g->pm->d_nonexp_tiles.p;
@@ -885,7 +916,9 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.missing = corr ? g->missing.p : nullptr;
     Q.src_begin = sb; Q.src_end = se; Q.radius = (int)radius; Q.gates_only = gates_only;
     Q.uf_count = g->uf_count;
-    Q.alpha = 15;
+    // Beamer's direction test on cell counts, weighted by the cost asymmetry: a top-down level reads
+    // every run of every frontier cell (avg R/N each), a bottom-up cell usually one or two runs
+    Q.alpha = (int)std::max<int64_t>(15, N > 0 ? g->nruns / N / 2 : 15);
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
     Q.work_counter = ctx->counters.p + 0; Q.error = ctx->counters.p + 1;
     DevBuf<int32_t> d_hist, d_nlev;
@@ -918,8 +951,9 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     int hc[2];
     HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level capacity");
-    unsigned long long st[8];
+    unsigned long long st[16];
     HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+    for (int i = 0; i < 5; i++) ctx->phase_cycles[i] = (long long)st[8 + i];
     ctx->last_stats[3] = 3 | ((long long)g->nspecial << 8);
     ctx->last_stats[4] = (long long)st[0];
     ctx->last_stats[5] = (long long)(st[3] | (st[4] << 32));
@@ -989,7 +1023,7 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     DevBuf<int64_t> d_lv;
     if (levels) HIPCHK(d_lv.alloc(std::max<int64_t>(N, 1) * 3));
     HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 8 * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), ctx->stream));
     VgaParams P;
     P.cols = h.cols(); P.rows = h.rows(); P.tw = tw; P.th = th;
     P.seed_tiles = g->pm->d_seed_tiles.p; P.uf_tiles = g->uf_tiles.p; P.uf_count = g->uf_count;
@@ -1060,6 +1094,111 @@ int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se,
                           float* out_device) {
     return vga_impl(ctx, g, radius, gates_only, sb, se, out_device, true, nullptr);
+}
+
+// ---------------------------------------------------------------- metric step depth
+int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
+    if (g->node_begin != 0 || g->node_end != g->nnodes)
+        return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
+    HIPCHK(hipSetDevice(ctx->device));
+    PointMapHost& h = *g->pm->host;
+    const int cols = h.cols(), rows = h.rows();
+    const int64_t C = (int64_t)cols * rows, N = g->nnodes;
+    const auto& st = h.state();
+    // selection: filled cells only, std::set<int> PixelRef order, no duplicates
+    std::vector<int32_t> sel;
+    for (int64_t i = 0; i < nsel; i++) {
+        const int32_t c = sel_cells[i];
+        if (c < 0 || c >= C) return fail(DMX_ERR_ARG, "selected cell outside the grid");
+        if (st[c] & CELL_FILLED) sel.push_back(c);
+    }
+    std::sort(sel.begin(), sel.end(), [&](int32_t a, int32_t b) {
+        return ((a / rows) << 16) + (a % rows) < ((b / rows) << 16) + (b % rows);
+    });
+    sel.erase(std::unique(sel.begin(), sel.end()), sel.end());
+    if (sel.empty()) return fail(DMX_ERR_STATE, "no filled cell selected");
+    // expanders: selected, BLOCKED or next to a BLOCKED cell (ngraph.cpp:67-76, pointdata.cpp:1016-1068)
+    std::vector<uint8_t> flags((size_t)C, 0);
+    int64_t nexp = 0;
+    for (int x = 0; x < cols; x++)
+        for (int y = 0; y < rows; y++) {
+            const int64_t c = h.index(x, y);
+            if (!(st[c] & CELL_FILLED)) continue;
+            uint8_t f = SDF_FILLED;
+            bool ex = (st[c] & CELL_BLOCKED) != 0;
+            for (int dx = -1; dx <= 1 && !ex; dx++)
+                for (int dy = -1; dy <= 1 && !ex; dy++)
+                    if ((dx || dy) && h.includes(x + dx, y + dy) && (st[h.index(x + dx, y + dy)] & CELL_BLOCKED)) ex = true;
+            if (ex) { f |= SDF_EXPAND; nexp++; }
+            flags[c] = f;
+        }
+    for (int32_t c : sel) flags[c] |= SDF_EXPAND;
+    hipStream_t s = ctx->stream;
+    DevBuf<uint8_t> d_flags;
+    DevBuf<unsigned long long> d_key, d_over;
+    DevBuf<float> d_mdist, d_cum, d_out;
+    DevBuf<int32_t> d_last, d_sel;
+    HIPCHK(d_flags.alloc(C));
+    HIPCHK(d_key.alloc(C));
+    HIPCHK(d_mdist.alloc(C));
+    HIPCHK(d_cum.alloc(C));
+    HIPCHK(d_last.alloc(C));
+    HIPCHK(d_sel.alloc(sel.size()));
+    HIPCHK(d_out.alloc(std::max<int64_t>(N, 1) * 3));
+    HIPCHK(hipMemcpyAsync(d_flags.p, flags.data(), C, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, s));
+    int64_t cap = 8 * (nexp + (int64_t)sel.size()) + SD_WIN + 1024;
+    for (int attempt = 0; attempt < 4; attempt++) {
+        HIPCHK(d_over.alloc(cap));
+        HIPCHK(hipMemsetAsync(d_key.p, 0xFF, C * 8, s));
+        std::vector<float> m1((size_t)C, -1.0f);
+        HIPCHK(hipMemcpyAsync(d_mdist.p, m1.data(), C * 4, hipMemcpyHostToDevice, s));
+        HIPCHK(hipMemsetAsync(d_cum.p, 0, C * 4, s));
+        HIPCHK(hipMemsetAsync(d_last.p, 0xFF, C * 4, s));
+        HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), s));
+        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), s));
+        StepDepthParams P;
+        P.cols = cols; P.rows = rows; P.flags = d_flags.p; P.cell_node = g->pm->d_cell_node.p;
+        P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
+        P.key = d_key.p; P.mdist = d_mdist.p; P.cum = d_cum.p; P.lastpix = d_last.p;
+        P.over = d_over.p; P.over_cap = cap; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
+        HIPCHK(hipEventRecord(ctx->ev0, s));
+        hipLaunchKernelGGL(stepdepth_kernel, dim3(1), dim3(SD_THREADS), 0, s, P, d_sel.p, (int)sel.size());
+        HIPCHK(hipGetLastError());
+        const int single = sel.size() == 1 ? 1 : 0;
+        hipLaunchKernelGGL(stepdepth_out_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rows, h.spacing(),
+                           g->pm->d_node_cell.p, N, d_key.p, d_cum.p, single, sel[0] / rows, sel[0] % rows, d_out.p);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipEventRecord(ctx->ev1, s));
+        HIPCHK(hipStreamSynchronize(s));
+        int hc[2];
+        HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+        if (hc[1] & KERR_FRONTIER) { cap *= 4; continue; }
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        ctx->last_sd_s = ms * 1e-3;
+        unsigned long long st3[3];
+        HIPCHK(hipMemcpy(st3, ctx->stats.p, sizeof(st3), hipMemcpyDeviceToHost));
+        for (int i = 0; i < 3; i++) ctx->last_sd_stats[i] = (long long)st3[i];
+        if (N) HIPCHK(hipMemcpy(out, d_out.p, N * 3 * 4, hipMemcpyDeviceToHost));
+        return DMX_OK;
+    }
+    return fail(DMX_ERR_CAPACITY, "step depth queue overflow after retries");
+}
+
+int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {
+    if (!ctx || !out5) return fail(DMX_ERR_ARG, "bad arguments");
+    for (int i = 0; i < 5; i++) out5[i] = ctx->phase_cycles[i];
+    return DMX_OK;
+}
+
+int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_popped, int64_t* cells_relaxed) {
+    if (!ctx) return fail(DMX_ERR_ARG, "ctx is NULL");
+    if (seconds) *seconds = ctx->last_sd_s;
+    if (expanders_popped) *expanders_popped = ctx->last_sd_stats[0];
+    if (cells_relaxed) *cells_relaxed = ctx->last_sd_stats[1];
+    return DMX_OK;
 }
 
 } // extern "C"

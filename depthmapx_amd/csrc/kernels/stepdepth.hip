@@ -1,0 +1,288 @@
+// stepdepth.hip -- VGA metric step depth (STEPDEPTH -sdt metric) on gfx950.
+//
+// Replaces VGAMetricDepth::run (salalib/vgamodules/vgametricdepth.cpp:23-92) with
+// Node/Bin::extractMetric (salalib/ngraph.cpp:67-76, :330-345) and PointMap::blockedAdjacent
+// (salalib/pointdata.cpp:1016-1068).
+//
+// The reference is a Dijkstra over a std::set<MetricTriple> ordered by (float dist, PixelRef) in
+// which only "expanders" (the selected cells, BLOCKED cells and cells next to a BLOCKED cell)
+// relax their visible cells.  Its results depend on the exact pop order (float sums, strict
+// double-vs-float comparisons, set de-duplication that keeps the first lastpixel, cumulative
+// angles overwritten on equal-distance updates), so this kernel keeps that order exactly:
+//   * only expanders enter the priority queue; every other cell is final once every expander with
+//     a smaller key has been processed (later candidates are never smaller), which is exactly
+//     when the reference pops it;
+//   * key(v) = (bits of the smallest distance ever queued for v) << 32 | PixelRef(v): the pop
+//     order of the reference; a cell is "already popped" for expander u iff key(v) < key(u);
+//   * one workgroup runs the sequential expander loop; the relaxation of each expander's runs
+//     (tens of thousands of cells) is spread over its 1024 threads in <=128-cell chunks;
+//   * the queue is an unsorted LDS window (parallel min per pop) refilled from an HBM overflow
+//     list by distance windows.
+#include "common.hpp"
+
+namespace dmx {
+
+constexpr int SD_THREADS = 1024;
+constexpr int SD_WIN = 4096;       // LDS queue window (u64 keys)
+constexpr int SD_CHUNKQ = 4096;    // LDS queue of long-run chunks
+constexpr int SD_CHUNK = 128;      // cells per chunk
+constexpr unsigned long long SD_INF = ~0ull;
+
+enum : uint8_t { SDF_FILLED = 1, SDF_EXPAND = 2 };
+
+struct StepDepthParams {
+    int cols, rows;
+    const uint8_t* flags;          // [C] SDF_* per cell (x-major)
+    const int32_t* cell_node;      // [C]
+    const int64_t* node_run_start;
+    const int32_t* node_nruns;
+    const Run* pool;
+    unsigned long long* key;       // [C] (min queued dist bits << 32) | PixelRef, SD_INF = never queued
+    float* mdist;                  // [C] Point::m_dist (-1 initially)
+    float* cum;                    // [C] Point::m_cumangle
+    int32_t* lastpix;              // [C] lastpixel of the queued entry with the smallest key (-1: NoPixel)
+    unsigned long long* over;      // HBM overflow list of queue keys
+    int64_t over_cap;
+    int* error;
+    unsigned long long* stats;     // [0] expanders popped, [1] cells relaxed, [2] refills
+};
+
+__device__ __forceinline__ int pix_of(int x, int y) { return (x << 16) + (y & 0xffff); }   // pixelref.h:81
+__device__ __forceinline__ unsigned long long sd_key(float d, int pix) {
+    return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)pix;
+}
+
+struct SdShared {
+    unsigned long long win[SD_WIN];
+    int2 chunk[SD_CHUNKQ];          // (run index, first cell offset)
+    unsigned long long red[SD_THREADS / 64];
+    unsigned long long gmin;        // lower bound of the keys in the overflow list
+    long long nover;                // entries in the overflow list
+    int nwin, nchunk, cut_ok, pad;
+    unsigned long long cur;         // key being popped
+    float cut_w;                    // refill window width (distance units)
+};
+
+__device__ __forceinline__ void sd_push(SdShared& S, const StepDepthParams& P, unsigned long long k) {
+    // keys below the overflow bound go to the LDS window while it has room
+    if (k < S.gmin) {
+        const int pos = atomicAdd(&S.nwin, 1);
+        if (pos < SD_WIN) { S.win[pos] = k; return; }
+        atomicSub(&S.nwin, 1);
+    }
+    const long long o = atomicAdd((unsigned long long*)&S.nover, 1ull);
+    if (o < P.over_cap) P.over[o] = k;
+    else atomicOr(P.error, KERR_FRONTIER);
+    atomicMin(&S.gmin, k);
+}
+
+// Relax cell (x, y) from expander u (Bin::extractMetric, ngraph.cpp:330-345).
+__device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, int x, int y, int ux, int uy, float du,
+                                         float cumu, int lastu, unsigned long long ku, unsigned& relaxed) {
+    const int64_t c = (int64_t)x * P.rows + y;
+    const uint8_t f = P.flags[c];
+    if (!(f & SDF_FILLED)) return;        // diagonal-gap cells never resolve (p.filled() check)
+    const unsigned long long kv = P.key[c];
+    if (kv < ku) return;                  // already popped: m_misc == ~0
+    relaxed++;
+    const int dx = x - ux, dy = y - uy;
+    const double dd = sqrt((double)(dx * dx + dy * dy));
+    const float md = P.mdist[c];
+    if (md == -1.0f || (double)du + dd < (double)md) {
+        const float nd = du + (float)dd;
+        P.mdist[c] = nd;
+        float a = 0.0f;
+        if (lastu != -1) {   // PixelRef angle (pixelref.h:121-131)
+            const int lx = lastu >> 16, ly = lastu & 0xffff;
+            const int ex = ux - lx, ey = uy - ly;
+            a = (float)(acos((double)(dx * ex + dy * ey) /
+                             (sqrt((double)(dx * dx + dy * dy)) * sqrt((double)(ex * ex + ey * ey)) + 1e-12)) /
+                        (3.14159265358979323846 * 0.5));
+        }
+        P.cum[c] = cumu + a;
+        const unsigned long long nk = sd_key(nd, pix_of(x, y));
+        if (nk < kv) {                    // a new smallest entry: it carries this lastpixel
+            P.key[c] = nk;
+            P.lastpix[c] = pix_of(ux, uy);
+            if (f & SDF_EXPAND) sd_push(S, P, nk);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P, const int32_t* sel, int nsel) {
+    __shared__ SdShared S;
+    __shared__ unsigned long long s_keep;
+    __shared__ int s_idx, s_cnt;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    unsigned long long popped = 0, refills = 0;
+    unsigned relaxed = 0;
+    if (tid == 0) {
+        S.nwin = 0; S.nchunk = 0; S.gmin = SD_INF; S.nover = 0; S.cut_w = 4.0f;
+    }
+    __syncthreads();
+    // the selected cells enter at distance 0 (vgametricdepth.cpp:45-47)
+    for (int i = tid; i < nsel; i += SD_THREADS) {
+        const int c = sel[i];
+        const unsigned long long k = sd_key(0.0f, pix_of(c / P.rows, c % P.rows));
+        P.key[c] = k;
+        sd_push(S, P, k);
+    }
+    __syncthreads();
+    for (;;) {
+        // ---- parallel min of the window (keys are unique)
+        unsigned long long m = SD_INF;
+        const int nw = min(S.nwin, SD_WIN);
+        for (int i = tid; i < nw; i += SD_THREADS) m = min(m, S.win[i]);
+        for (int off = 32; off >= 1; off >>= 1) m = min(m, (unsigned long long)__shfl_xor(m, off));
+        if (lane == 0) S.red[wave] = m;
+        __syncthreads();
+        if (tid == 0) {
+            unsigned long long mm = SD_INF;
+            for (int w = 0; w < SD_THREADS / 64; w++) mm = min(mm, S.red[w]);
+            S.cur = mm;
+        }
+        __syncthreads();
+        const unsigned long long ku = S.cur;
+        if (ku == SD_INF || ku >= S.gmin) {
+            if (S.nover == 0 && ku == SD_INF) break;
+            // ---- refill: flush the window into the overflow list, then take back the smallest keys
+            refills++;
+            for (int i = tid; i < nw; i += SD_THREADS) {
+                const long long o = atomicAdd((unsigned long long*)&S.nover, 1ull);
+                if (o < P.over_cap) P.over[o] = S.win[i];
+                else atomicOr(P.error, KERR_FRONTIER);
+                atomicMin(&S.gmin, S.win[i]);
+            }
+            __syncthreads();
+            if (tid == 0) S.nwin = 0;
+            const long long no = min(S.nover, P.over_cap);
+            const unsigned long long g0 = S.gmin;
+            unsigned long long cut;
+            for (;;) {
+                const float d0 = __uint_as_float((unsigned)(g0 >> 32));
+                cut = max(sd_key(d0 + S.cut_w, 0), g0 + 1ull);
+                int cnt = 0;
+                for (long long i = tid; i < no; i += SD_THREADS) cnt += (P.over[i] < cut) ? 1 : 0;
+                for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off);
+                if (tid == 0) s_cnt = 0;
+                __syncthreads();
+                if (lane == 0) atomicAdd(&s_cnt, cnt);
+                __syncthreads();
+                const int total = s_cnt;
+                __syncthreads();
+                if (total <= SD_WIN || cut == g0 + 1ull) {
+                    if (tid == 0 && total < SD_WIN / 8) S.cut_w *= 2.0f;
+                    break;
+                }
+                if (tid == 0) S.cut_w *= 0.5f;
+                __syncthreads();
+            }
+            // move valid keys below cut into the window, compact the valid rest in place
+            if (tid == 0) { s_keep = 0; S.gmin = SD_INF; }
+            __syncthreads();
+            for (long long base = 0; base < no; base += SD_THREADS) {
+                const long long i = base + tid;
+                const unsigned long long k = (i < no) ? P.over[i] : SD_INF;
+                bool valid = false;
+                if (i < no) {
+                    const int px = (int)((k >> 16) & 0xffff), py = (int)(k & 0xffff);
+                    valid = P.key[(int64_t)px * P.rows + py] == k;
+                }
+                const bool in = valid && k < cut;
+                const bool keep = valid && !in;
+                if (in) S.win[atomicAdd(&S.nwin, 1)] = k;
+                const unsigned long long km = __ballot(keep);
+                unsigned long long kb = 0;
+                if (lane == 0 && km) kb = atomicAdd(&s_keep, (unsigned long long)__popcll(km));
+                kb = __shfl(kb, 0);
+                __syncthreads();   // this block of P.over is read before it is overwritten
+                if (keep) {
+                    P.over[kb + __popcll(km & ((1ull << lane) - 1ull))] = k;
+                    atomicMin(&S.gmin, k);
+                }
+                __syncthreads();
+            }
+            if (tid == 0) S.nover = (long long)s_keep;
+            __syncthreads();
+            continue;
+        }
+        // ---- pop ku: find its slot, move the last key into it
+        for (int i = tid; i < nw; i += SD_THREADS)
+            if (S.win[i] == ku) s_idx = i;
+        __syncthreads();
+        if (tid == 0) {
+            S.win[s_idx] = S.win[nw - 1];
+            S.nwin = nw - 1;
+            S.nchunk = 0;
+        }
+        __syncthreads();
+        const int ux = (int)((ku >> 16) & 0xffff), uy = (int)(ku & 0xffff);
+        const int64_t uc = (int64_t)ux * P.rows + uy;
+        if (P.key[uc] != ku) continue;    // stale: the cell was queued again with a smaller key
+        popped++;
+        const float du = __uint_as_float((unsigned)(ku >> 32));
+        const float cumu = P.cum[uc];
+        const int lastu = P.lastpix[uc];
+        const int node = P.cell_node[uc];
+        const int64_t rs = P.node_run_start[node];
+        const int nr = P.node_nruns[node];
+        // ---- relax: runs up to SD_CHUNK cells by their thread, longer tails through the chunk queue
+        for (int r = tid; r < nr; r += SD_THREADS) {
+            const Run ru = P.pool[rs + r];
+            const int dxs = (ru.x1 > ru.x0) ? 1 : 0;
+            const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
+            const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+            const int own = min(len, SD_CHUNK);
+            for (int i = 0; i < own; i++) sd_relax(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+            for (int o = SD_CHUNK; o < len; o += SD_CHUNK) {
+                const int q = atomicAdd(&S.nchunk, 1);
+                if (q < SD_CHUNKQ) {
+                    S.chunk[q] = make_int2(r, o);
+                } else {
+                    const int e = min(len, o + SD_CHUNK);
+                    for (int i = o; i < e; i++) sd_relax(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+                }
+            }
+        }
+        __syncthreads();
+        const int nch = min(S.nchunk, SD_CHUNKQ);
+        for (int j = tid; j < nch; j += SD_THREADS) {
+            const int2 ch = S.chunk[j];
+            const Run ru = P.pool[rs + ch.x];
+            const int dxs = (ru.x1 > ru.x0) ? 1 : 0;
+            const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
+            const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+            const int e = min(len, ch.y + SD_CHUNK);
+            for (int i = ch.y; i < e; i++) sd_relax(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+        }
+        __syncthreads();
+    }
+    unsigned long long rl = relaxed;
+    for (int off = 32; off >= 1; off >>= 1) rl += __shfl_xor(rl, off);
+    if (lane == 0) atomicAdd(&P.stats[1], rl);
+    if (tid == 0) { P.stats[0] = popped; P.stats[2] = refills; }
+}
+
+// Attribute rows (vgametricdepth.cpp:54-61): float(spacing * dist), cumulative angle and, for a
+// single selected cell, the straight-line distance.
+__global__ void stepdepth_out_kernel(int rows, double spacing, const int32_t* node_cell, int64_t n,
+                                     const unsigned long long* key, const float* cum, int single, int selx, int sely,
+                                     float* out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int c = node_cell[k];
+    const unsigned long long kv = key[c];
+    float* o = out + k * 3;
+    if (kv == SD_INF) { o[0] = -1.0f; o[1] = -1.0f; o[2] = -1.0f; return; }
+    const float d = __uint_as_float((unsigned)(kv >> 32));
+    o[0] = cum[c];
+    o[1] = (float)(spacing * (double)d);
+    if (single) {
+        const int dx = c / rows - selx, dy = c % rows - sely;
+        o[2] = (float)(spacing * sqrt((double)(dx * dx + dy * dy)));
+    } else {
+        o[2] = -1.0f;
+    }
+}
+
+} // namespace dmx

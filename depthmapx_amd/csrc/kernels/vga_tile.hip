@@ -53,6 +53,9 @@ struct VgaTileParams {
     int64_t uf_count;
     int alpha;
     int* work_counter;
+    int chunk;                // consecutive sources per work grab (neighbouring sources share hints)
+    uint16_t* hint;           // [nt*64] scan position of the run that last hit for a recent source (0xFFFF:
+                              // none); shared by all workgroups: a stale value only costs one test
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
     int32_t* list;            // per workgroup [nt*64]: hard cells / frontier cells
@@ -73,37 +76,40 @@ __device__ __forceinline__ void xy_of_tile_id(int id, int tw, int& x, int& y) {
     y = (t / tw) * 8 + (b >> 3);
 }
 
+// The per-workgroup HBM scratch (V, X, queues, hints) is only ever touched by its own workgroup,
+// so workgroup scope is enough for every atomic and every ordering point: the atomics stay in the
+// XCD's L2 and the barriers need no L2 write-back (agent scope would bypass / flush the
+// non-coherent per-XCD L2 on every level).
+__device__ __forceinline__ unsigned long long ld_wg(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void or_wg(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void sync_global() { __syncthreads(); }
+
 // OR all cells of run `ru` into the tiled bitmap `bm` (LDS or HBM, atomic).
 __device__ __forceinline__ void run_or(unsigned long long* bm, int tw, Run ru) {
     if (ru.y0 == ru.y1 && ru.x0 != ru.x1) {
         const int y = ru.y0, rowoff = (y >> 3) * tw, sh = (y & 7) * 8;
         for (int tx = ru.x0 >> 3; tx <= (ru.x1 >> 3); tx++) {
             const int lo = max((int)ru.x0, tx * 8) & 7, hi = min((int)ru.x1, tx * 8 + 7) & 7;
-            atomicOr(&bm[rowoff + tx], (unsigned long long)((0xFFu >> (7 - hi)) & (0xFFu << lo) & 0xFFu) << sh);
+            or_wg(&bm[rowoff + tx], (unsigned long long)((0xFFu >> (7 - hi)) & (0xFFu << lo) & 0xFFu) << sh);
         }
     } else if (ru.x0 == ru.x1 && ru.y0 != ru.y1) {
         const int x = ru.x0, tx = x >> 3;
         const unsigned long long col = 0x0101010101010101ull << (x & 7);
         for (int ty = ru.y0 >> 3; ty <= (ru.y1 >> 3); ty++) {
             const int lo = max((int)ru.y0, ty * 8) & 7, hi = min((int)ru.y1, ty * 8 + 7) & 7;
-            atomicOr(&bm[ty * tw + tx], col & (~0ull >> (8 * (7 - hi))) & (~0ull << (8 * lo)));
+            or_wg(&bm[ty * tw + tx], col & (~0ull >> (8 * (7 - hi))) & (~0ull << (8 * lo)));
         }
     } else {
         const int dy = (ru.y1 > ru.y0) ? 1 : ((ru.y1 < ru.y0) ? -1 : 0);
         int y = ru.y0;
-        for (int x = ru.x0; x <= ru.x1; x++, y += dy) atomicOr(&bm[(y >> 3) * tw + (x >> 3)], 1ull << ((y & 7) * 8 + (x & 7)));
+        for (int x = ru.x0; x <= ru.x1; x++, y += dy) or_wg(&bm[(y >> 3) * tw + (x >> 3)], 1ull << ((y & 7) * 8 + (x & 7)));
     }
 }
 
-// Xg is written with plain stores by its owner thread and with atomics (performed at L2) by any
-// wave of the workgroup; reads after such phases bypass the CU's L1.
-__device__ __forceinline__ unsigned long long ld_l2(const unsigned long long* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void sync_global() {
-    __threadfence();
-    __syncthreads();
-}
 
 struct TileShared {
     int src, qn, hn, item;
@@ -165,13 +171,25 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
     int32_t* L = P.list + (size_t)blockIdx.x * nt * 64;
     const size_t hstride = (size_t)nt * 64;
     unsigned long long runs_tested = 0, fail_cells = 0, fail_runs = 0, cr_tiles = 0;
+    unsigned long long cyc[5] = {0, 0, 0, 0, 0};   // leader-thread phase clocks
+    unsigned long long tmark = 0;
 
-    if (tid == 0) { S.qn = 0; S.hn = 0; S.item = 0; S.cnt = 0; S.mass = 0; }
+    uint16_t* Hn = P.hint;
+    if (tid == 0) { S.qn = 0; S.hn = 0; S.item = 0; S.cnt = 0; S.mass = 0; S.src = -1; }
+    int64_t chunk_end = 0;
+    int64_t src = -1;
     for (;;) {
-        if (tid == 0) S.src = atomicAdd(P.work_counter, 1);
-        __syncthreads();
-        const int64_t src = P.src_begin + S.src;
-        __syncthreads();
+        // sources are taken in chunks of consecutive (spatially adjacent) nodes, whose BFSs hit
+        // through the same runs: the hint array carries that knowledge from one source to the next
+        if (src + 1 >= chunk_end) {
+            __syncthreads();
+            if (tid == 0) S.src = atomicAdd(P.work_counter, 1);
+            __syncthreads();
+            src = P.src_begin + (int64_t)S.src * P.chunk;
+            chunk_end = min(src + (int64_t)P.chunk, P.src_end);
+        } else {
+            src++;
+        }
         if (src >= P.src_end) break;
         const int scell = P.node_cell[src];
         const int sx = scell / rows, sy = scell % rows;
@@ -199,6 +217,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             if (P.radius != -1 && level >= P.radius) break;
             if (discovered >= target) break;
             const bool bottom_up = level > 0 && (m_f * (long long)P.alpha > m_u);
+            tmark = __builtin_amdgcn_s_memtime();
             if (level == 0) {
                 // ---- level 1: rasterise the source's runs (top-down from {s})
                 const int64_t rs = P.node_run_start[src];
@@ -207,6 +226,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 if (tid < nr) runs_tested += (unsigned long long)((nr - tid + NT - 1) / NT);
                 sync_global();
                 for (int t = tid; t < nt; t += NT) Xg[t] = F[t] & ~Vg[t];
+                { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[0] += n - tmark; tmark = n; }
             } else if (bottom_up) {
                 // ---- A: tile-common runs
                 for (int t0 = 0; t0 < nt; t0 += NT) {
@@ -238,6 +258,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     }
                 }
                 sync_global();
+                { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[1] += n - tmark; tmark = n; }
                 const int qn = S.qn;
                 // ---- B: head runs, one wave per queued tile, lane = cell
                 for (int it = wave; it < qn; it += NW) {
@@ -252,11 +273,16 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                             to_hard = true;
                             hard_val = -1 - id;   // special node: exact path
                         } else {
+                            const int hp = Hn[id];
+                            if (hp >= KH && hp != 0xFFFF) {   // the run that hit for a recent source
+                                runs_tested++;
+                                hit = run_hits(F, tw, P.scan_pool[P.tscan_start[id] + hp]);
+                            }
                             int h = 0;
-                            for (; h < KH; h++) {
+                            for (; h < KH && !hit; h++) {
                                 const Run hr = P.heads[h * hstride + id];
                                 if (hr.x0 < 0) break;
-                                if (run_hits(F, tw, hr)) { hit = true; h++; break; }
+                                if (run_hits(F, tw, hr)) { hit = true; if (hp != h) Hn[id] = (uint16_t)h; h++; break; }
                             }
                             runs_tested += h;
                             if (!hit) {
@@ -267,7 +293,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                         }
                     }
                     const unsigned long long hm = __ballot(hit);
-                    if (lane == 0 && hm) atomicOr(&Xg[t], hm);
+                    if (lane == 0 && hm) or_wg(&Xg[t], hm);
                     const unsigned long long hw = __ballot(to_hard);
                     if (hw) {
                         int base = 0;
@@ -277,6 +303,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     }
                 }
                 sync_global();
+                { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[2] += n - tmark; tmark = n; }
                 const int hn = S.hn;
                 // ---- C: hard cells, a wave scans 64 runs at a time (dynamic work counter)
                 for (;;) {
@@ -298,20 +325,34 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                         const int64_t rs = P.tscan_start[id];
                         nr = P.tnruns[id];
                         int base = KH;   // the first KH runs (the heads) were tested in phase B
-                        for (; base < nr && !found; base += 64) {
-                            const int r = base + lane;
-                            const bool h = (r < nr) && run_hits(F, tw, P.scan_pool[rs + r]);
-                            found = __ballot(h) != 0ull;
+                        // 4 runs per lane per step (256 per wave): four independent loads in flight
+                        for (; base < nr && !found; base += 256) {
+                            Run rr[4];
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                const int r = base + j * 64 + lane;
+                                if (r < nr) rr[j] = P.scan_pool[rs + r];
+                                else rr[j].x0 = -1;
+                            }
+                            int first = 1 << 30;
+#pragma unroll
+                            for (int j = 0; j < 4; j++)
+                                if (first == (1 << 30) && rr[j].x0 >= 0 && run_hits(F, tw, rr[j])) first = base + j * 64 + lane;
+                            int fmin = first;
+                            for (int off = 32; off >= 1; off >>= 1) fmin = min(fmin, __shfl_xor(fmin, off));
+                            found = fmin != (1 << 30);
+                            if (found && lane == 0) Hn[id] = (uint16_t)min(fmin, 0xFFFE);
                         }
                         if (lane == 0) runs_tested += (unsigned long long)(min(base, nr) - KH);
                     }
                     if (lane == 0) {
-                        if (found) atomicOr(&Xg[id >> 6], 1ull << (id & 63));
+                        if (found) or_wg(&Xg[id >> 6], 1ull << (id & 63));
                         else { fail_cells++; fail_runs += (unsigned long long)nr; }
                     }
                 }
             } else {
-                // ---- top-down from the frontier F (small frontier): push runs into Xg, mask with V
+                // ---- top-down from the frontier F (small frontier): list it, then reuse F's LDS as
+                // the bitmap the frontier's runs are pushed into
                 for (int t = tid; t < nt; t += NT) {
                     unsigned long long f = F[t];
                     const int c = __popcll(f);
@@ -322,6 +363,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                         L[pos++] = (t << 6) | b;
                     }
                 }
+                sync_global();
+                for (int t = tid; t < nt; t += NT) F[t] = 0ull;
                 sync_global();
                 const int fn = S.hn;
                 for (;;) {
@@ -334,19 +377,23 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     const int node = P.cell_node[x * rows + y];
                     const int64_t rs = P.node_run_start[node];
                     const int nr = P.node_nruns[node];
-                    for (int r = lane; r < nr; r += 64) run_or(Xg, tw, P.pool[rs + r]);
+                    for (int r = lane; r < nr; r += 64) run_or(F, tw, P.pool[rs + r]);
                     if (lane == 0) runs_tested += (unsigned long long)nr;
                 }
                 sync_global();
-                __threadfence();
-                for (int t = tid; t < nt; t += NT) Xg[t] = ld_l2(&Xg[t]) & ~Vg[t];
+                for (int t = tid; t < nt; t += NT) Xg[t] = F[t] & ~Vg[t];
             }
             sync_global();
-            __threadfence();
+            {
+                const unsigned long long n = __builtin_amdgcn_s_memtime();
+                if (bottom_up) cyc[3] += n - tmark;
+                else cyc[0] += n - tmark;
+                tmark = n;
+            }
             // ---- level bookkeeping: count X, publish the expandable part as the next frontier
             unsigned long long c_loc = 0, m_loc = 0;
             for (int t = tid; t < nt; t += NT) {
-                unsigned long long x = ld_l2(&Xg[t]);
+                unsigned long long x = ld_wg(&Xg[t]);
                 if (x) {
                     c_loc += (unsigned long long)__popcll(x);
                     Vg[t] |= x;
@@ -363,6 +410,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             if (lane == 0 && c_loc) { atomicAdd(&S.cnt, c_loc); atomicAdd(&S.mass, m_loc); }
             sync_global();
             const long long cnt = (long long)S.cnt, mass = (long long)S.mass;
+            { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[4] += n - tmark; tmark = n; }
             __syncthreads();
             if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; }
             if (cnt == 0) break;
@@ -395,6 +443,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
         if (fail_cells) { atomicAdd(&P.stats[5], fail_cells); atomicAdd(&P.stats[6], fail_runs); }
         if (cr_tiles) atomicAdd(&P.stats[7], cr_tiles);
     }
+    if (tid == 0)
+        for (int i = 0; i < 5; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
 }
 
 // ---------------------------------------------------------------- prep: tile-ordered cell arrays

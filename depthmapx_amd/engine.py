@@ -15,6 +15,8 @@ import numpy as np
 from . import _native as N
 
 MAKEGRAPH_COLUMNS = ["Connectivity", "Point First Moment", "Point Second Moment"]
+STEPDEPTH_COLUMNS = ["Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length",
+                     "Metric Straight-Line Distance"]
 VGA_COLUMNS = ["Visual Entropy", "Visual Integration [HH]", "Visual Integration [P-value]",
                "Visual Integration [Tekl]", "Visual Mean Depth", "Visual Node Count",
                "Visual Relativised Entropy"]
@@ -40,6 +42,16 @@ class Context:
         mk, vg = ctypes.c_double(), ctypes.c_double()
         N.check(N.lib().dmx_ctx_last_timing(self.h, ctypes.byref(mk), ctypes.byref(vg)))
         return mk.value, vg.value
+
+    def last_stepdepth(self):
+        t, p, r = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
+        N.check(N.lib().dmx_ctx_last_stepdepth(self.h, ctypes.byref(t), ctypes.byref(p), ctypes.byref(r)))
+        return dict(seconds=t.value, expanders_popped=p.value, cells_relaxed=r.value)
+
+    def last_phase_cycles(self):
+        out = np.zeros(5, dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_phase_cycles(self.h, N.ptr(out)))
+        return dict(zip(["level1", "tile_common", "heads", "hard", "bookkeeping"], (int(v) for v in out)))
 
     def last_stats(self):
         out = np.zeros(16, dtype=np.int64)
@@ -102,6 +114,20 @@ class PointMap:
         out = np.zeros(i["cols"] * i["rows"], dtype=np.int32)
         N.check(N.lib().dmx_pointmap_state(self.h, N.ptr(out)))
         return out
+
+    def pixelate(self, x, y):
+        """PointMap::pixelate(p, constrain=true) (salalib/pointdata.cpp:263-283) -> x-major cell index."""
+        i = self.info()
+        blx, bly = i["bottom_left"]
+        px = int(np.floor((x - blx + self.spacing / 2.0) / self.spacing))
+        py = int(np.floor((y - bly + self.spacing / 2.0) / self.spacing))
+        px = min(max(px, 0), i["cols"] - 1)
+        py = min(max(py, 0), i["rows"] - 1)
+        return px * i["rows"] + py
+
+    def region_contains(self, x, y):
+        r = self._region
+        return r[0] <= x <= r[2] and r[1] <= y <= r[3]
 
     def cell_lines(self):
         i = self.info()
@@ -174,6 +200,22 @@ class Graph:
         N.check(N.lib().dmx_vga_global(self.ctx.h, self.h, float(radius), int(bool(gates_only)), int(src_begin),
                                        int(src_end), N.ptr(out), N.ptr(lv)))
         return (out, lv) if levels else out
+
+    def metric_step_depth(self, points=None, cells=None):
+        """STEPDEPTH -sdt metric (dm_runmethods::runStepDepth, depthmapXcli/runmethods.cpp:735-778):
+        select the cell under each point (MetaGraph::setCurSel; 'Point outside of target region'
+        like the CLI), then VGAMetricDepth::run on the GPU.  Returns [N][3] float32 in
+        STEPDEPTH_COLUMNS order."""
+        sel = [] if cells is None else [int(c) for c in cells]
+        for (x, y) in (points or []):
+            if not self.pm.region_contains(x, y):
+                raise N.DmxError(-6, "Point outside of target region")
+            sel.append(self.pm.pixelate(x, y))
+        arr = np.ascontiguousarray(sel, dtype=np.int32)
+        n = self.info()["nnodes"]
+        out = np.full((n, 3), -1.0, dtype=np.float32)
+        N.check(N.lib().dmx_metric_stepdepth(self.ctx.h, self.h, N.ptr(arr), len(arr), N.ptr(out)))
+        return out
 
     def vga_visual_global_device(self, out_dev_ptr, radius=-1.0, gates_only=False, src_begin=0, src_end=-1):
         N.check(N.lib().dmx_vga_global_device(self.ctx.h, self.h, float(radius), int(bool(gates_only)),

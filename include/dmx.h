@@ -53,6 +53,11 @@ int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
  * [7] sources run. */
 int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
 
+/* Diagnostics of the last tile-resolved VGA launch: core-clock cycles spent (workgroup leader,
+ * summed over workgroups) in level 1, phase A (tile-common runs), B (head runs), C (hard cells)
+ * and level bookkeeping. */
+int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5);
+
 /* ---- VISPREP preparation (host model) ----------------------------------------------------- */
 /* MetaGraph::addNewPointMap + PointMap::setGrid(spacing, (0,0)) (salalib/pointdata.cpp:122-171),
  * with the drawing `lines` ([n][4] = x1,y1,x2,y2 as PointMap::blockLines reads them,
@@ -109,6 +114,18 @@ int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
                    float* out, int64_t* levels);
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin,
                           int64_t src_end, float* out_device);
+
+/* ---- VGA metric step depth (GPU) ----------------------------------------------------------- */
+/* dm_runmethods::runStepDepth with -sdt metric -> MetaGraph::analyseGraph(point_depth_selection=2)
+ * -> VGAMetricDepth::run (depthmapXcli/runmethods.cpp:735-778, salalib/mgraph.cpp:327-330,
+ * vgamodules/vgametricdepth.cpp:23-92).  sel_cells: x-major cell indices of the selection
+ * (PointMap::setCurSel keeps FILLED cells only; order and duplicates do not matter).  out: host
+ * [N][3] in node order: Metric Step Shortest-Path Angle, Metric Step Shortest-Path Length,
+ * Metric Straight-Line Distance (single selected cell only, else -1); unreached cells -1.
+ * DMX_ERR_STATE if no filled cell is selected (the reference then skips the analysis). */
+int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out);
+/* Kernel time of the last step-depth call, expanders popped, cells relaxed. */
+int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_popped, int64_t* cells_relaxed);
 
 #ifdef __cplusplus
 }

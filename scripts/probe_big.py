@@ -13,7 +13,7 @@ from bench import load_lines  # noqa: E402
 W = int(sys.argv[1])
 ns = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 if len(sys.argv) > 3:
-    os.environ["DMX_VGA_KERNEL"] = sys.argv[3]
+    os.environ["DMX_VGA_KERNEL"] = sys.argv[3]  # "" keeps the default
 ctx = dmx.Context(0)
 pm = dmx.PointMap([0.0, 0.0, float(W), float(W)], load_lines(W, 50), 1.0)
 assert pm.make_points(0.5, 0.5)
@@ -27,16 +27,20 @@ b = max(0, N // 2 - ns // 2)
 e = min(N, b + ns)
 t0 = time.time()
 g.vga_visual_global(src_begin=b, src_end=b + 1)   # prep (uf, symmetry, tiles)
-t1 = time.time()
-out = g.vga_visual_global(src_begin=b, src_end=e)
-t2 = time.time()
-st = ctx.last_stats()
-nsrc = e - b
-tk = ctx.last_timing()[1]
-print(json.dumps({"prep_wall_s": t1 - t0, "vga_sources": nsrc, "vga_kernel_s": tk, "vga_wall_s": t2 - t1,
-                  "vga_s_per_source": tk / nsrc, "est_full_vga_s": tk / nsrc * N,
-                  "runs_read_per_src": st["vga_runs_expanded"] / nsrc, "fail_cells_per_src": st["vga_fail_cells"] / nsrc,
-                  "fail_runs_per_src": st["vga_fail_runs"] / nsrc, "cr_tiles_per_src": st["vga_cr_tiles"] / nsrc,
-                  "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc,
-                  "levels_td_per_src": st["vga_top_down_levels"] / nsrc, "kernel": st["vga_kernel"],
-                  "launch": st["vga_launch"]}), flush=True)
+print(json.dumps({"prep_wall_s": time.time() - t0}), flush=True)
+configs = [c.split("=") for c in (sys.argv[4:] if len(sys.argv) > 4 else ["DMX_VGA_CHUNK=1"])]
+for k, v in configs:
+    os.environ[k] = v
+    out = g.vga_visual_global(src_begin=b, src_end=e)
+    st = ctx.last_stats()
+    nsrc = e - b
+    tk = ctx.last_timing()[1]
+    print(json.dumps({"config": "%s=%s" % (k, v), "vga_sources": nsrc, "vga_kernel_s": tk,
+                      "vga_s_per_source": tk / nsrc, "est_full_vga_s": tk / nsrc * N,
+                      "runs_read_per_src": st["vga_runs_expanded"] / nsrc,
+                      "fail_cells_per_src": st["vga_fail_cells"] / nsrc,
+                      "fail_runs_per_src": st["vga_fail_runs"] / nsrc, "cr_tiles_per_src": st["vga_cr_tiles"] / nsrc,
+                      "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc, "kernel": st["vga_kernel"],
+                      "launch_blocks": st["vga_launch"] & 0xFFFFFFFF,
+                      "phase_cycles_per_src": {kk: vv / nsrc for kk, vv in ctx.last_phase_cycles().items()}}),
+          flush=True)

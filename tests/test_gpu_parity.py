@@ -193,3 +193,61 @@ def test_vga_asymmetric_graph_corrections(ctx, monkeypatch):
         o2, lv2 = g2.vga_visual_global(src_begin=b, src_end=e, levels=True)
         np.testing.assert_array_equal(lv[b:e], lv2[b:e])
         np.testing.assert_array_equal(o[b:e].view(np.uint32), o2[b:e].view(np.uint32))
+
+
+SD_CASES = ["kat", "syn16", "syn32", "syn64", "gallery"]
+
+
+def _assert_stepdepth(got, want):
+    # path length and straight-line distance: float sums of correctly rounded sqrt -> bit-exact;
+    # cumulative angle: acos is libm vs device-libm (1 ulp) -> within 1e-6 relative
+    np.testing.assert_array_equal(got[:, 1].view(np.uint32), want[:, 1].view(np.uint32))
+    np.testing.assert_array_equal(got[:, 2].view(np.uint32), want[:, 2].view(np.uint32))
+    tol = 1e-6 * np.maximum(1.0, np.abs(want[:, 0]))
+    assert (np.abs(got[:, 0] - want[:, 0]) <= tol).all()
+
+
+@pytest.mark.parametrize("name", SD_CASES)
+def test_metric_stepdepth_matches_reference(ctx, name):
+    meta, A = load_case(name)
+    if "stepdepth" not in A:
+        pytest.skip("fixture without step depth")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    pts = [tuple(float(v) for v in p.split(",")) for p in meta["stepdepth"]]
+    got = g.metric_step_depth(points=pts)
+    _assert_stepdepth(got, A["stepdepth"])
+    sd = ctx.last_stepdepth()
+    assert sd["expanders_popped"] > 0
+
+
+@pytest.mark.parametrize("seed", [3, 7])
+def test_metric_stepdepth_random_matches_oracle(ctx, seed):
+    from pyoracle import OracleMap
+    from golden.gen_synthetic import make_lines
+    W = 48
+    lines = np.array(make_lines(W, 80, seed=seed, lmin=0.02, lmax=0.3), dtype=np.float64)
+    region = [0.0, 0.0, float(W), float(W)]
+    pm = dmx.PointMap(region, lines, 1.0)
+    om = OracleMap(region, 1.0, lines)
+    assert pm.make_points(0.5, 0.5) and om.fill(0.5, 0.5)
+    g = pm.make_graph(ctx)
+    om.make_graph(threads=8)
+    st = pm.state()
+    rng = np.random.default_rng(seed)
+    filled = np.nonzero(st & 2)[0]
+    for nsel in (1, 3):
+        cells = np.sort(rng.choice(filled, nsel, replace=False))
+        got = g.metric_step_depth(cells=cells)
+        rows = pm.rows
+        order = np.argsort((cells // rows) * 65536 + cells % rows)
+        want = om.metric_stepdepth(cells[order])
+        _assert_stepdepth(got, want)
+
+
+def test_metric_stepdepth_errors(ctx):
+    meta, _ = load_case("syn32")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    with pytest.raises(dmx.DmxError):
+        g.metric_step_depth(points=[(-5.0, 1.0)])   # outside the region

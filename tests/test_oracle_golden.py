@@ -119,3 +119,17 @@ def test_reference_gallery_attributes_file():
     assert len(rows) == meta["nodes"]
     np.testing.assert_array_equal(rows[:, 3], A["attrs"][:, 0])
     np.testing.assert_allclose(rows[:, 4:6], A["attrs"][:, 1:3], rtol=1e-6)
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery"])
+def test_metric_stepdepth_matches_reference_bitexact(name):
+    """VGAMetricDepth::run restatement vs the reference's STEPDEPTH -sdt metric columns
+    (ref_probe --stepdepth, runStepDepth semantics: setCurSel at each point)."""
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    sel = A["stepdepth_sel"]                         # std::set<int> of PixelRef ints
+    cells = (sel >> 16) * meta["rows"] + (sel & 0xFFFF)
+    got = om.metric_stepdepth(cells)
+    np.testing.assert_array_equal(got.view(np.uint32), A["stepdepth"].view(np.uint32))
+    assert (A["stepdepth"][:, 1] >= 0).sum() > 0
