@@ -1,16 +1,20 @@
 #!/usr/bin/env python3
 """Headline benchmark: grid cells/s for VISPREP makeGraph + VGA global (radius n) on a synthetic
-N x N open-plan grid with 50 random occluders (BASELINE.json metric).
+W x W open-plan grid with 50 random occluders (BASELINE.json metric).
 
 One step = the whole hot path for every filled cell of the grid:
-  makeGraph (sparkGraph2) over this rank's source-cell shard -> [N>1: RCCL all-gather of the
-  run-length graph shards] -> VGA global BFS + measures over this rank's source shard ->
-  [N>1: RCCL all-gather of the 7 float columns].
+  makeGraph (sparkGraph2) -> VGA global BFS + measures (VGAVisualGlobal::run) for every source.
+Multi-GPU (one process per GPU, RCCL): sources are split into contiguous x-major ranges.  The VGA
+BFS of any source walks the whole graph, so every rank needs all of it:
+  --mk-mode shard:     each rank builds its source range, the run-length shards are all-gathered
+                       over RCCL and assembled (bytes ~ 8 B/run: 574 MB at 256^2, 36 GB at 1000^2);
+  --mk-mode replicate: every rank builds the whole graph (no data-path collective);
+  auto:                replicate when the all-gather would outlast makeGraph (W >= 512).
+then VGA for the rank's sources and one RCCL all-gather of the 7 float columns.
 Inputs (grid state + occluder pieces) are resident in HBM before the timed region; value =
-filled cells / step time (all ranks), i.e. source cells carried through makeGraph + VGA per
-second.
+filled cells / step time (max over ranks).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 256]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 256|1000]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 """
 import argparse
@@ -24,7 +28,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def load_lines(W, occluders):
@@ -48,27 +52,28 @@ def load_traffic(workload):
         return None
 
 
-def cpu_baseline(region, lines, spacing, fill, graph_np, budget_s):
+def cpu_baseline(region, lines, spacing, fill, g, budget_s):
     """The C restatement (oracle/, bit-exact vs the reference) timed single-threaded on a bounded
     sample of the same workload: makeGraph on a contiguous block of sources, then VGA global BFS
-    on a block of sources over the full graph (imported from the GPU result, identical bits)."""
+    on a block of sources over the full graph (copied from the GPU result, identical bits)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from pyoracle import OracleMap
     om = OracleMap(region, spacing, lines)
     om.fill(*fill)
-    N = graph_np["bins"].shape[0]
+    N = g.info()["nnodes"]
     mid = N // 2
-    # makeGraph sample: grow until ~40% of the budget
-    k, t_mk = 8, 0.0
+    k, t_mk = 4, 0.0
     while True:
         t0 = time.perf_counter()
         om.make_graph(node_begin=mid, node_end=min(N, mid + k), threads=1)
         t_mk = time.perf_counter() - t0
-        if t_mk > 0.4 * budget_s or mid + k >= N:
+        if t_mk > 0.3 * budget_s or mid + k >= N:
             break
-        k = min(N - mid, max(k * 2, int(k * 0.4 * budget_s / max(t_mk, 1e-3))))
+        k = min(N - mid, max(k * 2, int(k * 0.3 * budget_s / max(t_mk, 1e-3))))
     mk_per_src = t_mk / min(k, N - mid)
-    om.set_graph(graph_np["bins"], graph_np["runs"])
+    gn = g.copy(runs=True)
+    om.set_graph(gn["bins"], gn["runs"])
+    del gn
     kv, t_v = 1, 0.0
     while True:
         t0 = time.perf_counter()
@@ -78,10 +83,9 @@ def cpu_baseline(region, lines, spacing, fill, graph_np, budget_s):
             break
         kv = min(N - mid, max(kv * 2, int(kv * 0.4 * budget_s / max(t_v, 1e-3))))
     vga_per_src = t_v / min(kv, N - mid)
-    value = 1.0 / (mk_per_src + vga_per_src)
-    return {"value": value, "unit": "cells/s", "cores": 1, "kind": "port",
+    return {"value": 1.0 / (mk_per_src + vga_per_src), "unit": "cells/s", "cores": 1, "kind": "port",
             "sample": "oracle/dmx_oracle.c single thread: makeGraph on %d sources (%.2f s) + VGA global BFS "
-                      "on %d sources (%.2f s) from node %d; per-source times extrapolated to cells/s"
+                      "on %d sources (%.2f s) from node %d over the full graph; per-source times -> cells/s"
                       % (min(k, N - mid), t_mk, min(kv, N - mid), t_v, mid),
             "makegraph_s_per_source": mk_per_src, "vga_s_per_source": vga_per_src}
 
@@ -93,6 +97,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--grid", type=int, default=256, help="W: region [0,W]^2 at spacing 1 -> (W+1)^2 cells")
     ap.add_argument("--occluders", type=int, default=50)
+    ap.add_argument("--mk-mode", choices=["auto", "shard", "replicate"], default="auto")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -110,6 +115,9 @@ def main():
     from depthmapx_amd.sharded import allgather_blobs, allgather_rows, shard_range
 
     W = args.grid
+    mk_mode = args.mk_mode
+    if mk_mode == "auto":
+        mk_mode = "replicate" if (world > 1 and W >= 512) else "shard"
     lines = load_lines(W, args.occluders)
     region = [0.0, 0.0, float(W), float(W)]
     fill = (0.5, 0.5)
@@ -127,18 +135,21 @@ def main():
     stats = {}
 
     def step(record):
-        # 1. makeGraph for this rank's sources
-        shard = pm.make_graph(ctx, node_begin=b, node_end=e)
+        # 1. makeGraph: this rank's sources (shard) or all of them (replicate)
+        if world > 1 and mk_mode == "shard":
+            shard = pm.make_graph(ctx, node_begin=b, node_end=e)
+        else:
+            shard = pm.make_graph(ctx)
         t_mk = ctx.last_timing()[0]
         st = dict(ctx.last_stats())
-        if world > 1:
+        if world > 1 and mk_mode == "shard":
             # 2. all-gather the run-length graph shards (RCCL), assemble the whole graph
             blob = torch.empty(shard.blob_size(), dtype=torch.uint8, device=dev)
             shard.write_blob_device(blob.data_ptr(), blob.numel())
             flat, mx, sizes = allgather_blobs(blob, dist)
             torch.cuda.synchronize()
             g = pm.assemble(ctx, [flat.data_ptr() + i * mx for i in range(world)], sizes)
-            del flat, blob
+            del flat, blob, shard
         else:
             g = shard
         # 3. VGA global for this rank's sources
@@ -162,9 +173,9 @@ def main():
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
         g = step(True)
-        if _ != args.steps - 1:
+        if i != args.steps - 1:
             del g
     torch.cuda.synchronize()
     if world > 1:
@@ -179,13 +190,13 @@ def main():
         steps = max(args.steps, 1)
         mk_s = kt["makegraph_s"] / max(kt["n"], 1)
         vga_s = kt["vga_s"] / max(kt["n"], 1)
-        nr_shard = stats.get("mk_runs", 0)
-        # algorithmic bytes (DESIGN.md "Roofline accounting"), per launch on this rank
-        tw, th = (info["cols"] + 7) // 8, (info["rows"] + 7) // 8
         nsrc = e - b
-        mk_bytes = 8 * nr_shard + 4 * stats.get("mk_cells_examined", 0)
-        vga_bytes = 8 * stats.get("vga_runs_expanded", 0) + 8 * tw * th * nsrc + 8 * stats.get("vga_cells_reached", 0)
-        dominant = "vga_global_kernel" if vga_s >= mk_s else "makegraph_kernel"
+        # algorithmic bytes per launch
+        mk_bytes = 8 * stats.get("mk_runs", 0) + 4 * stats.get("mk_cells_examined", 0)
+        tw, th = (info["cols"] + 7) // 8, (info["rows"] + 7) // 8
+        levels = stats.get("vga_bottom_up_levels", 0) + stats.get("vga_top_down_levels", 0)
+        vga_bytes = 8 * stats.get("vga_runs_expanded", 0) + 16 * tw * th * nsrc + 32 * tw * th * levels
+        dominant = "vga_tile_kernel" if vga_s >= mk_s else "makegraph_kernel"
         dom_bytes, dom_s = (vga_bytes, vga_s) if vga_s >= mk_s else (mk_bytes, mk_s)
         achieved = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
         traffic = load_traffic(workload)
@@ -204,21 +215,24 @@ def main():
             "dtype": "f64",
             "data": "synthetic (committed occluder CSV, seed 1)",
             "config": {"workload": workload, "grid": "%dx%d" % (info["cols"], info["rows"]), "filled_cells": N,
-                       "runs": int(g.info()["nruns"]), "parallelism": "source-shard x%d" % world},
+                       "runs": int(g.info()["nruns"]),
+                       "parallelism": "source-shard x%d (makeGraph %s)" % (world, mk_mode)},
             "kernels": {"makegraph_s": mk_s, "vga_s": vga_s,
-                        "makegraph_cells_per_s": nsrc / mk_s if mk_s else None,
+                        "makegraph_cells_per_s": (N if mk_mode == "replicate" or world == 1 else nsrc) / mk_s
+                        if mk_s else None,
                         "visible_pairs": stats.get("mk_visible_pairs"),
-                        "vga_runs_read": stats.get("vga_runs_expanded"),
                         "vga_kernel": stats.get("vga_kernel"),
+                        "vga_runs_tested": stats.get("vga_runs_expanded"),
+                        "vga_tiles_resolved_by_common_runs": stats.get("vga_cr_tiles"),
                         "vga_levels_bottom_up": stats.get("vga_bottom_up_levels"),
                         "vga_levels_top_down": stats.get("vga_top_down_levels"),
-                        "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc},
+                        "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc,
+                        "makegraph_algorithmic_bytes": mk_bytes, "vga_algorithmic_bytes": vga_bytes},
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": tr},
         }
         if not args.no_cpu_baseline and world == 1:
-            gn = g.copy(runs=True)
-            rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, gn, args.cpu_budget)
+            rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, g, args.cpu_budget)
             rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
         print(json.dumps(rec), flush=True)
     if world > 1:

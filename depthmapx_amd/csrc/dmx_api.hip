@@ -853,11 +853,11 @@ static int prepare_tiles(dmx_graph* g) {
     return DMX_OK;
 }
 
-extern "C++" template <int NT>
+extern "C++" template <int NT, bool SPECIAL>
 static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_t lds, int64_t* blocks_out,
                        DevBuf<unsigned long long>& xg, DevBuf<int4>& queue, DevBuf<int32_t>& list) {
     int occ = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT>, NT, lds));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT, SPECIAL>, NT, lds));
     if (occ < 1) occ = 1;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cu * occ, nsrc));
     const int64_t nt = (int64_t)Q.tw * Q.th;
@@ -876,7 +876,7 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
     if (const char* c = getenv("DMX_VGA_CHUNK")) P.chunk = std::max(1, atoi(c));
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-    hipLaunchKernelGGL((vga_tile_kernel<NT>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
+    hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));   // hint freed on return
     *blocks_out = blocks;
@@ -916,16 +916,15 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.missing = corr ? g->missing.p : nullptr;
     Q.src_begin = sb; Q.src_end = se; Q.radius = (int)radius; Q.gates_only = gates_only;
     Q.uf_count = g->uf_count;
-    // Beamer's direction test on cell counts, weighted by the cost asymmetry: a top-down level reads
-    // every run of every frontier cell (avg R/N each), a bottom-up cell usually one or two runs
-    Q.alpha = (int)std::max<int64_t>(15, N > 0 ? g->nruns / N / 2 : 15);
+    // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
+    Q.alpha = 15;
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
     Q.work_counter = ctx->counters.p + 0; Q.error = ctx->counters.p + 1;
     DevBuf<int32_t> d_hist, d_nlev;
     HIPCHK(d_hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));
     HIPCHK(d_nlev.alloc(std::max<int64_t>(N, 1)));
     Q.maxlev = maxlev; Q.hist_out = d_hist.p; Q.nlev_out = d_nlev.p; Q.stats = ctx->stats.p;
-    const size_t lds = (size_t)nt * 8 + (size_t)VGA_HMAX * 4;
+    const size_t lds = (size_t)nt * 8 + (size_t)(th * ((tw + 63) / 64) + tw * ((th + 63) / 64)) * 8 + (size_t)VGA_HMAX * 4;
     DevBuf<unsigned long long> xg;
     DevBuf<int4> queue;
     DevBuf<int32_t> list;
@@ -933,8 +932,16 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     int kt = 0, ntpb = 0;
     (void)kt;
     if (nsrc > 0) {
-        if (nt <= 4096) { rc = launch_tile<256>(ctx, Q, nsrc, lds, &blocks, xg, queue, list); ntpb = 256; }
-        else { rc = launch_tile<1024>(ctx, Q, nsrc, lds, &blocks, xg, queue, list); ntpb = 1024; }
+        const bool sp = g->nspecial > 0;
+        if (nt <= 4096) {
+            rc = sp ? launch_tile<256, true>(ctx, Q, nsrc, lds, &blocks, xg, queue, list)
+                    : launch_tile<256, false>(ctx, Q, nsrc, lds, &blocks, xg, queue, list);
+            ntpb = 256;
+        } else {
+            rc = sp ? launch_tile<1024, true>(ctx, Q, nsrc, lds, &blocks, xg, queue, list)
+                    : launch_tile<1024, false>(ctx, Q, nsrc, lds, &blocks, xg, queue, list);
+            ntpb = 1024;
+        }
         if (rc) return rc;
         hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsrc + 255) / 256)), dim3(256), 0, ctx->stream, sb, se,
                            d_hist.p, d_nlev.p, outp, levels ? d_lv.p : nullptr, ctx->stats.p);

@@ -25,6 +25,7 @@ namespace dmx {
 
 constexpr int KH = 8;        // head runs per cell (first KH entries of its scan order)
 constexpr int CRK = 4;       // tile-common runs per tile
+constexpr int BEXT = 56;     // runs after the heads a cell scans on its own lane before going wave-cooperative
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
 
 struct VgaTileParams {
@@ -111,6 +112,60 @@ __device__ __forceinline__ void run_or(unsigned long long* bm, int tw, Run ru) {
 }
 
 
+// Run test against the LDS frontier with coarse occupancy summaries: Fsr (bit per tile, tile rows
+// in row-major order) and Fsc (bit per tile, tile columns) let a horizontal / vertical run skip
+// every empty tile it crosses with one or two word reads, so a miss -- the common case when a
+// cell's visible region lies in the source's shadow -- costs O(1) LDS reads instead of O(len/8).
+struct FView {
+    const unsigned long long* F;
+    const unsigned long long* Fsr;
+    const unsigned long long* Fsc;
+    int tw, wr, wc;
+};
+__device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
+    if (ru.y0 == ru.y1) {   // horizontal (or a single cell)
+        const int y = ru.y0, ty = y >> 3, sh = (y & 7) * 8;
+        const int t0 = ru.x0 >> 3, t1 = ru.x1 >> 3;
+        const unsigned long long* row = V.Fsr + ty * V.wr;
+        for (int w = t0 >> 6; w <= (t1 >> 6); w++) {
+            const int lo = max(t0 - w * 64, 0), hi = min(t1 - w * 64, 63);
+            unsigned long long m = row[w] & (~0ull << lo) & (~0ull >> (63 - hi));
+            while (m) {
+                const int tx = w * 64 + __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const int a = max((int)ru.x0, tx * 8) & 7, b = min((int)ru.x1, tx * 8 + 7) & 7;
+                if (V.F[ty * V.tw + tx] & ((unsigned long long)((0xFFu >> (7 - b)) & (0xFFu << a) & 0xFFu) << sh)) return true;
+            }
+        }
+        return false;
+    } else if (ru.x0 == ru.x1) {   // vertical
+        const int x = ru.x0, tx = x >> 3;
+        const unsigned long long colm = 0x0101010101010101ull << (x & 7);
+        const int t0 = ru.y0 >> 3, t1 = ru.y1 >> 3;
+        const unsigned long long* col = V.Fsc + tx * V.wc;
+        for (int w = t0 >> 6; w <= (t1 >> 6); w++) {
+            const int lo = max(t0 - w * 64, 0), hi = min(t1 - w * 64, 63);
+            unsigned long long m = col[w] & (~0ull << lo) & (~0ull >> (63 - hi));
+            while (m) {
+                const int ty = w * 64 + __ffsll((long long)m) - 1;
+                m &= m - 1;
+                const int a = max((int)ru.y0, ty * 8) & 7, b = min((int)ru.y1, ty * 8 + 7) & 7;
+                if (V.F[ty * V.tw + tx] & colm & (~0ull >> (8 * (7 - b))) & (~0ull << (8 * a))) return true;
+            }
+        }
+        return false;
+    } else {                       // diagonal: cell by cell, skipping empty tiles
+        const int dy = (ru.y1 > ru.y0) ? 1 : -1;
+        int y = ru.y0;
+        for (int x = ru.x0; x <= ru.x1; x++, y += dy) {
+            const int tx = x >> 3, ty = y >> 3;
+            if (!((V.Fsr[ty * V.wr + (tx >> 6)] >> (tx & 63)) & 1ull)) continue;
+            if (V.F[ty * V.tw + tx] & (1ull << ((y & 7) * 8 + (x & 7)))) return true;
+        }
+        return false;
+    }
+}
+
 struct TileShared {
     int src, qn, hn, item;
     unsigned long long cnt, mass;
@@ -156,13 +211,19 @@ __device__ __forceinline__ bool special_hit(const VgaTileParams& P, const unsign
 
 // V (visited) and X (next level) are per-workgroup bitmaps in HBM (they stay in the L2/MALL; a
 // source touches each word a few times), F (frontier, read by every run test) is in LDS.
-template <int NT>
+// SPECIAL = false: the graph has no asymmetric nodes (every U_f cell is regular), no exact path.
+template <int NT, bool SPECIAL>
 __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long F[];
     __shared__ TileShared S;
     constexpr int NW = NT / 64;
     const int nt = P.tw * P.th;
-    int* hist = (int*)(F + nt);
+    const int wr = (P.tw + 63) / 64, wc = (P.th + 63) / 64, nfs = P.th * wr + P.tw * wc;
+    unsigned long long* Fsr = F + nt;           // [th][wr]
+    unsigned long long* Fsc = Fsr + P.th * wr;  // [tw][wc]
+    int* hist = (int*)(Fsc + P.tw * wc);
+    FView FV;
+    FV.F = F; FV.Fsr = Fsr; FV.Fsc = Fsc; FV.tw = P.tw; FV.wr = wr; FV.wc = wc;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tw = P.tw, rows = P.rows;
     unsigned long long* Vg = P.xg + (size_t)blockIdx.x * 2 * nt;
@@ -241,7 +302,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                                 const Run c = P.cr[CRK * t + j];
                                 if (c.x0 < 0) break;
                                 runs_tested++;
-                                hit = run_hits(F, tw, c);
+                                hit = run_hits_fs(FV, c);
                             }
                             if (hit) { Xg[t] = R; U &= ~R; cr_tiles++; }
                         }
@@ -269,25 +330,38 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     int hard_val = 0;
                     if ((mask >> lane) & 1ull) {
                         const int id = (t << 6) | lane;
-                        if (!((P.regular_tiles[t] >> lane) & 1ull)) {
+                        if (SPECIAL && !((P.regular_tiles[t] >> lane) & 1ull)) {
                             to_hard = true;
                             hard_val = -1 - id;   // special node: exact path
                         } else {
+                            const int64_t ss = P.tscan_start[id];
+                            const int nr = P.tnruns[id];
                             const int hp = Hn[id];
-                            if (hp >= KH && hp != 0xFFFF) {   // the run that hit for a recent source
+                            if (hp >= KH && hp < nr) {   // the run that hit for a recent source
                                 runs_tested++;
-                                hit = run_hits(F, tw, P.scan_pool[P.tscan_start[id] + hp]);
+                                hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
                             }
-                            int h = 0;
-                            for (; h < KH && !hit; h++) {
-                                const Run hr = P.heads[h * hstride + id];
-                                if (hr.x0 < 0) break;
-                                if (run_hits(F, tw, hr)) { hit = true; if (hp != h) Hn[id] = (uint16_t)h; h++; break; }
+                            // heads (coalesced across the wave), then the next runs of the scan order
+                            // on this lane; 4 loads in flight per batch
+                            const int lim = min(nr, KH + BEXT);
+                            for (int base = 0; base < lim && !hit; base += 4) {
+                                Run rr[4];
+#pragma unroll
+                                for (int j = 0; j < 4; j++) {
+                                    const int r = base + j;
+                                    if (r < KH) rr[j] = P.heads[r * hstride + id];
+                                    else if (r < lim) rr[j] = P.scan_pool[ss + r];
+                                    else rr[j].x0 = -1;
+                                }
+#pragma unroll
+                                for (int j = 0; j < 4; j++)
+                                    if (!hit && rr[j].x0 >= 0) {
+                                        runs_tested++;
+                                        if (run_hits_fs(FV, rr[j])) { hit = true; if (hp != base + j) Hn[id] = (uint16_t)(base + j); }
+                                    }
                             }
-                            runs_tested += h;
                             if (!hit) {
-                                const int nr = P.tnruns[id];
-                                if (nr > h) { to_hard = true; hard_val = id; }
+                                if (nr > KH + BEXT) { to_hard = true; hard_val = id; }
                                 else { fail_cells++; fail_runs += nr; }
                             }
                         }
@@ -316,7 +390,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     if (special) id = -1 - id;
                     bool found = false;
                     int nr = 0;
-                    if (special) {
+                    if (SPECIAL && special) {
                         int x, y;
                         xy_of_tile_id(id, tw, x, y);
                         found = special_hit(P, F, x, y, &nr);
@@ -324,7 +398,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     } else {
                         const int64_t rs = P.tscan_start[id];
                         nr = P.tnruns[id];
-                        int base = KH;   // the first KH runs (the heads) were tested in phase B
+                        int base = KH + BEXT;   // the first KH + BEXT runs were tested in phase B
                         // 4 runs per lane per step (256 per wave): four independent loads in flight
                         for (; base < nr && !found; base += 256) {
                             Run rr[4];
@@ -337,13 +411,13 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                             int first = 1 << 30;
 #pragma unroll
                             for (int j = 0; j < 4; j++)
-                                if (first == (1 << 30) && rr[j].x0 >= 0 && run_hits(F, tw, rr[j])) first = base + j * 64 + lane;
+                                if (first == (1 << 30) && rr[j].x0 >= 0 && run_hits_fs(FV, rr[j])) first = base + j * 64 + lane;
                             int fmin = first;
                             for (int off = 32; off >= 1; off >>= 1) fmin = min(fmin, __shfl_xor(fmin, off));
                             found = fmin != (1 << 30);
                             if (found && lane == 0) Hn[id] = (uint16_t)min(fmin, 0xFFFE);
                         }
-                        if (lane == 0) runs_tested += (unsigned long long)(min(base, nr) - KH);
+                        if (lane == 0) runs_tested += (unsigned long long)(min(base, nr) - KH - BEXT);
                     }
                     if (lane == 0) {
                         if (found) or_wg(&Xg[id >> 6], 1ull << (id & 63));
@@ -391,6 +465,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 tmark = n;
             }
             // ---- level bookkeeping: count X, publish the expandable part as the next frontier
+            for (int i = tid; i < nfs; i += NT) Fsr[i] = 0ull;
+            __syncthreads();
             unsigned long long c_loc = 0, m_loc = 0;
             for (int t = tid; t < nt; t += NT) {
                 unsigned long long x = ld_wg(&Xg[t]);
@@ -400,6 +476,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     Xg[t] = 0ull;
                     if (P.radius != -1) x &= ~P.nonexp_tiles[t];
                     m_loc += (unsigned long long)__popcll(x);
+                    if (x) {
+                        const int tx = t % tw, ty = t / tw;
+                        atomicOr(&Fsr[ty * wr + (tx >> 6)], 1ull << (tx & 63));
+                        atomicOr(&Fsc[tx * wc + (ty >> 6)], 1ull << (ty & 63));
+                    }
                 }
                 F[t] = x;
             }
