@@ -26,6 +26,22 @@ PointMapHost::PointMapHost(const Rect& region, double spacing, const double* lin
     seg_off_.assign((size_t)cells() + 1, 0);
 }
 
+void PointMapHost::load_state(int cols, int rows, double spacing, Vec2 bl, const int32_t* state) {
+    cols_ = cols;
+    rows_ = rows;
+    spacing_ = spacing;
+    bl_ = bl;
+    region_ = Rect{bl_.x - spacing_ / 2.0, bl_.y - spacing_ / 2.0, bl_.x + double(cols_ - 1) * spacing_ + spacing_ / 2.0,
+                   bl_.y + double(rows_ - 1) * spacing_ + spacing_ / 2.0};
+    state_.assign(state, state + (size_t)cells());
+    seg_off_.assign((size_t)cells() + 1, 0);
+    segs_.clear();
+    draw_.clear();
+    blocked_ = true;
+    filled_ = 0;
+    for (int32_t s : state_) filled_ += (s & CELL_FILLED) ? 1 : 0;
+}
+
 Rect PointMapHost::cell_rect(int x, int y, double border) const {
     return Rect{bl_.x + spacing_ * (double(x) - 0.5 - border), bl_.y + spacing_ * (double(y) - 0.5 - border),
                 bl_.x + spacing_ * (double(x) + 0.5 + border), bl_.y + spacing_ * (double(y) + 0.5 + border)};

@@ -39,6 +39,10 @@ class PointMapHost {
     // Returns 0 = filled, 1 = point outside region, 2 = makePoints refused (off-grid, already
     // filled, or seed hidden from its cell centre).
     int fill(double x, double y);
+    // A map restored from a .graph PointMap chunk: grid geometry and cell states as stored
+    // (PointMap::read, pointdata.cpp:1073-1156).  No occluder pieces: such a map can run VGA and
+    // step depth on its graph but not makeGraph.
+    void load_state(int cols, int rows, double spacing, Vec2 bl, const int32_t* state);
     // PointMap::sparkGraph2's boundary-graph pre-pass (pointdata.cpp:1254-1264).
     void keep_edges_only();
     void block_lines(); // idempotent (m_blockedlines)

@@ -127,6 +127,32 @@ int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
 /* Kernel time of the last step-depth call, expanders popped, cells relaxed. */
 int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_popped, int64_t* cells_relaxed);
 
+/* ---- .graph PointMap chunk (host) ------------------------------------------------------------ */
+/* The bytes PointMap::write emits into a .graph file (salalib/pointdata.cpp:1158-1188, with
+ * AttributeTable::write attributetable.cpp:427-456, Point::write point.cpp:51-73, Node/Bin/PixelVec
+ * write ngraph.cpp:209-220,447-472,517-583): header, attribute table (columns alphabetical, stats
+ * replayed in setValue order), every cell x-major with its run-length node (4-bit ShiftLength).
+ * bins/runs/gridconn as dmx_graph_copy returns them; values [ncols][nnodes] in insertion order;
+ * displayed indexes the columns.  buf NULL (or cap too small): only *size is set. */
+int dmx_chunk_write(const dmx_pointmap* pm, int64_t nnodes, const int32_t* bins, const int16_t* runs, int64_t nruns,
+                    const uint8_t* gridconn, int ncols, const char* const* names, const float* values,
+                    const uint8_t* locked, int displayed, int boundary, uint8_t* buf, int64_t cap, int64_t* size);
+/* PointMap::read (pointdata.cpp:1073-1156, ngraph.cpp:420-445,491-563): decode a chunk; runs come
+ * back with the reference's lossy 4-bit row shift applied. */
+typedef struct dmx_chunk dmx_chunk;
+int dmx_chunk_parse(const uint8_t* buf, int64_t size, dmx_chunk** out);
+int dmx_chunk_free(dmx_chunk* c);
+int dmx_chunk_info(const dmx_chunk* c, int32_t* cols, int32_t* rows, double* spacing, double* bl, int64_t* nnodes,
+                   int64_t* nruns, int32_t* ncols, int32_t* displayed_sorted, int64_t* bytes_used);
+int dmx_chunk_column(const dmx_chunk* c, int i, char* name, int name_cap, float* values, int* locked);
+int dmx_chunk_arrays(const dmx_chunk* c, int32_t* state, int32_t* bins, int16_t* runs, uint8_t* gridconn);
+/* A state-only point map (region = MetaGraph::getRegion()) and its device graph from a chunk: what
+ * the reference CLI's VGA / STEPDEPTH steps analyse after loadGraph (runmethods.cpp:33). */
+int dmx_chunk_load(dmx_ctx* ctx, const dmx_chunk* c, const double* region, dmx_pointmap** pm, dmx_graph** g);
+/* Device graph from host node records (e.g. a graph the reference itself built or loaded). */
+int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const int32_t* bins, const int16_t* runs,
+                        int64_t nruns, const uint8_t* gridconn, const float* attrs, dmx_graph** out);
+
 #ifdef __cplusplus
 }
 #endif

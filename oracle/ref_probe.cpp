@@ -202,6 +202,12 @@ int main(int argc, char** argv) {
         }
         nodes++;
     }
+    {
+        // the PointMap chunk of the .graph file exactly as MetaGraph::write emits it after VISPREP
+        // (PointMap::write, salalib/pointdata.cpp:1158-1188)
+        std::ofstream cf(outDir + "/pm_chunk_mk.bin", std::ios::binary);
+        pm.write(cf);
+    }
     dump(outDir + "/attrs.bin", attrs);
     dump(outDir + "/bins.bin", bins);
     dump(outDir + "/runs.bin", runs);

@@ -104,6 +104,11 @@ def run_case(name):
             arrays["vga"] = rd("vga.bin", np.float32).reshape(N, 7)
         if rt:
             arrays["vga_rt"] = rd("vga_rt.bin", np.float32).reshape(N, 7)
+        chunk = open(os.path.join(d, "pm_chunk_mk.bin"), "rb").read()
+        arrays["pm_chunk_sha256"] = np.frombuffer(hashlib.sha256(chunk).digest(), dtype=np.uint8)
+        arrays["pm_chunk_size"] = np.array([len(chunk)], dtype=np.int64)
+        if len(chunk) <= 64 * 1024:
+            arrays["pm_chunk"] = np.frombuffer(chunk, dtype=np.uint8)
         if name in STEPDEPTH:
             arrays["stepdepth"] = rd("stepdepth.bin", np.float32).reshape(N, 3)
             arrays["stepdepth_sel"] = rd("stepdepth_sel.bin", np.int32)
