@@ -40,7 +40,8 @@ SIGNATURES = {
     "dmx_metric_stepdepth": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "dmx_ctx_last_stepdepth": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_ctx_last_phase_cycles": (_i32, [_vp, _vp]),
-    "dmx_chunk_write": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
+    "dmx_chunk_write": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
+    "dmx_pointmap_set_state": (_i32, [_vp, _vp]),
     "dmx_chunk_parse": (_i32, [_vp, _i64, _vp]),
     "dmx_chunk_free": (_i32, [_vp]),
     "dmx_chunk_info": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -32,14 +32,32 @@ def up_to_date():
     return all(os.path.getmtime(p) <= t for p in _deps())
 
 
+CLI_SRC = os.path.join(CSRC, "cli", "dmxcli.cpp")
+CLI_OUT = os.path.join(HERE, "_lib", "dmxcli")
+
+
+def build_cli(verbose=True):
+    """The depthmapXcli-compatible front-end (host C++ over libdmx.so)."""
+    if os.path.exists(CLI_OUT) and os.path.getmtime(CLI_OUT) >= max(os.path.getmtime(CLI_SRC), os.path.getmtime(OUT)):
+        return CLI_OUT
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", CLI_SRC, "-o", CLI_OUT,
+           "-L" + os.path.dirname(OUT), "-ldmx", "-Wl,-rpath,$ORIGIN"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return CLI_OUT
+
+
 def build(force=False, verbose=True):
     if not force and up_to_date():
+        build_cli(verbose)
         return OUT
     os.makedirs(os.path.dirname(OUT), exist_ok=True)
     cmd = [HIPCC] + FLAGS + ["-o", OUT] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
+    build_cli(verbose)
     return OUT
 
 

@@ -1,0 +1,693 @@
+// dmxcli -- command-line front-end of the MI355X engine with the depthmapXcli mode-parser surface
+// for the accelerated path: VISPREP (grid, fill, makeGraph), VGA (-vm visibility -vg -vr) and
+// STEPDEPTH (-sdt metric).  Flags, validation messages, the "-t" timing CSV and the exit status
+// follow the reference CLI:
+//   depthmapXcli/main.cpp:22-54, commandlineparser.cpp:51-142, visprepparser.cpp:26-172,
+//   vgaparser.cpp:29-106, radiusconverter.cpp:24-61, stepdepthparser.cpp:26-100,
+//   runmethods.cpp:33-45 (loadGraph), :227-267 (runVga), :279-341 (runVisualPrep),
+//   :735-778 (runStepDepth), performancewriter.cpp:60-76, salalib/gridproperties.cpp:4-13.
+// Host code over the C ABI (include/dmx.h); every analysis runs on the GPU.
+//
+// Files: the input of VISPREP is a drawing -- a CSV of lines (header x1,y1,x2,y2; what
+// "depthmapXcli -m IMPORT -it drawing" ingests) or a container written by this tool.  Output
+// containers (".dmxg") hold the region, the drawing lines and the PointMap chunk of the .graph
+// format, byte-identical to what PointMap::write emits ("The .graph boundary").
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../include/dmx.h"
+
+namespace {
+
+struct CommandLineException : std::runtime_error { using std::runtime_error::runtime_error; };
+struct RuntimeException : std::runtime_error { using std::runtime_error::runtime_error; };
+
+bool has_only_digits(const std::string& s) { return s.find_first_not_of("0123456789") == std::string::npos; }
+bool has_only_digits_dots_commas(const std::string& s) { return s.find_first_not_of("0123456789,.-") == std::string::npos; }
+
+// ENFORCE_ARGUMENT (depthmapXcli/parsingutils.h:19-25)
+void enforce_argument(const char* flag, int& i, int argc, char** argv) {
+    if (++i >= argc || (argv[i][0] == '-' && !isdigit((unsigned char)argv[i][1]) && argv[i][1] != '.'))
+        throw CommandLineException(std::string(flag) + " requires an argument");
+}
+
+void check(int rc) {
+    if (rc != DMX_OK) throw RuntimeException(dmx_last_error());
+}
+
+// PerformanceWriter (performancewriter.cpp:60-76) + DO_TIMED (runmethods.h:37-40)
+struct Perf {
+    std::string file;
+    std::vector<std::string> lines;
+    void add(const std::string& action, double s) {
+        std::stringstream ss;
+        ss << "\"" << action << "\"," << s << "\n";
+        lines.push_back(ss.str());
+    }
+    void write() const {
+        if (file.empty()) return;
+        std::ofstream f(file);
+        f << "\"action\",\"duration\"\n";
+        for (auto& l : lines) f << l;
+    }
+};
+template <typename F> void timed(Perf& perf, const char* action, F&& f) {
+    const auto t0 = std::chrono::steady_clock::now();
+    f();
+    perf.add(action, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+}
+
+// EntityParsing::parsePoints (salalib/entityparsing.cpp:116-170): header naming x and y columns
+std::vector<std::pair<double, double>> parse_points(std::istream& in, char delim) {
+    std::string line;
+    std::getline(in, line);
+    std::vector<std::string> head;
+    {
+        std::stringstream ss(line);
+        std::string t;
+        while (std::getline(ss, t, delim)) {
+            std::transform(t.begin(), t.end(), t.begin(), ::tolower);
+            head.push_back(t);
+        }
+    }
+    if (head.size() < 2) throw RuntimeException("Badly formatted header (should contain x and y)");
+    int xc = -1, yc = -1;
+    for (size_t i = 0; i < head.size(); i++) {
+        if (head[i] == "x") xc = (int)i;
+        else if (head[i] == "y") yc = (int)i;
+    }
+    if (xc < 0 || yc < 0) throw RuntimeException("Badly formatted header (should contain x and y)");
+    std::vector<std::pair<double, double>> pts;
+    while (std::getline(in, line)) {
+        if (line.empty()) continue;
+        std::vector<std::string> f;
+        std::stringstream ss(line);
+        std::string t;
+        while (std::getline(ss, t, delim)) f.push_back(t);
+        if ((int)f.size() <= std::max(xc, yc)) throw RuntimeException("Error parsing line: " + line);
+        pts.emplace_back(std::stod(f[xc]), std::stod(f[yc]));
+    }
+    return pts;
+}
+
+std::vector<std::pair<double, double>> points_from_args(const std::vector<std::string>& pts, const std::string& file) {
+    if (!file.empty()) {
+        std::ifstream f(file);
+        if (!f) {
+            std::stringstream m;
+            m << "Failed to load file " << file << ", error " << std::strerror(errno);
+            throw RuntimeException(m.str());
+        }
+        return parse_points(f, '\t');
+    }
+    std::stringstream ss;
+    ss << "x,y";
+    for (auto& p : pts) ss << "\n" << p;
+    return parse_points(ss, ',');
+}
+
+// ---------------------------------------------------------------- the document (".dmxg" container)
+struct Column {
+    std::string name;
+    std::vector<float> values;
+    bool locked = false;
+    std::vector<uint8_t> set;
+};
+
+struct Document {
+    double region[4] = {0, 0, 0, 0};
+    std::vector<double> lines;        // [L][4]
+    bool has_map = false;
+    std::vector<uint8_t> chunk;       // PointMap::write bytes
+};
+
+const char kMagic[4] = {'D', 'M', 'X', 'G'};
+
+Document read_document(const std::string& path) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) throw RuntimeException("Failed to load graph from file " + path + ", error -1");
+    Document d;
+    char magic[4] = {0, 0, 0, 0};
+    f.read(magic, 4);
+    if (std::memcmp(magic, kMagic, 4) != 0) {
+        // a drawing: CSV of lines x1,y1,x2,y2 (the reference's IMPORT -it drawing input)
+        f.close();
+        std::ifstream t(path);
+        std::string line;
+        std::getline(t, line);
+        double mn[2] = {1e300, 1e300}, mx[2] = {-1e300, -1e300};
+        while (std::getline(t, line)) {
+            if (line.empty()) continue;
+            double v[4];
+            if (std::sscanf(line.c_str(), "%lf,%lf,%lf,%lf", &v[0], &v[1], &v[2], &v[3]) != 4)
+                throw RuntimeException("Failed to load graph from file " + path + ", error -1");
+            for (int i = 0; i < 4; i++) d.lines.push_back(v[i]);
+            for (int i = 0; i < 2; i++) {
+                mn[0] = std::min(mn[0], v[2 * i]); mx[0] = std::max(mx[0], v[2 * i]);
+                mn[1] = std::min(mn[1], v[2 * i + 1]); mx[1] = std::max(mx[1], v[2 * i + 1]);
+            }
+        }
+        if (d.lines.empty()) throw RuntimeException("Failed to load graph from file " + path + ", error -1");
+        d.region[0] = mn[0]; d.region[1] = mn[1]; d.region[2] = mx[0]; d.region[3] = mx[1];
+        return d;
+    }
+    uint32_t version = 0;
+    f.read((char*)&version, 4);
+    f.read((char*)d.region, sizeof(d.region));
+    int64_t nl = 0;
+    f.read((char*)&nl, 8);
+    d.lines.resize((size_t)nl * 4);
+    if (nl) f.read((char*)d.lines.data(), (std::streamsize)(nl * 32));
+    uint8_t hm = 0;
+    f.read((char*)&hm, 1);
+    d.has_map = hm != 0;
+    if (d.has_map) {
+        int64_t n = 0;
+        f.read((char*)&n, 8);
+        d.chunk.resize((size_t)n);
+        f.read((char*)d.chunk.data(), (std::streamsize)n);
+    }
+    if (!f) throw RuntimeException("Failed to load graph from file " + path + ", error -1");
+    return d;
+}
+
+void write_document(const std::string& path, const Document& d) {
+    std::ofstream f(path, std::ios::binary | std::ios::trunc);
+    if (!f) throw RuntimeException("Failed to write " + path);
+    f.write(kMagic, 4);
+    const uint32_t version = 1;
+    f.write((const char*)&version, 4);
+    f.write((const char*)d.region, sizeof(d.region));
+    const int64_t nl = (int64_t)d.lines.size() / 4;
+    f.write((const char*)&nl, 8);
+    if (nl) f.write((const char*)d.lines.data(), (std::streamsize)(nl * 32));
+    const uint8_t hm = d.has_map ? 1 : 0;
+    f.write((const char*)&hm, 1);
+    if (d.has_map) {
+        const int64_t n = (int64_t)d.chunk.size();
+        f.write((const char*)&n, 8);
+        f.write((const char*)d.chunk.data(), (std::streamsize)n);
+    }
+}
+
+struct Context {
+    dmx_ctx* ctx = nullptr;
+    Context() { check(dmx_ctx_create(0, &ctx)); }
+    ~Context() { dmx_ctx_free(ctx); }
+};
+
+struct LoadedMap {
+    dmx_chunk* chunk = nullptr;
+    dmx_pointmap* pm = nullptr;
+    dmx_graph* g = nullptr;
+    int64_t nnodes = 0, nruns = 0;
+    std::vector<Column> columns;
+    std::vector<int32_t> bins;
+    std::vector<int16_t> runs;
+    std::vector<uint8_t> gridconn;
+    ~LoadedMap() {
+        if (g) dmx_graph_free(g);
+        if (pm) dmx_pointmap_free(pm);
+        if (chunk) dmx_chunk_free(chunk);
+    }
+};
+
+// loadGraph for an analysis step: the PointMap chunk decoded (4-bit shift quirk included) and its
+// graph uploaded to the GPU.
+void load_map(Context& C, const Document& d, LoadedMap& m) {
+    if (!d.has_map) throw RuntimeException("No map exists to use. Please create a new one by providing a grid size");
+    check(dmx_chunk_parse(d.chunk.data(), (int64_t)d.chunk.size(), &m.chunk));
+    int32_t ncols = 0, disp = 0;
+    check(dmx_chunk_info(m.chunk, nullptr, nullptr, nullptr, nullptr, &m.nnodes, &m.nruns, &ncols, &disp, nullptr));
+    m.columns.resize(ncols);
+    for (int i = 0; i < ncols; i++) {
+        char name[512];
+        int locked = 0;
+        m.columns[i].values.resize(m.nnodes);
+        check(dmx_chunk_column(m.chunk, i, name, sizeof(name), m.columns[i].values.data(), &locked));
+        m.columns[i].name = name;
+        m.columns[i].locked = locked != 0;
+    }
+    m.bins.resize((size_t)m.nnodes * 128);
+    m.runs.resize((size_t)std::max<int64_t>(m.nruns, 1) * 4);
+    m.gridconn.resize((size_t)m.nnodes);
+    check(dmx_chunk_arrays(m.chunk, nullptr, m.bins.data(), m.runs.data(), m.gridconn.data()));
+    check(dmx_chunk_load(C.ctx, m.chunk, d.region, &m.pm, &m.g));
+}
+
+std::vector<uint8_t> write_chunk(dmx_pointmap* pm, int64_t n, const int32_t* bins, const int16_t* runs, int64_t nruns,
+                                 const uint8_t* gc, const std::vector<Column>& cols, int displayed) {
+    std::vector<const char*> names;
+    std::vector<float> vals;
+    std::vector<uint8_t> locked, masks;
+    for (auto& c : cols) {
+        names.push_back(c.name.c_str());
+        vals.insert(vals.end(), c.values.begin(), c.values.end());
+        locked.push_back(c.locked ? 1 : 0);
+        if (c.set.empty()) masks.insert(masks.end(), (size_t)n, (uint8_t)1);
+        else masks.insert(masks.end(), c.set.begin(), c.set.end());
+    }
+    int64_t size = 0;
+    check(dmx_chunk_write(pm, n, bins, runs, nruns, gc, (int)cols.size(), names.data(), vals.data(), locked.data(),
+                          masks.data(), displayed, 0, nullptr, 0, &size));
+    std::vector<uint8_t> out((size_t)size);
+    check(dmx_chunk_write(pm, n, bins, runs, nruns, gc, (int)cols.size(), names.data(), vals.data(), locked.data(),
+                          masks.data(), displayed, 0, out.data(), size, &size));
+    return out;
+}
+
+// ---------------------------------------------------------------- modes (IModeParser, imodeparser.h:24-32)
+struct Args {
+    std::string file, out, timing;
+    bool simple = false, progress = false;
+};
+
+struct Mode {
+    virtual ~Mode() {}
+    virtual std::string name() const = 0;
+    virtual void parse(int argc, char** argv) = 0;
+    virtual void run(const Args& a, Perf& perf) = 0;
+};
+
+// VisPrepParser (visprepparser.cpp:26-172) + runVisualPrep (runmethods.cpp:279-341)
+struct VisPrep : Mode {
+    double grid = -1, maxvis = -1;
+    bool boundary = false, make = false, unmake = false, removeLinks = false;
+    std::vector<std::pair<double, double>> fills;
+    std::string name() const override { return "VISPREP"; }
+    void parse(int argc, char** argv) override {
+        std::vector<std::string> points;
+        std::string pointFile;
+        for (int i = 1; i < argc; ++i) {
+            if (!std::strcmp("-pg", argv[i])) {
+                if (grid >= 0) throw CommandLineException("-pg can only be used once");
+                enforce_argument("-pg", i, argc, argv);
+                grid = std::atof(argv[i]);
+                if (grid <= 0) throw CommandLineException(std::string("-pg must be a number >0, got ") + argv[i]);
+            } else if (!std::strcmp("-pp", argv[i])) {
+                if (!pointFile.empty()) throw CommandLineException("-pp cannot be used together with -pf");
+                enforce_argument("-pp", i, argc, argv);
+                if (!has_only_digits_dots_commas(argv[i])) {
+                    std::stringstream m;
+                    m << "Invalid fill point provided (" << argv[i] << "). Should only contain digits dots and commas";
+                    throw CommandLineException(m.str());
+                }
+                points.push_back(argv[i]);
+            } else if (!std::strcmp("-pf", argv[i])) {
+                if (!points.empty()) throw CommandLineException("-pf cannot be used together with -pp");
+                enforce_argument("-pf", i, argc, argv);
+                pointFile = argv[i];
+            } else if (!std::strcmp("-pr", argv[i])) {
+                enforce_argument("-pr", i, argc, argv);
+                maxvis = std::atof(argv[i]);
+                if (maxvis == 0.0) {
+                    std::stringstream m;
+                    m << "Restricted visibility of '" << argv[i] << "' makes no sense, use a positive number or -1 for unrestricted";
+                    throw CommandLineException(m.str());
+                }
+            } else if (!std::strcmp("-pb", argv[i])) {
+                boundary = true;
+            } else if (!std::strcmp("-pm", argv[i])) {
+                if (unmake) throw CommandLineException("-pm cannot be used together with -pu");
+                make = true;
+            } else if (!std::strcmp("-pu", argv[i])) {
+                if (make) throw CommandLineException("-pu cannot be used together with -pm");
+                unmake = true;
+            } else if (!std::strcmp("-pl", argv[i])) {
+                removeLinks = true;
+            }
+        }
+        if (!make && !unmake && grid <= 0 && pointFile.empty() && points.empty()) throw CommandLineException("Nothing to do");
+        if (grid > 0 && make && pointFile.empty() && points.empty())
+            throw CommandLineException("Creating a graph for an unfilled grid is not possible. Either -pp or -pf must be given");
+        if (!pointFile.empty() || !points.empty()) fills = points_from_args(points, pointFile);
+        if (unmake && (grid > 0 || !fills.empty()))
+            throw CommandLineException("-pu can not be used with any other option apart from -pl");
+        if (removeLinks && !unmake) throw CommandLineException("-pl can only be used together with -pu");
+    }
+    void run(const Args& a, Perf& perf) override {
+        Document d;
+        timed(perf, "Load graph file", [&] { d = read_document(a.file); });
+        std::cout << "Initial checks... " << std::flush;
+        if (d.lines.empty()) throw RuntimeException("Graph must have line data before preparing VGA");
+        Context C;
+        dmx_pointmap* pm = nullptr;
+        std::unique_ptr<dmx_pointmap, int (*)(dmx_pointmap*)> pmguard(nullptr, dmx_pointmap_free);
+        double spacing = grid;
+        if (grid > 0) {
+            // GridProperties (salalib/gridproperties.cpp:4-13)
+            const double maxdim = std::max(d.region[2] - d.region[0], d.region[3] - d.region[1]);
+            const int maxexp = (int)std::floor(std::log10(maxdim)) - 1, minexp = maxexp - 2;
+            const int mant = (int)std::floor(maxdim / std::pow(10.0, double(maxexp + 1)));
+            const double gmax = (double)2 * mant * std::pow(10.0, double(maxexp));
+            const double gmin = (double)mant * std::pow(10.0, double(minexp));
+            if (grid > gmax || grid < gmin) {
+                std::stringstream m;
+                m << "Chosen grid spacing " << grid << " is outside of the expected interval of " << gmin
+                  << " <= spacing <= " << gmax;
+                throw RuntimeException(m.str());
+            }
+            std::cout << "ok\nSetting up grid... " << std::flush;
+            timed(perf, "Setting grid", [&] {
+                check(dmx_pointmap_create(d.region, grid, d.lines.data(), (int64_t)d.lines.size() / 4, &pm));
+            });
+            pmguard.reset(pm);
+        } else {
+            if (!d.has_map) throw RuntimeException("No map exists to use. Please create a new one by providing a grid size");
+            dmx_chunk* ch = nullptr;
+            check(dmx_chunk_parse(d.chunk.data(), (int64_t)d.chunk.size(), &ch));
+            int32_t cols = 0, rows = 0;
+            check(dmx_chunk_info(ch, &cols, &rows, &spacing, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
+            std::vector<int32_t> st((size_t)cols * rows);
+            check(dmx_chunk_arrays(ch, st.data(), nullptr, nullptr, nullptr));
+            dmx_chunk_free(ch);
+            check(dmx_pointmap_create(d.region, spacing, d.lines.data(), (int64_t)d.lines.size() / 4, &pm));
+            pmguard.reset(pm);
+            check(dmx_pointmap_set_state(pm, st.data()));
+        }
+        if (unmake) throw RuntimeException("Unmaking a graph is not part of the accelerated path");
+        if (!fills.empty()) {
+            std::cout << "ok\nFilling grid... " << std::flush;
+            timed(perf, "Filling grid", [&] {
+                for (auto& p : fills) {
+                    int made = 0;
+                    // fillGraph (runmethods.cpp:269-277)
+                    check(dmx_pointmap_fill(pm, p.first, p.second, &made));
+                }
+            });
+        }
+        std::vector<Column> cols;
+        dmx_graph* g = nullptr;
+        int64_t n = 0, nr = 0;
+        if (make) {
+            std::cout << "ok\nMaking graph... " << std::flush;
+            timed(perf, "Making graph", [&] { check(dmx_makegraph(C.ctx, pm, maxvis, boundary ? 1 : 0, 0, -1, &g)); });
+        }
+        std::cout << " ok\nWriting out result..." << std::flush;
+        timed(perf, "Writing graph", [&] {
+            std::vector<int32_t> bins;
+            std::vector<int16_t> runs;
+            std::vector<uint8_t> gc;
+            if (g) {
+                int64_t b, e;
+                check(dmx_graph_info(g, &n, &b, &e, &nr));
+                std::vector<float> attrs((size_t)n * 3);
+                bins.resize((size_t)n * 128);
+                runs.resize((size_t)std::max<int64_t>(nr, 1) * 4);
+                gc.resize((size_t)n);
+                check(dmx_graph_copy(g, attrs.data(), bins.data(), runs.data(), gc.data()));
+                const char* mk[3] = {"Connectivity", "Point First Moment", "Point Second Moment"};
+                for (int j = 0; j < 3; j++) {
+                    Column c;
+                    c.name = mk[j];
+                    c.locked = j == 0;
+                    c.values.resize((size_t)n);
+                    for (int64_t k = 0; k < n; k++) c.values[k] = attrs[k * 3 + j];
+                    cols.push_back(c);
+                }
+                dmx_graph_free(g);
+            } else {
+                int64_t filled = 0;
+                check(dmx_pointmap_info(pm, nullptr, nullptr, nullptr, nullptr, &filled));
+                n = filled;
+                bins.assign((size_t)n * 128, 0);
+                gc.assign((size_t)n, 0);
+                runs.assign(4, 0);
+            }
+            d.chunk = write_chunk(pm, n, bins.data(), runs.data(), nr, gc.data(), cols, cols.empty() ? -1 : 0);
+            d.has_map = true;
+            write_document(a.out, d);
+        });
+        std::cout << " ok" << std::endl;
+    }
+};
+
+// VgaParser (vgaparser.cpp:29-106), RadiusConverter (radiusconverter.cpp:24-37), runVga (runmethods.cpp:227-267)
+struct Vga : Mode {
+    enum { NONE, ISOVIST, VISIBILITY, METRIC, ANGULAR, THRU } mode = NONE;
+    bool local = false, global = false;
+    std::string radius;
+    std::string name() const override { return "VGA"; }
+    void parse(int argc, char** argv) override {
+        for (int i = 1; i < argc;) {
+            if (!std::strcmp("-vm", argv[i])) {
+                if (mode != NONE) throw CommandLineException("-vm can only be used once, modes are mutually exclusive");
+                enforce_argument("-vm", i, argc, argv);
+                if (!std::strcmp(argv[i], "isovist")) mode = ISOVIST;
+                else if (!std::strcmp(argv[i], "visibility")) mode = VISIBILITY;
+                else if (!std::strcmp(argv[i], "metric")) mode = METRIC;
+                else if (!std::strcmp(argv[i], "angular")) mode = ANGULAR;
+                else if (!std::strcmp(argv[i], "thruvision")) mode = THRU;
+                else throw CommandLineException(std::string("Invalid VGA mode: ") + argv[i]);
+            } else if (!std::strcmp(argv[i], "-vg")) {
+                global = true;
+            } else if (!std::strcmp(argv[i], "-vl")) {
+                local = true;
+            } else if (!std::strcmp(argv[i], "-vr")) {
+                enforce_argument("-vr", i, argc, argv);
+                radius = argv[i];
+            }
+            ++i;
+        }
+        if (mode == NONE) mode = ISOVIST;
+        if (mode == VISIBILITY && global) {
+            if (radius.empty())
+                throw CommandLineException("Global measures in VGA/visibility analysis require a radius, use -vr <radius>");
+            if (radius != "n" && !has_only_digits(radius))
+                throw CommandLineException(std::string("Radius must be a positive integer number or n, got ") + radius);
+        } else if (mode == METRIC) {
+            if (radius.empty()) throw CommandLineException("Metric vga requires a radius, use -vr <radius>");
+        }
+    }
+    void run(const Args& a, Perf& perf) override {
+        Document d;
+        timed(perf, "Load graph file", [&] { d = read_document(a.file); });
+        Context C;
+        LoadedMap m;
+        load_map(C, d, m);
+        std::cout << "Getting options..." << std::flush;
+        if (mode != VISIBILITY) throw RuntimeException("Only -vm visibility is part of the accelerated path");
+        if (local) throw RuntimeException("-vl (visual local) is not part of the accelerated path yet");
+        double r = -1.0;
+        if (global) {
+            if (radius != "n") {
+                const long rad = std::strtol(radius.c_str(), nullptr, 10);
+                if (rad < 1 || rad > 99)
+                    throw RuntimeException(std::string("Radius for visibility analysis must be n for the whole range or an "
+                                                       "integer between 1 and 99 inclusive. Got ") + radius);
+                r = (double)rad;
+            }
+        }
+        std::cout << " ok\nAnalysing graph..." << std::flush;
+        std::vector<float> out((size_t)m.nnodes * 7, -1.0f);
+        if (global) timed(perf, "Run VGA", [&] { check(dmx_vga_global(C.ctx, m.g, r, 0, 0, -1, out.data(), nullptr)); });
+        std::cout << " ok\nWriting out result..." << std::flush;
+        timed(perf, "Writing graph", [&] {
+            // VGAVisualGlobal::run column insertion order and setValue pattern (vgavisualglobal.cpp:38-193)
+            const std::string suffix = r != -1.0 ? " R" + std::to_string((int)r) : std::string();
+            struct Spec { const char* name; int outcol; bool simple; };
+            const Spec specs[7] = {{"Visual Entropy", 0, false}, {"Visual Integration [HH]", 1, true},
+                                   {"Visual Integration [P-value]", 2, false}, {"Visual Integration [Tekl]", 3, false},
+                                   {"Visual Mean Depth", 4, false}, {"Visual Node Count", 5, false},
+                                   {"Visual Relativised Entropy", 6, false}};
+            int displayed = -1;
+            if (global)
+                for (auto& sp : specs) {
+                    if (a.simple && !sp.simple) continue;
+                    Column c;
+                    c.name = std::string(sp.name) + suffix;
+                    c.values.resize((size_t)m.nnodes);
+                    c.set.resize((size_t)m.nnodes);
+                    for (int64_t k = 0; k < m.nnodes; k++) {
+                        const float tn = out[k * 7 + 5];
+                        const bool ran = tn >= 1.0f;   // skipped sources set nothing
+                        c.values[k] = out[k * 7 + sp.outcol];
+                        bool set = ran;
+                        if (sp.outcol >= 1 && sp.outcol <= 3) set = ran && tn > 1.0f;   // HH / P / Tekl need > 1 node
+                        c.set[k] = set ? 1 : 0;
+                        if (!set) c.values[k] = -1.0f;
+                    }
+                    if (sp.outcol == 1) displayed = (int)m.columns.size();
+                    m.columns.push_back(c);
+                }
+            d.chunk = write_chunk(m.pm, m.nnodes, m.bins.data(), m.runs.data(), m.nruns, m.gridconn.data(), m.columns,
+                                  displayed);
+            write_document(a.out, d);
+        });
+        std::cout << " ok" << std::endl;
+    }
+};
+
+// StepDepthParser (stepdepthparser.cpp:26-100) + runStepDepth (runmethods.cpp:735-778)
+struct StepDepth : Mode {
+    enum { NONE, ANGULAR, METRIC, VISUAL } type = NONE;
+    std::vector<std::pair<double, double>> points;
+    std::string name() const override { return "STEPDEPTH"; }
+    void parse(int argc, char** argv) override {
+        std::vector<std::string> pts;
+        std::string pointFile;
+        for (int i = 1; i < argc; ++i) {
+            if (!std::strcmp("-sdp", argv[i])) {
+                if (!pointFile.empty()) throw CommandLineException("-sdp cannot be used together with -sdf");
+                enforce_argument("-sdp", i, argc, argv);
+                if (!has_only_digits_dots_commas(argv[i])) {
+                    std::stringstream m;
+                    m << "Invalid step depth point provided (" << argv[i] << "). Should only contain digits dots and commas";
+                    throw CommandLineException(m.str());
+                }
+                pts.push_back(argv[i]);
+            } else if (!std::strcmp("-sdf", argv[i])) {
+                if (!pts.empty()) throw CommandLineException("-sdf cannot be used together with -sdp");
+                enforce_argument("-sdf", i, argc, argv);
+                pointFile = argv[i];
+            } else if (!std::strcmp("-sdt", argv[i])) {
+                enforce_argument("-sdt", i, argc, argv);
+                if (!std::strcmp(argv[i], "angular")) type = ANGULAR;
+                else if (!std::strcmp(argv[i], "metric")) type = METRIC;
+                else if (!std::strcmp(argv[i], "visual")) type = VISUAL;
+                else throw CommandLineException(std::string("Invalid step type: ") + argv[i]);
+            }
+        }
+        if (pointFile.empty() && pts.empty()) throw CommandLineException("Either -sdp or -sdf must be given");
+        points = points_from_args(pts, pointFile);
+        if (type == NONE) throw CommandLineException("Step depth type (-sdt) must be provided");
+    }
+    void run(const Args& a, Perf& perf) override {
+        Document d;
+        timed(perf, "Load graph file", [&] { d = read_document(a.file); });
+        Context C;
+        LoadedMap m;
+        load_map(C, d, m);
+        std::cout << "ok\nSelecting cells... " << std::flush;
+        int32_t cols = 0, rows = 0;
+        double spacing = 0, bl[2] = {0, 0};
+        check(dmx_chunk_info(m.chunk, &cols, &rows, &spacing, bl, nullptr, nullptr, nullptr, nullptr, nullptr));
+        std::vector<int32_t> sel;
+        for (auto& p : points) {
+            if (!(p.first >= d.region[0] && p.first <= d.region[2] && p.second >= d.region[1] && p.second <= d.region[3]))
+                throw RuntimeException("Point outside of target region");
+            // PointMap::pixelate(p, constrain=true) (pointdata.cpp:263-283)
+            int x = (int)std::floor((p.first - bl[0] + spacing / 2.0) / spacing);
+            int y = (int)std::floor((p.second - bl[1] + spacing / 2.0) / spacing);
+            x = std::min(std::max(x, 0), cols - 1);
+            y = std::min(std::max(y, 0), rows - 1);
+            sel.push_back(x * rows + y);
+        }
+        std::cout << "ok\nCalculating step-depth... " << std::flush;
+        if (type != METRIC) throw RuntimeException("Only -sdt metric is part of the accelerated path");
+        std::vector<float> out((size_t)m.nnodes * 3, -1.0f);
+        int rc = DMX_OK;
+        timed(perf, "Calculating step-depth",
+              [&] { rc = dmx_metric_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data()); });
+        if (rc != DMX_OK && rc != DMX_ERR_STATE) check(rc);   // no selection: analyseGraph returns false
+        std::cout << " ok\nWriting out result..." << std::flush;
+        timed(perf, "Writing graph", [&] {
+            int displayed = -1;
+            if (rc == DMX_OK) {
+                // VGAMetricDepth::run column order (vgametricdepth.cpp:27-33); cells it never pops keep -1
+                const bool single = [&] {   // PointMap::setCurSel keeps FILLED cells only
+                    std::vector<int32_t> st((size_t)cols * rows);
+                    check(dmx_chunk_arrays(m.chunk, st.data(), nullptr, nullptr, nullptr));
+                    std::vector<int32_t> s;
+                    for (int32_t c : sel)
+                        if (st[c] & 2) s.push_back(c);
+                    std::sort(s.begin(), s.end());
+                    s.erase(std::unique(s.begin(), s.end()), s.end());
+                    return s.size() == 1;
+                }();
+                const char* names[3] = {"Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length",
+                                        "Metric Straight-Line Distance"};
+                for (int j = 0; j < (single ? 3 : 2); j++) {
+                    Column c;
+                    c.name = names[j];
+                    c.values.resize((size_t)m.nnodes);
+                    c.set.resize((size_t)m.nnodes);
+                    for (int64_t k = 0; k < m.nnodes; k++) {
+                        c.values[k] = out[k * 3 + j];
+                        c.set[k] = out[k * 3 + 1] >= 0.0f ? 1 : 0;
+                    }
+                    if (j == 1) displayed = (int)m.columns.size();
+                    m.columns.push_back(c);
+                }
+            }
+            d.chunk = write_chunk(m.pm, m.nnodes, m.bins.data(), m.runs.data(), m.nruns, m.gridconn.data(), m.columns,
+                                  displayed);
+            write_document(a.out, d);
+        });
+        std::cout << " ok" << std::endl;
+    }
+};
+
+void print_help() {
+    std::cout << "Usage: dmxcli -m <mode> -f <filename> -o <output file> [-t <times.csv>] [-s] [-p] [mode options]\n"
+                 "Modes (the accelerated depthmapXcli path):\n"
+                 "  VISPREP   -pg <grid spacing> -pp <x,y> | -pf <points file> [-pr <max visibility>] [-pb] [-pm]\n"
+                 "  VGA       -vm visibility -vg -vr <radius|n>\n"
+                 "  STEPDEPTH -sdt metric -sdp <x,y> | -sdf <points file>\n"
+                 "Input: a CSV drawing (x1,y1,x2,y2) or a .dmxg written by this tool; output: .dmxg\n";
+}
+
+} // namespace
+
+int main(int argc, char* argv[]) {
+    std::vector<std::unique_ptr<Mode>> modes;
+    modes.emplace_back(new VisPrep());
+    modes.emplace_back(new Vga());
+    modes.emplace_back(new StepDepth());
+    try {
+        // CommandLineParser::parse (commandlineparser.cpp:51-133)
+        if (argc <= 1) throw CommandLineException("No commandline parameters provided - don't know what to do");
+        Mode* mode = nullptr;
+        Args a;
+        for (int i = 1; i < argc;) {
+            if (!std::strcmp("-h", argv[i])) { print_help(); return 0; }
+            if (!std::strcmp("-v", argv[i])) { std::cout << "dmxcli (depthmapX VISPREP/VGA/STEPDEPTH on MI355X)\n"; return 0; }
+            if (!std::strcmp("-m", argv[i])) {
+                if (mode) throw CommandLineException("-m can only be used once");
+                enforce_argument("-m", i, argc, argv);
+                for (auto& m : modes)
+                    if (m->name() == argv[i]) mode = m.get();
+                if (!mode) throw CommandLineException(std::string("Invalid mode: ") + argv[i]);
+            } else if (!std::strcmp("-f", argv[i])) {
+                enforce_argument("-f", i, argc, argv);
+                a.file = argv[i];
+            } else if (!std::strcmp("-o", argv[i])) {
+                enforce_argument("-o", i, argc, argv);
+                a.out = argv[i];
+            } else if (!std::strcmp("-t", argv[i])) {
+                enforce_argument("-t", i, argc, argv);
+                a.timing = argv[i];
+            } else if (!std::strcmp("-s", argv[i])) {
+                a.simple = true;
+            } else if (!std::strcmp("-p", argv[i])) {
+                a.progress = true;
+            }
+            ++i;
+        }
+        if (!mode) throw CommandLineException("-m for mode is required");
+        if (a.file.empty()) throw CommandLineException("-f for input file is required");
+        if (a.out.empty()) throw CommandLineException("-o for output file is required");
+        mode->parse(argc, argv);
+        Perf perf;
+        perf.file = a.timing;
+        mode->run(a, perf);
+        perf.write();
+    } catch (std::exception& e) {
+        std::cout << e.what() << "\n"
+                  << "Type 'depthmapXcli -h' for help" << std::endl;
+        return -1;
+    }
+    return 0;
+}

@@ -1272,13 +1272,15 @@ int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const in
 
 int dmx_chunk_write(const dmx_pointmap* pm, int64_t nnodes, const int32_t* bins, const int16_t* runs, int64_t nruns,
                     const uint8_t* gridconn, int ncols, const char* const* names, const float* values,
-                    const uint8_t* locked, int displayed, int boundary, uint8_t* buf, int64_t cap, int64_t* size) {
+                    const uint8_t* locked, const uint8_t* setmask, int displayed, int boundary, uint8_t* buf, int64_t cap,
+                    int64_t* size) {
     if (!pm || !size || nnodes < 0 || ncols < 0 || (ncols && (!names || !values))) return fail(DMX_ERR_ARG, "bad arguments");
     std::vector<ChunkColumn> cols((size_t)ncols);
     for (int i = 0; i < ncols; i++) {
         cols[i].name = names[i];
         cols[i].locked = locked ? locked[i] != 0 : false;
         cols[i].values.assign(values + (size_t)i * nnodes, values + (size_t)(i + 1) * nnodes);
+        if (setmask) cols[i].set.assign(setmask + (size_t)i * nnodes, setmask + (size_t)(i + 1) * nnodes);
     }
     std::vector<uint8_t> out;
     std::string err;
@@ -1342,6 +1344,14 @@ int dmx_chunk_arrays(const dmx_chunk* c, int32_t* state, int32_t* bins, int16_t*
     if (bins && !p.bins.empty()) std::memcpy(bins, p.bins.data(), p.bins.size() * 4);
     if (runs && !p.runs.empty()) std::memcpy(runs, p.runs.data(), p.runs.size() * 2);
     if (gridconn && !p.gridconn.empty()) std::memcpy(gridconn, p.gridconn.data(), p.gridconn.size());
+    return DMX_OK;
+}
+
+int dmx_pointmap_set_state(dmx_pointmap* pm, const int32_t* state) {
+    if (!pm || !state) return fail(DMX_ERR_ARG, "bad arguments");
+    PointMapHost& h = *pm->host;
+    h.restore_fill(state);
+    pm->version++;
     return DMX_OK;
 }
 

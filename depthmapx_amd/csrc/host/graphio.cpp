@@ -70,10 +70,12 @@ inline uint8_t bin_dir(int b) {
 
 struct Stats { double min = -1.0, max = -1.0, total = -1.0; };
 
-// AttributeRowImpl::setValue + AttributeColumnImpl::updateStats on a fresh column (every value -1).
-Stats replay_stats(const float* v, int64_t n) {
+// AttributeRowImpl::setValue + AttributeColumnImpl::updateStats on a fresh column (every value -1),
+// for the rows the analysis actually set (x-major order).
+Stats replay_stats(const float* v, const uint8_t* set, int64_t n) {
     Stats s;
     for (int64_t i = 0; i < n; i++) {
+        if (set && !set[i]) continue;
         const float val = v[i];
         const float old = 0.0f;   // the previous value is -1, clamped to 0
         if (s.total < 0) s.total = val;
@@ -116,7 +118,7 @@ int write_pointmap_chunk(const PointMapHost& h, int64_t nnodes, const int32_t* b
     w.put<int32_t>((int32_t)cols.size());
     for (int ci : order) {
         const ChunkColumn& c = cols[ci];
-        const Stats s = replay_stats(c.values.data(), nnodes);
+        const Stats s = replay_stats(c.values.data(), c.set.empty() ? nullptr : c.set.data(), nnodes);
         w.str(c.name);
         w.put<float>((float)s.min);
         w.put<float>((float)s.max);

@@ -12,6 +12,7 @@ struct ChunkColumn {
     std::string name;
     bool locked = false;
     std::vector<float> values;      // node (x-major) order
+    std::vector<uint8_t> set;       // rows the analysis called setValue on (empty: all rows)
     float min = -1.0f, max = -1.0f; // as read
     double total = -1.0;
 };

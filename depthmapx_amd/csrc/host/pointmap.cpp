@@ -42,6 +42,15 @@ void PointMapHost::load_state(int cols, int rows, double spacing, Vec2 bl, const
     for (int32_t s : state_) filled_ += (s & CELL_FILLED) ? 1 : 0;
 }
 
+void PointMapHost::restore_fill(const int32_t* state) {
+    const int32_t keep = CELL_FILLED | CELL_EDGE | CELL_CONTEXTFILLED | CELL_EMPTY;
+    filled_ = 0;
+    for (int64_t c = 0; c < cells(); c++) {
+        state_[c] = (state_[c] & ~keep) | (state[c] & keep);
+        filled_ += (state_[c] & CELL_FILLED) ? 1 : 0;
+    }
+}
+
 Rect PointMapHost::cell_rect(int x, int y, double border) const {
     return Rect{bl_.x + spacing_ * (double(x) - 0.5 - border), bl_.y + spacing_ * (double(y) - 0.5 - border),
                 bl_.x + spacing_ * (double(x) + 0.5 + border), bl_.y + spacing_ * (double(y) + 0.5 + border)};

@@ -43,6 +43,8 @@ class PointMapHost {
     // (PointMap::read, pointdata.cpp:1073-1156).  No occluder pieces: such a map can run VGA and
     // step depth on its graph but not makeGraph.
     void load_state(int cols, int rows, double spacing, Vec2 bl, const int32_t* state);
+    // Fill states of a saved map of this same grid (FILLED / EDGE / CONTEXTFILLED bits).
+    void restore_fill(const int32_t* state);
     // PointMap::sparkGraph2's boundary-graph pre-pass (pointdata.cpp:1254-1264).
     void keep_edges_only();
     void block_lines(); // idempotent (m_blockedlines)

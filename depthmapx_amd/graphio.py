@@ -13,8 +13,8 @@ from . import _native as N
 
 
 def write_chunk(pm, bins, runs, gridconn, columns, displayed=0, boundary=False):
-    """columns: list of (name, values[N] float32, locked) in insertion order (MAKEGRAPH_COLUMNS
-    order after VISPREP, then the VGA columns); displayed indexes that list."""
+    """columns: list of (name, values[N] float32, locked[, setmask[N]]) in insertion order
+    (MAKEGRAPH_COLUMNS after VISPREP, then the VGA columns); displayed indexes that list."""
     bins = np.ascontiguousarray(bins, dtype=np.int32)
     runs = np.ascontiguousarray(runs, dtype=np.int16).reshape(-1, 4)
     gridconn = np.ascontiguousarray(gridconn, dtype=np.uint8)
@@ -23,9 +23,13 @@ def write_chunk(pm, bins, runs, gridconn, columns, displayed=0, boundary=False):
     vals = np.ascontiguousarray(np.stack([np.asarray(c[1], dtype=np.float32) for c in columns]) if columns
                                 else np.zeros((0, n), np.float32))
     locked = np.ascontiguousarray([1 if (len(c) > 2 and c[2]) else 0 for c in columns] or [0], dtype=np.uint8)
+    masks = None
+    if any(len(c) > 3 and c[3] is not None for c in columns):
+        masks = np.ascontiguousarray(np.stack([np.asarray(c[3], dtype=np.uint8) if (len(c) > 3 and c[3] is not None)
+                                               else np.ones(n, np.uint8) for c in columns]))
     size = ctypes.c_int64()
     args = [pm.h, n, N.ptr(bins), N.ptr(runs), len(runs), N.ptr(gridconn), len(columns), names, N.ptr(vals),
-            N.ptr(locked), int(displayed), int(bool(boundary))]
+            N.ptr(locked), N.ptr(masks), int(displayed), int(bool(boundary))]
     N.check(N.lib().dmx_chunk_write(*args, None, 0, ctypes.byref(size)))
     buf = np.zeros(size.value, dtype=np.uint8)
     N.check(N.lib().dmx_chunk_write(*args, N.ptr(buf), size.value, ctypes.byref(size)))

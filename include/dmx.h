@@ -69,6 +69,9 @@ int dmx_pointmap_free(dmx_pointmap* pm);
  * salalib/pointdata.cpp:402-481).  DMX_ERR_OUTSIDE if the point is outside the region;
  * *made = 0 where makePoints returns false. */
 int dmx_pointmap_fill(dmx_pointmap* pm, double x, double y, int* made);
+/* Restore the FILLED / EDGE / CONTEXTFILLED cell states of a map saved earlier (e.g. the state
+ * array of a PointMap chunk of the same grid), as PointMap::read does before makeGraph. */
+int dmx_pointmap_set_state(dmx_pointmap* pm, const int32_t* state);
 /* cols, rows, bottom-left cell centre, filled count. */
 int dmx_pointmap_info(const dmx_pointmap* pm, int32_t* cols, int32_t* rows, double* bl_x, double* bl_y,
                       int64_t* filled);
@@ -136,7 +139,10 @@ int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_pop
  * displayed indexes the columns.  buf NULL (or cap too small): only *size is set. */
 int dmx_chunk_write(const dmx_pointmap* pm, int64_t nnodes, const int32_t* bins, const int16_t* runs, int64_t nruns,
                     const uint8_t* gridconn, int ncols, const char* const* names, const float* values,
-                    const uint8_t* locked, int displayed, int boundary, uint8_t* buf, int64_t cap, int64_t* size);
+                    const uint8_t* locked, const uint8_t* setmask, int displayed, int boundary, uint8_t* buf, int64_t cap,
+                    int64_t* size);
+/* setmask (optional, [ncols][nnodes]): rows the analysis called setValue on (column statistics
+ * skip the others, like the reference's AttributeColumnImpl::updateStats). */
 /* PointMap::read (pointdata.cpp:1073-1156, ngraph.cpp:420-445,491-563): decode a chunk; runs come
  * back with the reference's lossy 4-bit row shift applied. */
 typedef struct dmx_chunk dmx_chunk;

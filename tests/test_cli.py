@@ -1,0 +1,122 @@
+"""dmxcli: the depthmapXcli mode-parser surface for VISPREP / VGA / STEPDEPTH
+(depthmapXcli/commandlineparser.cpp:51-142, visprepparser.cpp:26-172, vgaparser.cpp:29-106,
+stepdepthparser.cpp:26-100, main.cpp:47-52).  CPU tests cover flag validation (no GPU needed: a
+failing parse never reaches the device); the GPU test runs the whole CLI pipeline."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CLI = os.path.join(REPO, "depthmapx_amd", "_lib", "dmxcli")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def run(*args):
+    p = subprocess.run([CLI] + list(args), capture_output=True, text=True)
+    return p.returncode, p.stdout
+
+
+@pytest.fixture(scope="module", autouse=True)
+def built():
+    if not os.path.exists(CLI):
+        from depthmapx_amd import build
+        build.build()
+
+
+@pytest.mark.parametrize("args,message", [
+    ([], "No commandline parameters provided - don't know what to do"),
+    (["-m", "NOPE", "-f", "a", "-o", "b"], "Invalid mode: NOPE"),
+    (["-m", "VISPREP", "-m", "VGA"], "-m can only be used once"),
+    (["-f", "a", "-o", "b"], "-m for mode is required"),
+    (["-m", "VGA", "-o", "b"], "-f for input file is required"),
+    (["-m", "VGA", "-f", "a"], "-o for output file is required"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b"], "Nothing to do"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b", "-pg", "1", "-pg", "2"], "-pg can only be used once"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b", "-pg", "0"], "-pg must be a number >0, got 0"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b", "-pg", "1", "-pm"],
+     "Creating a graph for an unfilled grid is not possible. Either -pp or -pf must be given"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b", "-pp", "1a,2"],
+     "Invalid fill point provided (1a,2). Should only contain digits dots and commas"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b", "-pm", "-pu"], "-pu cannot be used together with -pm"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b", "-pr", "0", "-pm"],
+     "Restricted visibility of '0' makes no sense, use a positive number or -1 for unrestricted"),
+    (["-m", "VISPREP", "-f", "a", "-o", "b", "-pg"], "-pg requires an argument"),
+    (["-m", "VGA", "-f", "a", "-o", "b", "-vm", "visibility", "-vg"],
+     "Global measures in VGA/visibility analysis require a radius, use -vr <radius>"),
+    (["-m", "VGA", "-f", "a", "-o", "b", "-vm", "visibility", "-vg", "-vr", "x"],
+     "Radius must be a positive integer number or n, got x"),
+    (["-m", "VGA", "-f", "a", "-o", "b", "-vm", "nope"], "Invalid VGA mode: nope"),
+    (["-m", "VGA", "-f", "a", "-o", "b", "-vm", "metric"], "Metric vga requires a radius, use -vr <radius>"),
+    (["-m", "STEPDEPTH", "-f", "a", "-o", "b", "-sdt", "metric"], "Either -sdp or -sdf must be given"),
+    (["-m", "STEPDEPTH", "-f", "a", "-o", "b", "-sdp", "1,1"], "Step depth type (-sdt) must be provided"),
+    (["-m", "STEPDEPTH", "-f", "a", "-o", "b", "-sdp", "1,1", "-sdt", "odd"], "Invalid step type: odd"),
+])
+def test_parser_messages_like_depthmapxcli(args, message):
+    rc, out = run(*args)
+    assert rc == 255, out   # main returns -1
+    assert out.splitlines() == [message, "Type 'depthmapXcli -h' for help"]
+
+
+def test_help_and_missing_file(tmp_path):
+    rc, out = run("-h")
+    assert rc == 0 and "VISPREP" in out
+    rc, out = run("-m", "VISPREP", "-f", str(tmp_path / "none.csv"), "-o", str(tmp_path / "o.dmxg"), "-pg", "1",
+                  "-pp", "0.5,0.5", "-pm")
+    assert rc == 255 and "Failed to load graph from file" in out
+
+
+@pytest.mark.gpu
+def test_cli_pipeline_matches_reference(tmp_path):
+    """VISPREP -pg 1 -pp 0.5,0.5 -pm -> VGA -vm visibility -vg -vr n -> STEPDEPTH -sdt metric on the
+    synthetic 32^2 drawing: the VISPREP PointMap chunk is byte-identical to the reference's, the
+    VGA columns equal the reference CLI's (VGA on the re-read graph), step depth matches the C
+    restatement on the same re-read graph, and the -t CSV carries the reference's action names."""
+    import hashlib
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from depthmapx_amd import graphio
+    from golden_io import load_case
+    from pyoracle import OracleMap
+    meta, A = load_case("syn32")
+    src = os.path.join(GOLDEN, "inputs", "syn32.csv")
+    g1, g2, g3 = (str(tmp_path / n) for n in ("a.dmxg", "b.dmxg", "c.dmxg"))
+    t1 = str(tmp_path / "t1.csv")
+    rc, out = run("-m", "VISPREP", "-f", src, "-o", g1, "-pg", "1", "-pp", "0.5,0.5", "-pm", "-t", t1)
+    assert rc == 0, out
+    assert [l.split(",")[0] for l in open(t1).read().splitlines()] == [
+        '"action"', '"Load graph file"', '"Setting grid"', '"Filling grid"', '"Making graph"', '"Writing graph"']
+
+    def chunk(path):
+        b = open(path, "rb").read()
+        nl = int(np.frombuffer(b[40:48], np.int64)[0])
+        o = 48 + nl * 32 + 1
+        n = int(np.frombuffer(b[o:o + 8], np.int64)[0])
+        return b[o + 8:o + 8 + n]
+    c1 = chunk(g1)
+    assert hashlib.sha256(c1).digest() == A["pm_chunk_sha256"].tobytes()
+    rc, out = run("-m", "VGA", "-f", g1, "-o", g2, "-vm", "visibility", "-vg", "-vr", "n")
+    assert rc == 0, out
+    doc = graphio.read_chunk(chunk(g2))
+    names = [c[0] for c in doc["columns"]]
+    assert names[:3] == ["Connectivity", "Point First Moment", "Point Second Moment"]
+    from depthmapx_amd import VGA_COLUMNS
+    assert names[3:] == VGA_COLUMNS
+    got = np.stack([c[1] for c in doc["columns"][3:]], axis=1)
+    want = A["vga_rt"]
+    assert (np.abs(got.astype(np.float64) - want) <= 1e-6 * np.maximum(1.0, np.abs(want))).all()
+    rc, out = run("-m", "STEPDEPTH", "-f", g2, "-o", g3, "-sdt", "metric", "-sdp", "16.5,16.5")
+    assert rc == 0, out
+    d3 = graphio.read_chunk(chunk(g3))
+    cols = {c[0]: c[1] for c in d3["columns"]}
+    om = OracleMap(meta["region"], meta["spacing"], np.load(os.path.join(GOLDEN, meta["lines_npy"])))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph()
+    om.set_graph(doc["bins"], doc["runs"])
+    rows = meta["rows"]
+    ref = om.metric_stepdepth(np.array([16 * rows + 16], np.int32))
+    np.testing.assert_array_equal(cols["Metric Step Shortest-Path Length"], ref[:, 1])
+    np.testing.assert_array_equal(cols["Metric Straight-Line Distance"], ref[:, 2])
+    assert np.allclose(cols["Metric Step Shortest-Path Angle"], ref[:, 0], rtol=1e-6, atol=1e-6)

@@ -251,3 +251,41 @@ def test_metric_stepdepth_errors(ctx):
     g = pm.make_graph(ctx)
     with pytest.raises(dmx.DmxError):
         g.metric_step_depth(points=[(-5.0, 1.0)])   # outside the region
+
+
+CHUNK_CASES = ["kat", "syn16", "syn32", "gallery", "syn64"]
+
+
+@pytest.mark.parametrize("name", CHUNK_CASES)
+def test_gpu_graph_chunk_bytes_match_reference(ctx, name):
+    """VISPREP's output: the PointMap chunk written from the GPU graph is byte-identical to the one
+    the reference writes (PointMap::write)."""
+    import hashlib
+    from depthmapx_amd import graphio
+    meta, A = load_case(name)
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    c = g.copy(runs=True)
+    cols = [(n, c["attrs"][:, j], j == 0) for j, n in enumerate(dmx.MAKEGRAPH_COLUMNS)]
+    blob = graphio.write_chunk(pm, c["bins"], c["runs"], c["gridconn"], cols, displayed=0)
+    assert len(blob) == int(A["pm_chunk_size"][0])
+    assert hashlib.sha256(blob).digest() == A["pm_chunk_sha256"].tobytes()
+
+
+@pytest.mark.parametrize("name", [n for n in CHUNK_CASES if n != "syn64"])
+def test_vga_after_graph_roundtrip_matches_reference_cli(ctx, name):
+    """The reference CLI runs VGA on the graph re-read from the .graph file (4-bit shift quirk):
+    VISPREP chunk -> decode -> GPU VGA == the reference's VGA after its own round trip."""
+    from depthmapx_amd import graphio
+    meta, A = load_case(name)
+    if "vga_rt" not in A:
+        pytest.skip("no round-trip fixture")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    c = g.copy(runs=True)
+    cols = [(n, c["attrs"][:, j], j == 0) for j, n in enumerate(dmx.MAKEGRAPH_COLUMNS)]
+    blob = graphio.write_chunk(pm, c["bins"], c["runs"], c["gridconn"], cols, displayed=0)
+    pm2, g2 = graphio.load_chunk(ctx, blob, meta["region"])
+    out = g2.vga_visual_global(radius=-1)
+    _assert_vga_close(out, A["vga_rt"])
+    np.testing.assert_array_equal(out[:, 5], A["vga_rt"][:, 5])
