@@ -363,55 +363,107 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     // capacities (retried on overflow)
     int gcap = 128, bcap = 128;
     int64_t capB = 32 * (int64_t)D + 2048;
+    if (const char* e = getenv("DMX_MK_GCAP")) gcap = std::max(2, atoi(e));   // test hooks for the retry path
+    if (const char* e = getenv("DMX_MK_BCAP")) bcap = std::max(2, atoi(e));
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     int64_t pool_cap = std::max<int64_t>(n * std::max<int64_t>(64, 6 * (int64_t)D), 1024);
     ctx->last_mk_s = 0;
-    for (int attempt = 0; attempt < 8; attempt++) {
-        size_t lds = makegraph_lds(gcap, bcap, D);
-        if (lds > 160 * 1024) return fail(DMX_ERR_CAPACITY, "makegraph LDS requirement exceeds 160 KiB");
-        int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, makegraph_kernel, 64, lds));
-        if (occ < 1) occ = 1;
-        const int64_t waves = std::min<int64_t>((int64_t)ctx->num_cu * occ, std::max<int64_t>(n, 1));
-        const int64_t capA = capB;
-        const size_t stage_bytes = (size_t)waves * (capA * 8 + capB * 8 + (3 * ((size_t)D + 1) + 4) * 4);
-        HIPCHK(hipMemGetInfo(&free_b, &total_b));
-        const size_t pool_bytes_max = free_b > stage_bytes + (1ull << 30) ? (free_b - stage_bytes - (1ull << 30)) : 0;
-        if ((size_t)pool_cap * sizeof(Run) > pool_bytes_max) pool_cap = (int64_t)(pool_bytes_max / sizeof(Run));
-        if (pool_cap <= 0) return fail(DMX_ERR_HIP, "not enough device memory for the run pool");
-        double ta = now_s();
-        HIPCHK(g->pool.alloc(pool_cap));
-        VLOG("makegraph: pool alloc %.3f GB %.3f s\n", pool_cap * 8.0 / 1e9, now_s() - ta);
-        ta = now_s();
-        DevBuf<unsigned long long> stA;
-        DevBuf<Run> stB;
-        DevBuf<uint32_t> pref;
-        HIPCHK(stA.alloc((size_t)waves * capA));
-        HIPCHK(stB.alloc((size_t)waves * capB));
-        HIPCHK(pref.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
+    DevBuf<int64_t> fail_list, node_list;
+    HIPCHK(fail_list.alloc(std::max<int64_t>(n, 1)));
+    HIPCHK(node_list.alloc(std::max<int64_t>(n, 1)));
+    for (int restart = 0; restart < 3; restart++) {
+        // one full pass, then re-runs of only the sources that overflowed an LDS / staging capacity
+        double kernel_s = 0.0;
+        int64_t list_n = -1;   // -1: the whole range
+        bool pool_over = false;
         HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
         HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), ctx->stream));
-        MakeGraphParams P;
-        P.cols = h.cols(); P.rows = h.rows();
-        P.spacing = h.spacing(); P.blx = h.bottom_left().x; P.bly = h.bottom_left().y;
-        P.maxdist = maxdist;
-        P.cellw = pm->d_cellw.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
-        P.node_begin = node_begin; P.node_end = node_end;
-        P.work_counter = ctx->counters.p + 0;
-        P.error = ctx->counters.p + 1;
-        P.pool_cursor = (unsigned long long*)(ctx->counters.p + 2);
-        P.pool_capacity = pool_cap; P.pool = g->pool.p;
-        P.node_run_start = g->node_run_start.p; P.bin_nruns = g->bin_nruns.p; P.bin_count = g->bin_count.p;
-        P.bin_dist = g->bin_dist.p; P.attrs = g->attrs.p;
-        P.stageA = stA.p; P.stageB = stB.p; P.prefix = pref.p;
-        P.capA = (int)capA; P.capB = (int)capB; P.gcap = gcap; P.bcap = bcap; P.dmax = D;
-        P.stats = ctx->stats.p;
-        VLOG("makegraph: stage alloc %.3f s\n", now_s() - ta);
+        size_t lds0 = makegraph_lds(gcap, bcap, D);
+        int occ0 = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, makegraph_kernel, 64, lds0));
+        {
+            const int64_t waves0 = std::min<int64_t>((int64_t)ctx->num_cu * std::max(occ0, 1), std::max<int64_t>(n, 1));
+            const size_t stage0 = (size_t)waves0 * (capB * 16 + (3 * ((size_t)D + 1) + 4) * 4) * 4;   // headroom for retries
+            HIPCHK(hipMemGetInfo(&free_b, &total_b));
+            const size_t pool_bytes_max = free_b > stage0 + (1ull << 30) ? (free_b - stage0 - (1ull << 30)) : 0;
+            if ((size_t)pool_cap * sizeof(Run) > pool_bytes_max) pool_cap = (int64_t)(pool_bytes_max / sizeof(Run));
+            if (pool_cap <= 0) return fail(DMX_ERR_HIP, "not enough device memory for the run pool");
+            double ta = now_s();
+            HIPCHK(g->pool.alloc(pool_cap));
+            VLOG("makegraph: pool alloc %.3f GB %.3f s\n", pool_cap * 8.0 / 1e9, now_s() - ta);
+        }
+        for (int attempt = 0; attempt < 8; attempt++) {
+            size_t lds = makegraph_lds(gcap, bcap, D);
+            if (lds > 160 * 1024) return fail(DMX_ERR_CAPACITY, "makegraph LDS requirement exceeds 160 KiB");
+            int occ = 0;
+            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, makegraph_kernel, 64, lds));
+            if (occ < 1) occ = 1;
+            const int64_t todo = list_n < 0 ? n : list_n;
+            const int64_t waves = std::min<int64_t>((int64_t)ctx->num_cu * occ, std::max<int64_t>(todo, 1));
+            const int64_t capA = capB;
+            DevBuf<unsigned long long> stA;
+            DevBuf<Run> stB;
+            DevBuf<uint32_t> pref;
+            HIPCHK(stA.alloc((size_t)waves * capA));
+            HIPCHK(stB.alloc((size_t)waves * capB));
+            HIPCHK(pref.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
+            // work counter, error word and failure count restart; the pool cursor carries on
+            HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 2 * sizeof(int), ctx->stream));
+            HIPCHK(hipMemsetAsync(ctx->counters.p + 4, 0, sizeof(int), ctx->stream));
+            MakeGraphParams P;
+            P.cols = h.cols(); P.rows = h.rows();
+            P.spacing = h.spacing(); P.blx = h.bottom_left().x; P.bly = h.bottom_left().y;
+            P.maxdist = maxdist;
+            P.cellw = pm->d_cellw.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
+            P.node_begin = node_begin; P.node_end = node_end;
+            P.work_counter = ctx->counters.p + 0;
+            P.error = ctx->counters.p + 1;
+            P.pool_cursor = (unsigned long long*)(ctx->counters.p + 2);
+            P.pool_capacity = pool_cap; P.pool = g->pool.p;
+            P.node_run_start = g->node_run_start.p; P.bin_nruns = g->bin_nruns.p; P.bin_count = g->bin_count.p;
+            P.bin_dist = g->bin_dist.p; P.attrs = g->attrs.p;
+            P.stageA = stA.p; P.stageB = stB.p; P.prefix = pref.p;
+            P.capA = (int)capA; P.capB = (int)capB; P.gcap = gcap; P.bcap = bcap; P.dmax = D;
+            P.stats = ctx->stats.p;
+            P.node_list = list_n < 0 ? nullptr : node_list.p;
+            P.list_n = list_n < 0 ? 0 : list_n;
+            P.fail_list = fail_list.p;
+            P.fail_count = ctx->counters.p + 4;
+            HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+            if (todo > 0) {
+                hipLaunchKernelGGL(makegraph_kernel, dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
+                HIPCHK(hipGetLastError());
+            }
+            HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            float ms = 0;
+            HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+            kernel_s += ms * 1e-3;
+            int hc[5] = {0, 0, 0, 0, 0};
+            HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+            const int err = hc[1], nfail = hc[4];
+            VLOG("makegraph: attempt %d (%lld sources, gcap %d bcap %d capB %lld): %.3f s, %d failed, err %d\n", attempt,
+                 (long long)todo, gcap, bcap, (long long)capB, ms * 1e-3, nfail, err);
+            if (err & KERR_BIN_MISMATCH) return fail(DMX_ERR_STATE, "internal: whichbin outside octant");
+            if (err & KERR_POOL_CAPACITY) {
+                unsigned long long used = 0;
+                std::memcpy(&used, &hc[2], 8);
+                pool_cap = std::max<int64_t>(pool_cap * 2, (int64_t)used + 1024);
+                pool_over = true;
+                break;
+            }
+            if (nfail == 0) break;
+            if (err & KERR_GAP_CAPACITY) gcap *= 2;
+            if (err & KERR_BLOCK_CAPACITY) bcap *= 2;
+            if (err & KERR_STAGE_CAPACITY) capB *= 2;
+            HIPCHK(hipMemcpyAsync(node_list.p, fail_list.p, (size_t)nfail * 8, hipMemcpyDeviceToDevice, ctx->stream));
+            list_n = nfail;
+            if (attempt == 7) return fail(DMX_ERR_CAPACITY, "makegraph capacities exceeded after retries");
+        }
+        if (pool_over) continue;
         HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
         if (n > 0) {
-            hipLaunchKernelGGL(makegraph_kernel, dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
-            HIPCHK(hipGetLastError());
             hipLaunchKernelGGL(gridconn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, h.rows(),
                                pm->d_node_cell.p + node_begin, n, g->node_run_start.p, g->bin_nruns.p, g->pool.p,
                                g->gridconn.p);
@@ -424,28 +476,21 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         HIPCHK(hipStreamSynchronize(ctx->stream));
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        kernel_s += ms * 1e-3;
         int hc[4] = {0, 0, 0, 0};
         HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
-        const int err = hc[1];
         unsigned long long used = 0;
         std::memcpy(&used, &hc[2], 8);
-        if (err == 0) {
-            unsigned long long st[2];
-            HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
-            ctx->last_stats[0] = (long long)st[0];
-            ctx->last_stats[1] = (long long)st[1];
-            ctx->last_stats[2] = (long long)used;
-            ctx->last_mk_s = ms * 1e-3;
-            g->nruns = (int64_t)used;
-            VLOG("makegraph: kernels %.3f s, total %.3f s\n", ms * 1e-3, now_s() - t_start);
-            *out = g.release();
-            return DMX_OK;
-        }
-        if (err & KERR_BIN_MISMATCH) return fail(DMX_ERR_STATE, "internal: whichbin outside octant");
-        if (err & KERR_GAP_CAPACITY) gcap *= 2;
-        if (err & KERR_BLOCK_CAPACITY) bcap *= 2;
-        if (err & KERR_STAGE_CAPACITY) capB *= 2;
-        if (err & KERR_POOL_CAPACITY) pool_cap = (int64_t)used + 1024;
+        unsigned long long st[2];
+        HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+        ctx->last_stats[0] = (long long)st[0];
+        ctx->last_stats[1] = (long long)st[1];
+        ctx->last_stats[2] = (long long)used;
+        ctx->last_mk_s = kernel_s;
+        g->nruns = (int64_t)used;
+        VLOG("makegraph: kernels %.3f s, total %.3f s\n", kernel_s, now_s() - t_start);
+        *out = g.release();
+        return DMX_OK;
     }
     return fail(DMX_ERR_CAPACITY, "makegraph capacities exceeded after retries");
 }

@@ -46,6 +46,12 @@ struct MakeGraphParams {
     int dmax;                  // max(cols, rows)
     int* error;
     unsigned long long* stats; // [0] sieve cells examined, [1] visible (source, target) pairs
+    // retry mode: process node_list[0, list_n) instead of [node_begin, node_end); sources that
+    // exceed a capacity are appended to fail_list and re-run by the host with larger capacities
+    const int64_t* node_list;
+    int64_t list_n;
+    int64_t* fail_list;
+    int* fail_count;
 };
 
 // ------------------------------------------------------------------ octant tables
@@ -216,8 +222,14 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
         int s_idx = 0;
         if (lane == 0) s_idx = atomicAdd(P.work_counter, 1);
         s_idx = __shfl(s_idx, 0);
-        const int64_t node = P.node_begin + s_idx;
-        if (node >= P.node_end) break;
+        int64_t node;
+        if (P.node_list) {
+            if (s_idx >= P.list_n) break;
+            node = P.node_list[s_idx];
+        } else {
+            node = P.node_begin + s_idx;
+            if (node >= P.node_end) break;
+        }
         const int cell = P.node_cell[node];
         const int cx = cell / P.rows, cy = cell % P.rows;
         const double c0x = P.blx + sp * 1.0 * (double)cx, c0y = P.bly + sp * 1.0 * (double)cy;
@@ -611,6 +623,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
             __syncthreads();
         }
         if (failed) {
+            if (lane == 0) P.fail_list[atomicAdd(P.fail_count, 1)] = node;
             // leave the wave in a clean LDS state and drop this source
             for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
             for (int i = lane; i <= AX; i += 64) L.cnt[i] = 0;

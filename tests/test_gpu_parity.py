@@ -289,3 +289,14 @@ def test_vga_after_graph_roundtrip_matches_reference_cli(ctx, name):
     out = g2.vga_visual_global(radius=-1)
     _assert_vga_close(out, A["vga_rt"])
     np.testing.assert_array_equal(out[:, 5], A["vga_rt"][:, 5])
+
+
+def test_makegraph_capacity_retries_are_exact(ctx, monkeypatch):
+    """Sources that overflow the LDS gap/block capacities are re-run with doubled capacities; with
+    tiny initial capacities almost every source takes that path and the graph is still exact."""
+    meta, A = load_case("gallery")
+    monkeypatch.setenv("DMX_MK_GCAP", "2")
+    monkeypatch.setenv("DMX_MK_BCAP", "2")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    _assert_graph_equal(g.copy(runs=True), A, True)
