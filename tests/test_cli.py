@@ -116,7 +116,8 @@ def test_cli_pipeline_matches_reference(tmp_path):
     om.make_graph()
     om.set_graph(doc["bins"], doc["runs"])
     rows = meta["rows"]
-    ref = om.metric_stepdepth(np.array([16 * rows + 16], np.int32))
+    # PointMap::pixelate(16.5, 16.5) at spacing 1 from bottom-left (0, 0): floor(16.5 + 0.5) = 17
+    ref = om.metric_stepdepth(np.array([17 * rows + 17], np.int32))
     np.testing.assert_array_equal(cols["Metric Step Shortest-Path Length"], ref[:, 1])
     np.testing.assert_array_equal(cols["Metric Straight-Line Distance"], ref[:, 2])
     assert np.allclose(cols["Metric Step Shortest-Path Angle"], ref[:, 0], rtol=1e-6, atol=1e-6)
