@@ -430,6 +430,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.list_n = list_n < 0 ? 0 : list_n;
             P.fail_list = fail_list.p;
             P.fail_count = ctx->counters.p + 4;
+            P.profile = verbose() ? 1 : 0;
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
                 hipLaunchKernelGGL(makegraph_kernel, dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
@@ -481,8 +482,15 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
         unsigned long long used = 0;
         std::memcpy(&used, &hc[2], 8);
-        unsigned long long st[2];
+        unsigned long long st[16];
         HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+        if (verbose()) {
+            double tot = 0;
+            for (int i = 8; i < 14; i++) tot += (double)st[i];
+            VLOG("makegraph phases (wave clocks): garbage %.1f%%, ranges %.1f%%, candidates %.1f%%, visible %.1f%%, "
+                 "placement %.1f%%, publish %.1f%% (%.3g total)\n", 100 * st[8] / tot, 100 * st[9] / tot, 100 * st[10] / tot,
+                 100 * st[11] / tot, 100 * st[12] / tot, 100 * st[13] / tot, tot);
+        }
         ctx->last_stats[0] = (long long)st[0];
         ctx->last_stats[1] = (long long)st[1];
         ctx->last_stats[2] = (long long)used;

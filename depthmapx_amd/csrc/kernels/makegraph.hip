@@ -52,7 +52,16 @@ struct MakeGraphParams {
     int64_t list_n;
     int64_t* fail_list;
     int* fail_count;
+    int profile;               // 1: accumulate per-phase clocks into stats[8..13]
 };
+
+// phase clocks (profile builds of a run only; wave-uniform scalar reads)
+#define MK_T(i)                                                           \
+    if (P.profile) {                                                      \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();       \
+        cyc[i] += n_ - tmark;                                             \
+        tmark = n_;                                                       \
+    }
 
 // ------------------------------------------------------------------ octant tables
 // q octants (sparksieve2.cpp:134-141):   \ 6 | 7 /   0 \ | / 1   2 / | \ 3   / 4 | 5 \ .
@@ -217,6 +226,10 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
     for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
     for (int i = lane; i <= AX; i += 64) L.cnt[i] = 0;
     __syncthreads();
+    // 0 depth-0 + collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible cells,
+    // 4 octant flush + canonical placement, 5 publish
+    unsigned long long cyc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long tmark = P.profile ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
         int s_idx = 0;
@@ -361,6 +374,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                     if (lane == 0) L.misc[1] = 0;
                     __syncthreads();
                 }
+                MK_T(0);
                 // loop condition: sieve.hasGaps() (pointdata.cpp:1454)
                 if (ng == 0) break;
                 depth++;
@@ -394,6 +408,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                 __syncthreads();
                 const int T = carryT;
                 examined += (unsigned long long)T;
+                MK_T(1);
                 bool hasgaps = false;
                 int gcur = 0; // per-lane gap pointer (t increases monotonically)
                 for (int t0 = 0; t0 < T; t0 += 64) {
@@ -443,6 +458,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                         }
                     }
                     hasgaps |= (ballot(ingrid) != 0ull);
+                    MK_T(2);
                     // ---- visible cells: bins, moments (reference order), run tracking
                     unsigned long long am = ballot(add);
                     if (am) {
@@ -508,6 +524,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                             nA += __popcll(em);
                         }
                     }
+                    MK_T(3);
                 }
                 if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
                 if (!hasgaps) break;      // sieve2 returned false (pointdata.cpp:1458)
@@ -621,6 +638,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
             if (lane == 0) { L.cnt[AX] = 0; L.misc[16 + q] = bpos; L.misc[24 + q] = seg_len; }
             bpos += seg_len;
             __syncthreads();
+            MK_T(4);
         }
         if (failed) {
             if (lane == 0) P.fail_list[atomicAdd(P.fail_count, 1)] = node;
@@ -658,11 +676,15 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
         if (lane == 0) {
             atomicAdd(&P.stats[0], examined);
             atomicAdd(&P.stats[1], (unsigned long long)nsize);
+            if (P.profile)
+                for (int i = 0; i < 6; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
             P.attrs[k * 3 + 0] = (float)nsize;
             P.attrs[k * 3 + 1] = (float)tsum;
             P.attrs[k * 3 + 2] = (float)tsum2;
         }
         __syncthreads();
+        for (int i = 0; i < 6; i++) cyc[i] = 0;
+        MK_T(5);
     }
 }
 
