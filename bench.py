@@ -195,7 +195,8 @@ def main():
         mk_bytes = 8 * stats.get("mk_runs", 0) + 4 * stats.get("mk_cells_examined", 0)
         tw, th = (info["cols"] + 7) // 8, (info["rows"] + 7) // 8
         levels = stats.get("vga_bottom_up_levels", 0) + stats.get("vga_top_down_levels", 0)
-        vga_bytes = 8 * stats.get("vga_runs_expanded", 0) + 16 * tw * th * nsrc + 32 * tw * th * levels
+        vga_bytes = (8 * stats.get("vga_runs_expanded", 0) + 16 * tw * th * nsrc + 32 * tw * th * levels +
+                     stats.get("vga_tvis_bytes", 0))
         dominant = "vga_tile_kernel" if vga_s >= mk_s else "makegraph_kernel"
         dom_bytes, dom_s = (vga_bytes, vga_s) if vga_s >= mk_s else (mk_bytes, mk_s)
         achieved = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
@@ -224,6 +225,7 @@ def main():
                         "vga_kernel": stats.get("vga_kernel"),
                         "vga_runs_tested": stats.get("vga_runs_expanded"),
                         "vga_tiles_resolved_by_common_runs": stats.get("vga_cr_tiles"),
+                        "vga_hard_cells_rejected_by_tile_visibility": stats.get("vga_pruned_cells"),
                         "vga_levels_bottom_up": stats.get("vga_bottom_up_levels"),
                         "vga_levels_top_down": stats.get("vga_top_down_levels"),
                         "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc,

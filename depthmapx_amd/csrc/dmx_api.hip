@@ -81,7 +81,7 @@ struct dmx_ctx {
     long long phase_cycles[5] = {0, 0, 0, 0, 0};   // tile BFS: level 1, A, B, C, bookkeeping (sum over workgroups)
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
-    long long last_stats[16] = {};
+    long long last_stats[24] = {};
 };
 
 struct dmx_pointmap {
@@ -131,6 +131,8 @@ struct dmx_graph {
     DevBuf<int64_t> tscan_start;
     DevBuf<int32_t> tnruns;
     DevBuf<Run> heads, cr;
+    DevBuf<unsigned long long> tvis;   // tile-visibility rows (empty: not built / too large)
+    int tvw = 0;
     DevBuf<unsigned long long> regular_tiles;
 };
 
@@ -263,7 +265,7 @@ int dmx_ctx_free(dmx_ctx* c) {
 
 int dmx_ctx_last_stats(dmx_ctx* c, int64_t* out, int n) {
     if (!c || !out) return fail(DMX_ERR_ARG, "bad arguments");
-    for (int i = 0; i < n && i < 16; i++) out[i] = c->last_stats[i];
+    for (int i = 0; i < n && i < 24; i++) out[i] = c->last_stats[i];
     return DMX_OK;
 }
 
@@ -362,9 +364,11 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
 
     // capacities (retried on overflow)
     int gcap = 128, bcap = 128;
+    int spill_cap = 4096;      // per-wave HBM blocks past bcap
     int64_t capB = 32 * (int64_t)D + 2048;
     if (const char* e = getenv("DMX_MK_GCAP")) gcap = std::max(2, atoi(e));   // test hooks for the retry path
     if (const char* e = getenv("DMX_MK_BCAP")) bcap = std::max(2, atoi(e));
+    if (const char* e = getenv("DMX_MK_SPILL")) spill_cap = std::max(1, atoi(e));
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     int64_t pool_cap = std::max<int64_t>(n * std::max<int64_t>(64, 6 * (int64_t)D), 1024);
@@ -408,6 +412,10 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             HIPCHK(stA.alloc((size_t)waves * capA));
             HIPCHK(stB.alloc((size_t)waves * capB));
             HIPCHK(pref.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
+            DevBuf<double2> bsp;
+            DevBuf<int> bspf;
+            HIPCHK(bsp.alloc((size_t)waves * 2 * spill_cap));
+            HIPCHK(bspf.alloc((size_t)waves * spill_cap));
             // work counter, error word and failure count restart; the pool cursor carries on
             HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 2 * sizeof(int), ctx->stream));
             HIPCHK(hipMemsetAsync(ctx->counters.p + 4, 0, sizeof(int), ctx->stream));
@@ -425,6 +433,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.bin_dist = g->bin_dist.p; P.attrs = g->attrs.p;
             P.stageA = stA.p; P.stageB = stB.p; P.prefix = pref.p;
             P.capA = (int)capA; P.capB = (int)capB; P.gcap = gcap; P.bcap = bcap; P.dmax = D;
+            P.bspill = bsp.p; P.bspill_flag = bspf.p; P.spill_cap = spill_cap;
             P.stats = ctx->stats.p;
             P.node_list = list_n < 0 ? nullptr : node_list.p;
             P.list_n = list_n < 0 ? 0 : list_n;
@@ -444,8 +453,8 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             int hc[5] = {0, 0, 0, 0, 0};
             HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
             const int err = hc[1], nfail = hc[4];
-            VLOG("makegraph: attempt %d (%lld sources, gcap %d bcap %d capB %lld): %.3f s, %d failed, err %d\n", attempt,
-                 (long long)todo, gcap, bcap, (long long)capB, ms * 1e-3, nfail, err);
+            VLOG("makegraph: attempt %d (%lld sources, gcap %d bcap %d spill %d capB %lld, occupancy %d): %.3f s, %d failed, "
+                 "err %d\n", attempt, (long long)todo, gcap, bcap, spill_cap, (long long)capB, occ, ms * 1e-3, nfail, err);
             if (err & KERR_BIN_MISMATCH) return fail(DMX_ERR_STATE, "internal: whichbin outside octant");
             if (err & KERR_POOL_CAPACITY) {
                 unsigned long long used = 0;
@@ -456,7 +465,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             }
             if (nfail == 0) break;
             if (err & KERR_GAP_CAPACITY) gcap *= 2;
-            if (err & KERR_BLOCK_CAPACITY) bcap *= 2;
+            if (err & KERR_BLOCK_CAPACITY) spill_cap *= 4;
             if (err & KERR_STAGE_CAPACITY) capB *= 2;
             HIPCHK(hipMemcpyAsync(node_list.p, fail_list.p, (size_t)nfail * 8, hipMemcpyDeviceToDevice, ctx->stream));
             list_n = nfail;
@@ -486,10 +495,11 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
         if (verbose()) {
             double tot = 0;
-            for (int i = 8; i < 14; i++) tot += (double)st[i];
-            VLOG("makegraph phases (wave clocks): garbage %.1f%%, ranges %.1f%%, candidates %.1f%%, visible %.1f%%, "
-                 "placement %.1f%%, publish %.1f%% (%.3g total)\n", 100 * st[8] / tot, 100 * st[9] / tot, 100 * st[10] / tot,
-                 100 * st[11] / tot, 100 * st[12] / tot, 100 * st[13] / tot, tot);
+            for (int i = 8; i < 16; i++) tot += (double)st[i];
+            VLOG("makegraph phases (wave clocks): garbage %.1f%%, ranges %.1f%%, candidates %.1f%%, bins %.1f%%, "
+                 "moments %.1f%%, run tracking %.1f%%, placement %.1f%%, publish %.1f%% (%.3g total)\n", 100 * st[8] / tot,
+                 100 * st[9] / tot, 100 * st[10] / tot, 100 * st[11] / tot, 100 * st[12] / tot, 100 * st[13] / tot,
+                 100 * st[14] / tot, 100 * st[15] / tot, tot);
         }
         ctx->last_stats[0] = (long long)st[0];
         ctx->last_stats[1] = (long long)st[1];
@@ -902,6 +912,23 @@ static int prepare_tiles(dmx_graph* g) {
                        lds, s, cols, rows, tw, th, g->regular_tiles.p, g->pm->d_cell_node.p, g->node_run_start.p,
                        g->node_nruns.p, g->scan_start.p, g->scan_pool.p, g->pool.p, dmax, g->cr.p);
     HIPCHK(hipGetLastError());
+    // tile-visibility rows (phase C rejects cells with no frontier tile in view); ~2 KB per cell at
+    // 1000^2, skipped when they would not fit comfortably
+    const int tvw = th * ((tw + 63) / 64);
+    const size_t tv_bytes = (size_t)Ct * tvw * 8;
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const char* tv_env = getenv("DMX_VGA_TVIS");
+    const bool tv_on = !(tv_env && atoi(tv_env) == 0);
+    if (tv_on && N && tv_bytes <= free_b / 4 && tv_bytes <= (32ull << 30)) {
+        HIPCHK(g->tvis.alloc(Ct * tvw));
+        HIPCHK(hipMemsetAsync(g->tvis.p, 0, tv_bytes, s));
+        const int64_t nb = std::min<int64_t>((N + TV_WAVES - 1) / TV_WAVES, (int64_t)ctx->num_cu * 16);
+        hipLaunchKernelGGL(tile_vis_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), (size_t)TV_WAVES * tvw * 8, s, rows, tw,
+                           th, g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, g->tvis.p);
+        HIPCHK(hipGetLastError());
+        g->tvw = tvw;
+    }
     HIPCHK(hipStreamSynchronize(s));
     g->tiles_ready = true;
     return DMX_OK;
@@ -960,6 +987,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.seed_tiles = g->notuf_tiles.p; Q.regular_tiles = g->regular_tiles.p; Q.nonexp_tiles = g->pm->d_nonexp_tiles.p;
     Q.cr = g->cr.p; Q.heads = g->heads.p; Q.tscan_start = g->tscan_start.p; Q.tnruns = g->tnruns.p;
     Q.scan_pool = g->scan_pool.p;
+    Q.tvis = g->tvw ? g->tvis.p : nullptr; Q.tvw = g->tvw;
     Q.node_cell = g->pm->d_node_cell.p; Q.cell_node = g->pm->d_cell_node.p; Q.node_flags = g->pm->d_node_flags.p;
     Q.node_run_start = g->node_run_start.p; Q.node_nruns = g->node_nruns.p; Q.pool = g->pool.p;
     const bool corr = g->nspecial > 0;
@@ -1025,6 +1053,11 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[10] = 0;
     ctx->last_stats[11] = (long long)st[7];
     ctx->last_stats[12] = blocks | ((long long)kt << 32) | ((long long)ntpb << 40);
+    ctx->last_stats[13] = (long long)st[13];
+    ctx->last_stats[14] = (long long)st[14] * g->tvw * 8;   // bytes of tile-visibility rows read
+    ctx->last_stats[15] = (long long)st[15];                          // runs scanned in phase C
+    ctx->last_stats[16] = (long long)st[1];                           // phase-C cells that hit
+    ctx->last_stats[17] = (long long)st[14];                          // phase-C cells (regular)
     if (!out_on_device && nsrc > 0)
         HIPCHK(hipMemcpy(out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
     if (levels && nsrc > 0)
@@ -1135,6 +1168,7 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     ctx->last_stats[8] = (long long)st[5];   // bottom-up cells that scanned all their runs without a hit
     ctx->last_stats[9] = (long long)st[6];   // runs read by those
     ctx->last_stats[10] = gbm ? 1 : 0;
+    for (int i = 13; i < 24; i++) ctx->last_stats[i] = 0;
     ctx->last_stats[3] = (long long)(use_do ? (g->symmetric ? 2 : 1) : 0) | ((long long)g->nspecial << 8);
     ctx->last_stats[4] = (long long)st[0];
     ctx->last_stats[5] = (long long)(st[3] | (st[4] << 32));                 // bottom-up | top-down levels

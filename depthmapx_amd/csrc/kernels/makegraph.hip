@@ -43,6 +43,9 @@ struct MakeGraphParams {
     uint32_t* prefix;          // per wave: 3*(D+1)+2 counts/prefix
     int capA, capB;
     int gcap, bcap;            // LDS gap / block capacities
+    double2* bspill;           // per wave: [2][spill_cap] blocks past bcap (raw, sorted)
+    int* bspill_flag;          // per wave: [spill_cap]
+    int spill_cap;
     int dmax;                  // max(cols, rows)
     int* error;
     unsigned long long* stats; // [0] sieve cells examined, [1] visible (source, target) pairs
@@ -218,6 +221,23 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
     const int wave_global = blockIdx.x;
     unsigned long long* stA = P.stageA + (size_t)wave_global * P.capA;
     Run* stB = P.stageB + (size_t)wave_global * P.capB;
+    double2* spill = P.bspill + (size_t)wave_global * 2 * P.spill_cap;   // [raw | sorted]
+    int* spill_flag = P.bspill_flag + (size_t)wave_global * P.spill_cap;
+    auto put_block = [&](int i, double2 v) {
+        if (i < bcap) L.blocks[i] = v;
+        else if (i - bcap < P.spill_cap) spill[i - bcap] = v;
+    };
+    auto get_block = [&](int i) -> double2 { return i < bcap ? L.blocks[i] : spill[i - bcap]; };
+    auto set_flag = [&](int i, int f) {
+        if (i < bcap) L.bflag[i] = f;
+        else spill_flag[i - bcap] = f;
+    };
+    auto get_flag = [&](int i) -> int { return i < bcap ? L.bflag[i] : spill_flag[i - bcap]; };
+    auto put_sorted = [&](int i, double2 v) {
+        if (i < bcap) L.bsorted[i] = v;
+        else spill[P.spill_cap + i - bcap] = v;
+    };
+    auto get_sorted = [&](int i) -> double2 { return i < bcap ? L.bsorted[i] : spill[P.spill_cap + i - bcap]; };
     uint32_t* pref = P.prefix + (size_t)wave_global * (3 * (D + 1) + 4);
     const double sp = P.spacing;
 
@@ -226,9 +246,9 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
     for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
     for (int i = lane; i <= AX; i += 64) L.cnt[i] = 0;
     __syncthreads();
-    // 0 depth-0 + collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible cells,
-    // 4 octant flush + canonical placement, 5 publish
-    unsigned long long cyc[6] = {0, 0, 0, 0, 0, 0};
+    // 0 depth-0 + collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible: bins,
+    // 4 visible: serial moments, 5 visible: run tracking, 6 octant flush + placement, 7 publish
+    unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tmark = P.profile ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
@@ -282,9 +302,8 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                 if (clip_seg(l, vp)) {
                     Vec2 a = l.start(), b = l.end();
                     double ta = tanify(c0x, c0y, a.x, a.y, q), tb = tanify(c0x, c0y, b.x, b.y, q);
-                    int slot = atomicAdd(&L.misc[1], 1);
-                    if (slot < bcap)
-                        L.blocks[slot] = (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10);
+                    const int slot = atomicAdd(&L.misc[1], 1);
+                    put_block(slot, (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10));
                 }
             }
             __syncthreads();
@@ -298,35 +317,35 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
             for (;;) {
                 // ---------------- collectgarbage (sparksieve2.cpp:89-132) for the previous depth
                 int nb = L.misc[1];
-                if (nb > bcap) { failed = true; if (lane == 0) atomicOr(P.error, KERR_BLOCK_CAPACITY); }
+                if (nb > bcap + P.spill_cap) { failed = true; if (lane == 0) atomicOr(P.error, KERR_BLOCK_CAPACITY); }
                 if (failed) break;
                 if (nb > 0) {
                     // std::sort (start asc, end desc) + std::unique: first-occurrence flags, then
-                    // each distinct block lands at its rank among the distinct blocks
+                    // each distinct block lands at its rank among the distinct blocks.  Blocks past
+                    // the LDS capacity live in this wave's HBM spill area (rare: long walls across
+                    // the sweep front); the same code reads both through get_block / set_flag.
                     for (int i = lane; i < nb; i += 64) {
-                        double2 me = L.blocks[i];
+                        const double2 me = get_block(i);
                         int first = 1;
                         for (int j = 0; j < i; j++) {
-                            double2 o = L.blocks[j];
+                            const double2 o = get_block(j);
                             if (o.x == me.x && o.y == me.y) { first = 0; break; }
                         }
-                        L.bflag[i] = first;
+                        set_flag(i, first);
                     }
                     __syncthreads();
                     int nu = 0;
                     for (int i = lane; i < nb; i += 64) {
-                        if (!L.bflag[i]) continue;
-                        double2 me = L.blocks[i];
+                        if (!get_flag(i)) continue;
+                        const double2 me = get_block(i);
                         int rank = 0;
                         for (int j = 0; j < nb; j++) {
-                            double2 o = L.blocks[j];
-                            if (L.bflag[j] && zone_less(o.x, o.y, me.x, me.y)) rank++;
+                            const double2 o = get_block(j);
+                            if (get_flag(j) && zone_less(o.x, o.y, me.x, me.y)) rank++;
                         }
-                        L.bsorted[rank] = me;
+                        put_sorted(rank, me);
                     }
-                    for (int base = 0; base < nb; base += 64) nu += __popcll(ballot(base + lane < nb && L.bflag[base + lane]));
-                    __syncthreads();
-                    for (int i = lane; i < nu; i += 64) L.blocks[i] = L.bsorted[i];
+                    for (int base = 0; base < nb; base += 64) nu += __popcll(ballot(base + lane < nb && get_flag(base + lane)));
                     __syncthreads();
                     // sequential merge on lane 0: gaps -> gaps2
                     if (lane == 0) {
@@ -334,7 +353,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                         bool over = false;
                         double2 cur = (ng > 0) ? L.gaps[0] : make_double2(0, 0);
                         while (bi < nu && gi < ng) {
-                            double2 bk = L.blocks[bi];
+                            const double2 bk = get_sorted(bi);
                             if (bk.y < cur.x) { bi++; continue; }
                             bool create = true;
                             if (bk.x <= cur.x) { create = false; if (bk.y > cur.x) cur.x = bk.y; }
@@ -452,9 +471,8 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                         for (int k = 0; k < nl; k++) {
                             const double* sg = P.segs + 4 * (size_t)(off + k);
                             double ta = tanify(c0x, c0y, sg[0], sg[1], q), tb = tanify(c0x, c0y, sg[2], sg[3], q);
-                            int slot = atomicAdd(&L.misc[1], 1);
-                            if (slot < bcap)
-                                L.blocks[slot] = (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10);
+                            const int slot = atomicAdd(&L.misc[1], 1);
+                            put_block(slot, (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10));
                         }
                     }
                     hasgaps |= (ballot(ingrid) != 0ull);
@@ -472,15 +490,21 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                             atomicAdd(&L.binc[bin], 1u);
                             atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
                         }
+                        MK_T(3);
                         // serial sums in lane order = reference addlist order
+                        // (the lane index is wave-uniform: v_readlane into SGPRs keeps the serial
+                        // chain on two dependent FP64 adds per cell instead of an LDS round trip)
+                        const int d_lo = __double2loint(this_dist), d_hi = __double2hiint(this_dist);
                         unsigned long long mm = am;
                         while (mm) {
-                            int l = __ffsll((long long)mm) - 1;
-                            double v = __shfl(this_dist, l);
+                            const int l = __ffsll((long long)mm) - 1;
+                            const double v = __hiloint2double(__builtin_amdgcn_readlane(d_hi, l),
+                                                              __builtin_amdgcn_readlane(d_lo, l));
                             tsum += v;
                             tsum2 += v * v;
                             mm &= mm - 1;
                         }
+                        MK_T(4);
                         nsize += __popcll(am);
                         // run tracking
                         bool emit = false;
@@ -524,7 +548,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                             nA += __popcll(em);
                         }
                     }
-                    MK_T(3);
+                    MK_T(5);
                 }
                 if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
                 if (!hasgaps) break;      // sieve2 returned false (pointdata.cpp:1458)
@@ -638,7 +662,7 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
             if (lane == 0) { L.cnt[AX] = 0; L.misc[16 + q] = bpos; L.misc[24 + q] = seg_len; }
             bpos += seg_len;
             __syncthreads();
-            MK_T(4);
+            MK_T(6);
         }
         if (failed) {
             if (lane == 0) P.fail_list[atomicAdd(P.fail_count, 1)] = node;
@@ -677,14 +701,14 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
             atomicAdd(&P.stats[0], examined);
             atomicAdd(&P.stats[1], (unsigned long long)nsize);
             if (P.profile)
-                for (int i = 0; i < 6; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
+                for (int i = 0; i < 8; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
             P.attrs[k * 3 + 0] = (float)nsize;
             P.attrs[k * 3 + 1] = (float)tsum;
             P.attrs[k * 3 + 2] = (float)tsum2;
         }
         __syncthreads();
-        for (int i = 0; i < 6; i++) cyc[i] = 0;
-        MK_T(5);
+        for (int i = 0; i < 8; i++) cyc[i] = 0;
+        MK_T(7);
     }
 }
 

@@ -38,6 +38,8 @@ struct VgaTileParams {
     const int64_t* tscan_start;               // [nt*64] start in scan_pool (tile order)
     const int32_t* tnruns;                    // [nt*64]
     const Run* scan_pool;
+    const unsigned long long* tvis;           // [nt*64][tvw] tiles seen by each cell, Fsr layout (null: off)
+    int tvw;                                  // th * ceil(tw / 64)
     const int32_t* node_cell;
     const int32_t* cell_node;
     const uint8_t* node_flags;
@@ -65,7 +67,9 @@ struct VgaTileParams {
     int32_t* nlev_out;        // [N] levels (0: source skipped)
     int* error;
     unsigned long long* stats;  // [0] runs tested, [2] cells reached, [3] BU levels, [4] TD levels,
-                                // [5] hard cells without a hit, [6] their runs, [7] tiles resolved by CR
+                                // [5] hard cells without a hit, [6] their runs, [7] tiles resolved by CR,
+                                // [8..12] phase clocks, [13] hard cells rejected by their tile-visibility row,
+                                // [14] tile-visibility rows read, [1] phase-C hits, [15] phase-C runs
 };
 
 __device__ __forceinline__ int tile_id_of(int x, int y, int tw) {
@@ -231,7 +235,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
     int4* Q = P.queue + (size_t)blockIdx.x * nt;
     int32_t* L = P.list + (size_t)blockIdx.x * nt * 64;
     const size_t hstride = (size_t)nt * 64;
-    unsigned long long runs_tested = 0, fail_cells = 0, fail_runs = 0, cr_tiles = 0;
+    unsigned long long runs_tested = 0, fail_cells = 0, fail_runs = 0, cr_tiles = 0, pruned = 0, tv_tests = 0, hard_runs = 0, hard_hits = 0;
     unsigned long long cyc[5] = {0, 0, 0, 0, 0};   // leader-thread phase clocks
     unsigned long long tmark = 0;
 
@@ -399,6 +403,21 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                         const int64_t rs = P.tscan_start[id];
                         nr = P.tnruns[id];
                         int base = KH + BEXT;   // the first KH + BEXT runs were tested in phase B
+                        bool pruned_now = false;
+                        if (P.tvis) {
+                            // no tile the cell sees holds a frontier cell: no run can hit (one
+                            // coalesced 2 KB row instead of the whole run list; most cells that
+                            // would scan everything without a hit stop here)
+                            const unsigned long long* tv = P.tvis + (size_t)id * P.tvw;
+                            bool any = false;
+                            for (int w = lane; w < P.tvw; w += 64) any |= (tv[w] & Fsr[w]) != 0ull;
+                            if (lane == 0) tv_tests++;
+                            if (__ballot(any) == 0ull) {
+                                base = nr;
+                                pruned_now = true;
+                                if (lane == 0) pruned++;
+                            }
+                        }
                         // 4 runs per lane per step (256 per wave): four independent loads in flight
                         for (; base < nr && !found; base += 256) {
                             Run rr[4];
@@ -417,7 +436,12 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                             found = fmin != (1 << 30);
                             if (found && lane == 0) Hn[id] = (uint16_t)min(fmin, 0xFFFE);
                         }
-                        if (lane == 0) runs_tested += (unsigned long long)(min(base, nr) - KH - BEXT);
+                        if (lane == 0 && !(P.tvis && base == nr && !found && nr > KH + BEXT && pruned_now)) {
+                            const unsigned long long sc = (unsigned long long)max(min(base, nr) - KH - BEXT, 0);
+                            runs_tested += sc;
+                            hard_runs += sc;
+                            hard_hits += found ? 1ull : 0ull;
+                        }
                     }
                     if (lane == 0) {
                         if (found) or_wg(&Xg[id >> 6], 1ull << (id & 63));
@@ -518,11 +542,19 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
         fail_cells += __shfl_xor(fail_cells, off);
         fail_runs += __shfl_xor(fail_runs, off);
         cr_tiles += __shfl_xor(cr_tiles, off);
+        pruned += __shfl_xor(pruned, off);
+        tv_tests += __shfl_xor(tv_tests, off);
+        hard_runs += __shfl_xor(hard_runs, off);
+        hard_hits += __shfl_xor(hard_hits, off);
     }
     if (lane == 0) {
         if (runs_tested) atomicAdd(&P.stats[0], runs_tested);
         if (fail_cells) { atomicAdd(&P.stats[5], fail_cells); atomicAdd(&P.stats[6], fail_runs); }
         if (cr_tiles) atomicAdd(&P.stats[7], cr_tiles);
+        if (pruned) atomicAdd(&P.stats[13], pruned);
+        if (tv_tests) atomicAdd(&P.stats[14], tv_tests);
+        if (hard_hits) atomicAdd(&P.stats[1], hard_hits);
+        if (hard_runs) atomicAdd(&P.stats[15], hard_runs);
     }
     if (tid == 0)
         for (int i = 0; i < 5; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
@@ -547,6 +579,51 @@ __global__ void tile_heads_kernel(int rows, int tw, const int32_t* node_cell, in
     tscan_start[id] = ss;
     tnruns[id] = nr;
     for (int h = 0; h < KH && h < nr; h++) heads[h * hstride + id] = scan_pool[ss + h];
+}
+
+// Tile-visibility rows: bit (ty, tx) of cell id's row is set iff the cell sees some cell of tile
+// (tx, ty); same [th][ceil(tw/64)] word layout as the kernel's Fsr summary, so one AND per word
+// tells whether any frontier tile is in view.  One wave per node, the row built in LDS.
+constexpr int TV_WAVES = 4;
+__global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int tw, int th, const int32_t* node_cell,
+                                                                 int64_t n, const int64_t* node_run_start,
+                                                                 const int32_t* node_nruns, const Run* pool,
+                                                                 unsigned long long* tvis) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long tvrow[];
+    const int wr = (tw + 63) / 64, tvw = th * wr;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long* row = tvrow + (size_t)wave * tvw;
+    for (int64_t k = (int64_t)blockIdx.x * TV_WAVES + wave; k < n; k += (int64_t)gridDim.x * TV_WAVES) {
+        for (int w = lane; w < tvw; w += 64) row[w] = 0ull;
+        __builtin_amdgcn_wave_barrier();
+        const int64_t rs = node_run_start[k];
+        const int nr = node_nruns[k];
+        for (int r = lane; r < nr; r += 64) {
+            const Run ru = pool[rs + r];
+            if (ru.y0 == ru.y1) {
+                const int ty = ru.y0 >> 3, t0 = ru.x0 >> 3, t1 = ru.x1 >> 3;
+                for (int w = t0 >> 6; w <= (t1 >> 6); w++) {
+                    const int lo = max(t0 - w * 64, 0), hi = min(t1 - w * 64, 63);
+                    atomicOr(&row[ty * wr + w], (~0ull << lo) & (~0ull >> (63 - hi)));
+                }
+            } else if (ru.x0 == ru.x1) {
+                const int tx = ru.x0 >> 3;
+                for (int ty = ru.y0 >> 3; ty <= (ru.y1 >> 3); ty++) atomicOr(&row[ty * wr + (tx >> 6)], 1ull << (tx & 63));
+            } else {
+                const int dy = (ru.y1 > ru.y0) ? 1 : -1;
+                int y = ru.y0;
+                for (int x = ru.x0; x <= ru.x1; x++, y += dy)
+                    atomicOr(&row[(y >> 3) * wr + (x >> 6 >> 3)], 1ull << ((x >> 3) & 63));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        const int c = node_cell[k];
+        const int id = tile_id_of(c / rows, c % rows, tw);
+        unsigned long long* out = tvis + (size_t)id * tvw;
+        for (int w = lane; w < tvw; w += 64) out[w] = row[w];
+        __builtin_amdgcn_wave_barrier();
+    }
 }
 
 // Lattice segment: cells (x0 + p*dx, y0 + p*dy), p = 0..len-1 (dx in {0,1}, dy in {-1,0,1}).

@@ -54,11 +54,12 @@ class Context:
         return dict(zip(["level1", "tile_common", "heads", "hard", "bookkeeping"], (int(v) for v in out)))
 
     def last_stats(self):
-        out = np.zeros(16, dtype=np.int64)
-        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 16))
+        out = np.zeros(24, dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 24))
         keys = ["mk_cells_examined", "mk_visible_pairs", "mk_runs", "vga_kernel", "vga_runs_expanded", "vga_levels",
                 "vga_cells_reached", "vga_sources", "vga_fail_cells", "vga_fail_runs", "vga_hbm_bitmaps",
-                "vga_cr_tiles", "vga_launch"]
+                "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",
+                "vga_hard_cells"]
         d = {k: int(v) for k, v in zip(keys, out)}
         lv = d.pop("vga_levels")
         d["vga_bottom_up_levels"], d["vga_top_down_levels"] = lv & 0xFFFFFFFF, lv >> 32

@@ -45,12 +45,15 @@ int dmx_ctx_free(dmx_ctx* ctx);
 /* Wall time of the kernels of the last makegraph / vga call, measured with HIP events on the
  * context stream (seconds); kernel_ms receives per-kernel averages. */
 int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
-/* Work counters of the last calls (for roofline accounting): [0] sieve cells examined,
- * [1] visible (source,target) pairs, [2] runs written, [3] VGA kernel used (0 top-down v1,
- * 1 direction-optimising restricted to top-down, 2 direction-optimising) | nodes needing exact
- * in-set corrections << 8, [4] runs read by the
- * BFS, [5] bottom-up levels | top-down levels << 32, [6] cells reached (sum over sources),
- * [7] sources run. */
+/* Work counters of the last calls (for roofline accounting), up to 24 entries:
+ * [0] sieve cells examined, [1] visible (source,target) pairs, [2] runs written,
+ * [3] VGA kernel used (0 top-down v1, 1 direction-optimising restricted to top-down,
+ *     2 direction-optimising, 3 tile-resolved) | nodes needing exact in-set corrections << 8,
+ * [4] runs read by the BFS, [5] bottom-up levels | top-down levels << 32, [6] cells reached (sum
+ * over sources), [7] sources run, [8] bottom-up cells that found no hit, [9] their runs,
+ * [10] bitmaps in HBM (direction-optimising), [11] tiles resolved by common runs, [12] launch
+ * shape, [13] hard cells rejected by their tile-visibility row, [14] bytes of those rows read,
+ * [15] runs scanned by hard cells, [16] hard cells that hit, [17] hard cells. */
 int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
 
 /* Diagnostics of the last tile-resolved VGA launch: core-clock cycles spent (workgroup leader,

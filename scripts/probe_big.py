@@ -40,6 +40,9 @@ for k, v in configs:
                       "runs_read_per_src": st["vga_runs_expanded"] / nsrc,
                       "fail_cells_per_src": st["vga_fail_cells"] / nsrc,
                       "fail_runs_per_src": st["vga_fail_runs"] / nsrc, "cr_tiles_per_src": st["vga_cr_tiles"] / nsrc,
+                      "pruned_cells_per_src": st["vga_pruned_cells"] / nsrc,
+                      "hard_cells_per_src": st["vga_hard_cells"] / nsrc, "hard_hits_per_src": st["vga_hard_hits"] / nsrc,
+                      "hard_runs_per_src": st["vga_hard_runs"] / nsrc,
                       "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc, "kernel": st["vga_kernel"],
                       "launch_blocks": st["vga_launch"] & 0xFFFFFFFF,
                       "phase_cycles_per_src": {kk: vv / nsrc for kk, vv in ctx.last_phase_cycles().items()}}),

@@ -291,12 +291,16 @@ def test_vga_after_graph_roundtrip_matches_reference_cli(ctx, name):
     np.testing.assert_array_equal(out[:, 5], A["vga_rt"][:, 5])
 
 
-def test_makegraph_capacity_retries_are_exact(ctx, monkeypatch):
-    """Sources that overflow the LDS gap/block capacities are re-run with doubled capacities; with
-    tiny initial capacities almost every source takes that path and the graph is still exact."""
+@pytest.mark.parametrize("gcap,bcap,spill", [("2", "2", None), ("128", "2", "2")])
+def test_makegraph_capacity_retries_are_exact(ctx, monkeypatch, gcap, bcap, spill):
+    """Blocks past the LDS capacity go to the wave's HBM spill area; sources that overflow the gap
+    capacity or the spill area are re-run with larger capacities.  With tiny initial capacities
+    almost every source takes those paths and the graph is still exact."""
     meta, A = load_case("gallery")
-    monkeypatch.setenv("DMX_MK_GCAP", "2")
-    monkeypatch.setenv("DMX_MK_BCAP", "2")
+    monkeypatch.setenv("DMX_MK_GCAP", gcap)
+    monkeypatch.setenv("DMX_MK_BCAP", bcap)
+    if spill:
+        monkeypatch.setenv("DMX_MK_SPILL", spill)
     pm = _map(meta)
     g = pm.make_graph(ctx)
     _assert_graph_equal(g.copy(runs=True), A, True)
