@@ -81,7 +81,7 @@ struct dmx_ctx {
     long long phase_cycles[5] = {0, 0, 0, 0, 0};   // tile BFS: level 1, A, B, C, bookkeeping (sum over workgroups)
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
-    long long last_stats[24] = {};
+    long long last_stats[32] = {};
 };
 
 struct dmx_pointmap {
@@ -132,6 +132,8 @@ struct dmx_graph {
     DevBuf<int32_t> tnruns;
     DevBuf<Run> heads, cr;
     DevBuf<unsigned long long> tvis;   // tile-visibility rows (empty: not built / too large)
+    DevBuf<unsigned long long> ftvis;  // full-visibility rows (every non-seed cell of the tile seen)
+    DevBuf<unsigned long long> ttvis;  // tile-to-tile full visibility (AND of ftvis over regular cells)
     int tvw = 0;
     DevBuf<unsigned long long> regular_tiles;
 };
@@ -246,7 +248,7 @@ int dmx_ctx_create(int device, dmx_ctx** out) {
     HIPCHK(hipEventCreate(&c->ev0));
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(c->counters.alloc(16));
-    HIPCHK(c->stats.alloc(16));
+    HIPCHK(c->stats.alloc(32));
     *out = c;
     return DMX_OK;
 }
@@ -265,7 +267,7 @@ int dmx_ctx_free(dmx_ctx* c) {
 
 int dmx_ctx_last_stats(dmx_ctx* c, int64_t* out, int n) {
     if (!c || !out) return fail(DMX_ERR_ARG, "bad arguments");
-    for (int i = 0; i < n && i < 24; i++) out[i] = c->last_stats[i];
+    for (int i = 0; i < n && i < 32; i++) out[i] = c->last_stats[i];
     return DMX_OK;
 }
 
@@ -382,7 +384,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         int64_t list_n = -1;   // -1: the whole range
         bool pool_over = false;
         HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
-        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), ctx->stream));
+        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), ctx->stream));
         size_t lds0 = makegraph_lds(gcap, bcap, D);
         int occ0 = 0;
         HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, makegraph_kernel, 64, lds0));
@@ -920,13 +922,32 @@ static int prepare_tiles(dmx_graph* g) {
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
     const char* tv_env = getenv("DMX_VGA_TVIS");
     const bool tv_on = !(tv_env && atoi(tv_env) == 0);
-    if (tv_on && N && tv_bytes <= free_b / 4 && tv_bytes <= (32ull << 30)) {
+    const char* ftv_env = getenv("DMX_VGA_FTVIS");
+    const bool ftv_on = !(ftv_env && atoi(ftv_env) == 0);
+    // (the tile kernel reads a row as 4 words a lane: tvw <= 256, true for every grid whose frontier
+    // bitmap fits the LDS)
+    if (tv_on && N && tvw <= 256 && tv_bytes * (ftv_on ? 2 : 1) <= free_b / 4 && tv_bytes <= (32ull << 30)) {
         HIPCHK(g->tvis.alloc(Ct * tvw));
         HIPCHK(hipMemsetAsync(g->tvis.p, 0, tv_bytes, s));
+        if (ftv_on) {
+            HIPCHK(g->ftvis.alloc(Ct * tvw));
+            HIPCHK(hipMemsetAsync(g->ftvis.p, 0, tv_bytes, s));
+        }
+        const int ncw = (nt + 3) / 4;
+        const size_t tv_lds = ((size_t)(ncw + 1) / 2 + (size_t)TV_WAVES * (tvw + (ncw + 1) / 2)) * 8;
+        if (tv_lds > 150 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the tile-visibility pass");
         const int64_t nb = std::min<int64_t>((N + TV_WAVES - 1) / TV_WAVES, (int64_t)ctx->num_cu * 16);
-        hipLaunchKernelGGL(tile_vis_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), (size_t)TV_WAVES * tvw * 8, s, rows, tw,
-                           th, g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, g->tvis.p);
+        hipLaunchKernelGGL(tile_vis_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), tv_lds, s, rows, tw,
+                           th, g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p,
+                           g->notuf_tiles.p, g->tvis.p, ftv_on ? g->ftvis.p : nullptr);
         HIPCHK(hipGetLastError());
+        const char* tt_env = getenv("DMX_VGA_TTVIS");
+        if (ftv_on && !(tt_env && atoi(tt_env) == 0)) {
+            HIPCHK(g->ttvis.alloc((size_t)nt * tvw));
+            hipLaunchKernelGGL(tile_tt_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, nt, tvw, g->regular_tiles.p,
+                               g->ftvis.p, g->ttvis.p);
+            HIPCHK(hipGetLastError());
+        }
         g->tvw = tvw;
     }
     HIPCHK(hipStreamSynchronize(s));
@@ -981,13 +1002,15 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     DevBuf<int64_t> d_lv;
     if (levels) HIPCHK(d_lv.alloc(std::max<int64_t>(N, 1) * 3));
     HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), ctx->stream));
     VgaTileParams Q;
     Q.cols = h.cols(); Q.rows = h.rows(); Q.tw = tw; Q.th = th;
     Q.seed_tiles = g->notuf_tiles.p; Q.regular_tiles = g->regular_tiles.p; Q.nonexp_tiles = g->pm->d_nonexp_tiles.p;
     Q.cr = g->cr.p; Q.heads = g->heads.p; Q.tscan_start = g->tscan_start.p; Q.tnruns = g->tnruns.p;
     Q.scan_pool = g->scan_pool.p;
     Q.tvis = g->tvw ? g->tvis.p : nullptr; Q.tvw = g->tvw;
+    Q.ftvis = (g->tvw && g->ftvis.p) ? g->ftvis.p : nullptr;
+    Q.ttvis = (g->tvw && g->ttvis.p) ? g->ttvis.p : nullptr;
     Q.node_cell = g->pm->d_node_cell.p; Q.cell_node = g->pm->d_cell_node.p; Q.node_flags = g->pm->d_node_flags.p;
     Q.node_run_start = g->node_run_start.p; Q.node_nruns = g->node_nruns.p; Q.pool = g->pool.p;
     const bool corr = g->nspecial > 0;
@@ -999,8 +1022,10 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.src_begin = sb; Q.src_end = se; Q.radius = (int)radius; Q.gates_only = gates_only;
     Q.uf_count = g->uf_count;
     // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
-    Q.alpha = 15;
+    Q.alpha = 60;   // top-down costs a frontier cell its whole run list (~R/N runs): keep it rare
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
+    Q.bext = BEXT_DEFAULT;
+    if (const char* b = getenv("DMX_VGA_BEXT")) Q.bext = std::max(0, atoi(b));
     Q.work_counter = ctx->counters.p + 0; Q.error = ctx->counters.p + 1;
     DevBuf<int32_t> d_hist, d_nlev;
     HIPCHK(d_hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));
@@ -1040,9 +1065,18 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     int hc[2];
     HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level capacity");
-    unsigned long long st[16];
+    unsigned long long st[32];
     HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
     for (int i = 0; i < 5; i++) ctx->phase_cycles[i] = (long long)st[8 + i];
+    ctx->last_stats[18] = (long long)st[16];                          // phase-C hits by a fully seen tile
+    ctx->last_stats[19] = (long long)st[17];                          // clocks of top-down levels > 1
+    ctx->last_stats[20] = (long long)st[18];                          // phase-B tiles
+    ctx->last_stats[21] = (long long)st[19];                          // phase-B cells
+    ctx->last_stats[22] = (long long)st[20];                          // phase-B tiles resolved by ttvis
+    ctx->last_stats[23] = (long long)st[21];                          // phase-C busy clocks summed over waves
+    ctx->last_stats[24] = (long long)st[22];                          // phase-C run-scan clocks summed over waves
+    ctx->last_stats[25] = (long long)st[23];                          // phase-C special-node clocks
+    ctx->last_stats[26] = (long long)st[24];                          // phase-C special-node tests
     ctx->last_stats[3] = 3 | ((long long)g->nspecial << 8);
     ctx->last_stats[4] = (long long)st[0];
     ctx->last_stats[5] = (long long)(st[3] | (st[4] << 32));
@@ -1117,7 +1151,7 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     DevBuf<int64_t> d_lv;
     if (levels) HIPCHK(d_lv.alloc(std::max<int64_t>(N, 1) * 3));
     HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), ctx->stream));
     VgaParams P;
     P.cols = h.cols(); P.rows = h.rows(); P.tw = tw; P.th = th;
     P.seed_tiles = g->pm->d_seed_tiles.p; P.uf_tiles = g->uf_tiles.p; P.uf_count = g->uf_count;
@@ -1252,7 +1286,7 @@ int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
         HIPCHK(hipMemsetAsync(d_cum.p, 0, C * 4, s));
         HIPCHK(hipMemsetAsync(d_last.p, 0xFF, C * 4, s));
         HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), s));
-        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 16 * sizeof(unsigned long long), s));
+        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), s));
         StepDepthParams P;
         P.cols = cols; P.rows = rows; P.flags = d_flags.p; P.cell_node = g->pm->d_cell_node.p;
         P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;

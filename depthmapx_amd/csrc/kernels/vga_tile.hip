@@ -25,7 +25,7 @@ namespace dmx {
 
 constexpr int KH = 8;        // head runs per cell (first KH entries of its scan order)
 constexpr int CRK = 4;       // tile-common runs per tile
-constexpr int BEXT = 56;     // runs after the heads a cell scans on its own lane before going wave-cooperative
+constexpr int BEXT_DEFAULT = 16;   // runs after the heads a cell scans on its own lane before going wave-cooperative
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
 
 struct VgaTileParams {
@@ -39,6 +39,8 @@ struct VgaTileParams {
     const int32_t* tnruns;                    // [nt*64]
     const Run* scan_pool;
     const unsigned long long* tvis;           // [nt*64][tvw] tiles seen by each cell, Fsr layout (null: off)
+    const unsigned long long* ftvis;          // [nt*64][tvw] tiles whose every non-seed cell the cell sees (null: off)
+    const unsigned long long* ttvis;          // [nt][tvw] AND of ftvis over the tile's regular cells (null: off)
     int tvw;                                  // th * ceil(tw / 64)
     const int32_t* node_cell;
     const int32_t* cell_node;
@@ -63,13 +65,16 @@ struct VgaTileParams {
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
     int32_t* list;            // per workgroup [nt*64]: hard cells / frontier cells
     int maxlev;
+    int bext;                 // phase-B runs after the heads (BEXT_DEFAULT)
     int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
     int32_t* nlev_out;        // [N] levels (0: source skipped)
     int* error;
     unsigned long long* stats;  // [0] runs tested, [2] cells reached, [3] BU levels, [4] TD levels,
                                 // [5] hard cells without a hit, [6] their runs, [7] tiles resolved by CR,
                                 // [8..12] phase clocks, [13] hard cells rejected by their tile-visibility row,
-                                // [14] tile-visibility rows read, [1] phase-C hits, [15] phase-C runs
+                                // [14] tile-visibility rows read, [1] phase-C hits, [15] phase-C runs,
+                                // [16] phase-C hits certified by a fully seen frontier tile, [17] top-down clocks,
+                                // [18] phase-B tiles, [19] phase-B cells, [20] phase-B tiles resolved by ttvis
 };
 
 __device__ __forceinline__ int tile_id_of(int x, int y, int tw) {
@@ -117,47 +122,55 @@ __device__ __forceinline__ void run_or(unsigned long long* bm, int tw, Run ru) {
 
 
 // Run test against the LDS frontier with coarse occupancy summaries: Fsr (bit per tile, tile rows
-// in row-major order) and Fsc (bit per tile, tile columns) let a horizontal / vertical run skip
-// every empty tile it crosses with one or two word reads, so a miss -- the common case when a
-// cell's visible region lies in the source's shadow -- costs O(1) LDS reads instead of O(len/8).
+// in row-major order) and Fsc (bit per tile, tile columns) give the tiles of the run that hold a
+// frontier cell (a miss -- the common case when a cell's visible region lies in the source's
+// shadow -- costs one or two summary reads).  The frontier words of those tiles are then read up to
+// 8 at a time (independent LDS reads, OR-accumulated), so a long run through a dense frontier costs
+// O(tiles / 8) dependent LDS round trips rather than O(tiles).
 struct FView {
     const unsigned long long* F;
     const unsigned long long* Fsr;
     const unsigned long long* Fsc;
     int tw, wr, wc;
 };
+// Tiles [t0, t1] of one summary line (bit per tile, <= 2 words: grids up to 1024 cells a side):
+// OR of F[base + tx * stride] & (cell mask of tile tx), 8 frontier tiles per round.
+template <bool VERT>
+__device__ __forceinline__ bool line_hits(const unsigned long long* F, const unsigned long long* sum, int base, int stride,
+                                          int t0, int t1, int a, int b, int sh) {
+    const int w0 = t0 >> 6, w1 = t1 >> 6;
+    for (int w = w0; w <= w1; w++) {
+        unsigned long long m = sum[w];
+        if (w == w0) m &= ~0ull << (t0 & 63);
+        if (w == w1) m &= ~0ull >> (63 - (t1 & 63));
+        while (m) {
+            const int p = __ffsll((long long)m) - 1;
+            unsigned long long acc = 0ull;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                if (p + j < 64 && ((m >> (p + j)) & 1ull)) {
+                    const int tx = w * 64 + p + j;
+                    const int lo = (tx == t0) ? a : 0, hi = (tx == t1) ? b : 7;
+                    unsigned long long cm;
+                    if (VERT) cm = (0x0101010101010101ull << sh) & (~0ull >> (8 * (7 - hi))) & (~0ull << (8 * lo));
+                    else cm = (unsigned long long)((0xFFu >> (7 - hi)) & (0xFFu << lo) & 0xFFu) << sh;
+                    acc |= F[base + tx * stride] & cm;
+                }
+            }
+            if (acc) return true;
+            m = (p + 8 >= 64) ? 0ull : (m & (~0ull << (p + 8)));
+        }
+    }
+    return false;
+}
 __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
-    if (ru.y0 == ru.y1) {   // horizontal (or a single cell)
-        const int y = ru.y0, ty = y >> 3, sh = (y & 7) * 8;
-        const int t0 = ru.x0 >> 3, t1 = ru.x1 >> 3;
-        const unsigned long long* row = V.Fsr + ty * V.wr;
-        for (int w = t0 >> 6; w <= (t1 >> 6); w++) {
-            const int lo = max(t0 - w * 64, 0), hi = min(t1 - w * 64, 63);
-            unsigned long long m = row[w] & (~0ull << lo) & (~0ull >> (63 - hi));
-            while (m) {
-                const int tx = w * 64 + __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const int a = max((int)ru.x0, tx * 8) & 7, b = min((int)ru.x1, tx * 8 + 7) & 7;
-                if (V.F[ty * V.tw + tx] & ((unsigned long long)((0xFFu >> (7 - b)) & (0xFFu << a) & 0xFFu) << sh)) return true;
-            }
-        }
-        return false;
-    } else if (ru.x0 == ru.x1) {   // vertical
+    if (ru.y0 == ru.y1) {   // horizontal (or a single cell): tile row ty, tiles x0>>3 .. x1>>3
+        const int y = ru.y0, ty = y >> 3;
+        return line_hits<false>(V.F, V.Fsr + ty * V.wr, ty * V.tw, 1, ru.x0 >> 3, ru.x1 >> 3, ru.x0 & 7, ru.x1 & 7,
+                                (y & 7) * 8);
+    } else if (ru.x0 == ru.x1) {   // vertical: tile column tx, tiles y0>>3 .. y1>>3
         const int x = ru.x0, tx = x >> 3;
-        const unsigned long long colm = 0x0101010101010101ull << (x & 7);
-        const int t0 = ru.y0 >> 3, t1 = ru.y1 >> 3;
-        const unsigned long long* col = V.Fsc + tx * V.wc;
-        for (int w = t0 >> 6; w <= (t1 >> 6); w++) {
-            const int lo = max(t0 - w * 64, 0), hi = min(t1 - w * 64, 63);
-            unsigned long long m = col[w] & (~0ull << lo) & (~0ull >> (63 - hi));
-            while (m) {
-                const int ty = w * 64 + __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const int a = max((int)ru.y0, ty * 8) & 7, b = min((int)ru.y1, ty * 8 + 7) & 7;
-                if (V.F[ty * V.tw + tx] & colm & (~0ull >> (8 * (7 - b))) & (~0ull << (8 * a))) return true;
-            }
-        }
-        return false;
+        return line_hits<true>(V.F, V.Fsc + tx * V.wc, tx, V.tw, ru.y0 >> 3, ru.y1 >> 3, ru.y0 & 7, ru.y1 & 7, x & 7);
     } else {                       // diagonal: cell by cell, skipping empty tiles
         const int dy = (ru.y1 > ru.y0) ? 1 : -1;
         int y = ru.y0;
@@ -175,42 +188,85 @@ struct TileShared {
     unsigned long long cnt, mass;
 };
 
+// Frontier cells on run `ru` (rare path: exact count for the asymmetric nodes).
+__device__ __forceinline__ int run_count_f(const unsigned long long* F, int tw, Run ru) {
+    int c = 0;
+    if (ru.y0 == ru.y1) {
+        const int y = ru.y0, ty = y >> 3, sh = (y & 7) * 8;
+        for (int tx = ru.x0 >> 3; tx <= (ru.x1 >> 3); tx++) {
+            const int lo = max((int)ru.x0, tx * 8) & 7, hi = min((int)ru.x1, tx * 8 + 7) & 7;
+            c += __popcll(F[ty * tw + tx] & ((unsigned long long)((0xFFu >> (7 - hi)) & (0xFFu << lo) & 0xFFu) << sh));
+        }
+    } else if (ru.x0 == ru.x1) {
+        const int x = ru.x0, tx = x >> 3;
+        const unsigned long long colm = 0x0101010101010101ull << (x & 7);
+        for (int ty = ru.y0 >> 3; ty <= (ru.y1 >> 3); ty++) {
+            const int lo = max((int)ru.y0, ty * 8) & 7, hi = min((int)ru.y1, ty * 8 + 7) & 7;
+            c += __popcll(F[ty * tw + tx] & colm & (~0ull >> (8 * (7 - hi))) & (~0ull << (8 * lo)));
+        }
+    } else {
+        const int dy = (ru.y1 > ru.y0) ? 1 : -1;
+        int y = ru.y0;
+        for (int x = ru.x0; x <= ru.x1; x++, y += dy) c += (int)((F[(y >> 3) * tw + (x >> 3)] >> ((y & 7) * 8 + (x & 7))) & 1ull);
+    }
+    return c;
+}
+__device__ __forceinline__ bool cell_on_run(Run ru, int x, int y) {
+    if (ru.y0 == ru.y1) return y == ru.y0 && x >= ru.x0 && x <= ru.x1;
+    if (ru.x0 == ru.x1) return x == ru.x0 && y >= ru.y0 && y <= ru.y1;
+    if (x < ru.x0 || x > ru.x1) return false;
+    return y == ru.y0 + ((ru.y1 > ru.y0) ? 1 : -1) * (x - ru.x0);
+}
+
 // Exact bottom-up test for a node with asymmetric visibility (rare): hit iff some frontier cell u
-// is an in-neighbour, i.e. u in Extra(v), or u in cells(v) and u not in Missing(v).  Whole wave.
-__device__ __forceinline__ bool special_hit(const VgaTileParams& P, const unsigned long long* F, int x, int y, int* nr_out) {
+// is an in-neighbour, i.e. u in Extra(v), or u in cells(v) and u not in Missing(v).  Whole wave:
+// Extra first, then the tile-visibility prune, then the scan order 64 runs a step with the summary
+// run test; a run that hits is confirmed unless every frontier cell on it is a Missing cell.
+__device__ __forceinline__ bool special_hit(const VgaTileParams& P, const FView& FV, int id, int x, int y, int* nr_out) {
     const int lane = threadIdx.x & 63;
     const int tw = P.tw, rows = P.rows;
+    const unsigned long long* F = FV.F;
     const int node = P.cell_node[x * rows + y];
     const int si = P.spec_index[node];
-    const int64_t rs = P.node_run_start[node];
-    const int nr = P.node_nruns[node];
+    const int64_t rs = P.tscan_start[id];
+    const int nr = P.tnruns[id];
     const int e0 = P.extra_off[si], e1 = P.extra_off[si + 1];
     const int m0 = P.missing_off[si], m1 = P.missing_off[si + 1];
+    *nr_out = nr;
     bool h = false;
     for (int j = e0 + lane; j < e1; j += 64) {
         const int uc = P.node_cell[P.extra[j]];
         const int ux = uc / rows, uy = uc % rows;
         if (F[(uy >> 3) * tw + (ux >> 3)] & (1ull << ((uy & 7) * 8 + (ux & 7)))) h = true;
     }
-    for (int r = lane; r < nr && !h; r += 64) {
-        const Run ru = P.pool[rs + r];
-        const int dx = (ru.x1 > ru.x0) ? 1 : 0;
-        const int dy = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
-        int cx = ru.x0, cy = ru.y0;
-        for (;;) {
-            if (F[(cy >> 3) * tw + (cx >> 3)] & (1ull << ((cy & 7) * 8 + (cx & 7)))) {
-                const int un = P.cell_node[cx * rows + cy];
-                bool miss = false;
-                for (int j = m0; j < m1; j++) miss |= (P.missing[j] == un);
-                if (!miss) { h = true; break; }
-            }
-            if (cx == ru.x1 && cy == ru.y1) break;
-            cx += dx;
-            cy += dy;
+    if (__ballot(h) != 0ull) return true;
+    if (P.tvis) {
+        const unsigned long long* tv = P.tvis + (size_t)id * P.tvw;
+        unsigned long long ta = 0ull;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int w = j * 64 + lane;
+            if (w < P.tvw) ta |= tv[w] & FV.Fsr[w];
         }
+        if (__ballot(ta != 0ull) == 0ull) return false;
     }
-    *nr_out = nr;
-    return __ballot(h) != 0ull;
+    for (int base = 0; base < nr; base += 64) {
+        const int r = base + lane;
+        if (r < nr) {
+            const Run ru = P.scan_pool[rs + r];
+            if (run_hits_fs(FV, ru)) {
+                int nm = 0;   // Missing cells on this run that are in the frontier
+                for (int j = m0; j < m1; j++) {
+                    const int mc = P.node_cell[P.missing[j]];
+                    const int mx = mc / rows, my = mc % rows;
+                    if (cell_on_run(ru, mx, my) && ((F[(my >> 3) * tw + (mx >> 3)] >> ((my & 7) * 8 + (mx & 7))) & 1ull)) nm++;
+                }
+                h = nm == 0 || run_count_f(F, tw, ru) > nm;
+            }
+        }
+        if (__ballot(h) != 0ull) return true;
+    }
+    return false;
 }
 
 // V (visited) and X (next level) are per-workgroup bitmaps in HBM (they stay in the L2/MALL; a
@@ -235,8 +291,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
     int4* Q = P.queue + (size_t)blockIdx.x * nt;
     int32_t* L = P.list + (size_t)blockIdx.x * nt * 64;
     const size_t hstride = (size_t)nt * 64;
-    unsigned long long runs_tested = 0, fail_cells = 0, fail_runs = 0, cr_tiles = 0, pruned = 0, tv_tests = 0, hard_runs = 0, hard_hits = 0;
-    unsigned long long cyc[5] = {0, 0, 0, 0, 0};   // leader-thread phase clocks
+    unsigned long long runs_tested = 0, fail_cells = 0, fail_runs = 0, cr_tiles = 0, pruned = 0, tv_tests = 0, hard_runs = 0, hard_hits = 0, ftv_hits = 0, b_tiles = 0, b_cells = 0, tt_tiles = 0, c_busy = 0, c_scan = 0, c_spec = 0, n_spec = 0;
+    unsigned long long cyc[6] = {0, 0, 0, 0, 0, 0};   // leader-thread phase clocks ([5]: top-down levels > 1)
     unsigned long long tmark = 0;
 
     uint16_t* Hn = P.hint;
@@ -329,32 +385,66 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 for (int it = wave; it < qn; it += NW) {
                     const int4 e = Q[it];
                     const int t = e.x;
-                    const unsigned long long mask = (unsigned long long)(unsigned)e.z | ((unsigned long long)(unsigned)e.w << 32);
+                    unsigned long long mask = (unsigned long long)(unsigned)e.z | ((unsigned long long)(unsigned)e.w << 32);
                     bool hit = false, to_hard = false;
                     int hard_val = 0;
+                    if (lane == 0) { b_tiles++; b_cells += (unsigned long long)__popcll(mask); }
+                    // every load that depends only on (t, lane) is issued up front, so the tile costs
+                    // about two memory round trips before the LDS tests instead of one per decision
+                    const unsigned long long reg = P.regular_tiles[t];
+                    const int id = (t << 6) | lane;
+                    const bool mine = (mask >> lane) & 1ull;
+                    const bool lane_reg = !SPECIAL || ((reg >> lane) & 1ull);
+                    int64_t ss = 0;
+                    int nr = 0, hp = 0xFFFF;
+                    Run hd[KH];
+                    if (mine && lane_reg) {
+                        ss = P.tscan_start[id];
+                        nr = P.tnruns[id];
+                        hp = Hn[id];
+#pragma unroll
+                        for (int r = 0; r < KH; r++) hd[r] = P.heads[r * hstride + id];
+                    }
+                    if (P.ttvis) {
+                        // a frontier tile that every regular cell of t sees completely: all of t's
+                        // unvisited regular cells are at the next level (tvw <= 256: 4 words a lane)
+                        const unsigned long long* tt = P.ttvis + (size_t)t * P.tvw;
+                        unsigned long long acc = 0ull;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const int w = j * 64 + lane;
+                            if (w < P.tvw) acc |= tt[w] & Fsr[w];
+                        }
+                        if (__ballot(acc != 0ull) != 0ull) {
+                            const unsigned long long R = mask & reg;
+                            if (lane == 0) { or_wg(&Xg[t], R); tt_tiles++; }
+                            mask &= ~R;
+                        }
+                    }
                     if ((mask >> lane) & 1ull) {
-                        const int id = (t << 6) | lane;
-                        if (SPECIAL && !((P.regular_tiles[t] >> lane) & 1ull)) {
+                        if (!lane_reg) {
                             to_hard = true;
                             hard_val = -1 - id;   // special node: exact path
                         } else {
-                            const int64_t ss = P.tscan_start[id];
-                            const int nr = P.tnruns[id];
-                            const int hp = Hn[id];
                             if (hp >= KH && hp < nr) {   // the run that hit for a recent source
                                 runs_tested++;
                                 hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
                             }
-                            // heads (coalesced across the wave), then the next runs of the scan order
-                            // on this lane; 4 loads in flight per batch
-                            const int lim = min(nr, KH + BEXT);
-                            for (int base = 0; base < lim && !hit; base += 4) {
+                            // heads (already in registers), then the next runs of the scan order on
+                            // this lane, 4 loads in flight per batch
+#pragma unroll
+                            for (int r = 0; r < KH; r++)
+                                if (!hit && r < nr) {
+                                    runs_tested++;
+                                    if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != r) Hn[id] = (uint16_t)r; }
+                                }
+                            const int lim = min(nr, KH + P.bext);
+                            for (int base = KH; base < lim && !hit; base += 4) {
                                 Run rr[4];
 #pragma unroll
                                 for (int j = 0; j < 4; j++) {
                                     const int r = base + j;
-                                    if (r < KH) rr[j] = P.heads[r * hstride + id];
-                                    else if (r < lim) rr[j] = P.scan_pool[ss + r];
+                                    if (r < lim) rr[j] = P.scan_pool[ss + r];
                                     else rr[j].x0 = -1;
                                 }
 #pragma unroll
@@ -365,7 +455,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                                     }
                             }
                             if (!hit) {
-                                if (nr > KH + BEXT) { to_hard = true; hard_val = id; }
+                                if (nr > KH + P.bext) { to_hard = true; hard_val = id; }
                                 else { fail_cells++; fail_runs += nr; }
                             }
                         }
@@ -384,6 +474,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[2] += n - tmark; tmark = n; }
                 const int hn = S.hn;
                 // ---- C: hard cells, a wave scans 64 runs at a time (dynamic work counter)
+                const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
                 for (;;) {
                     int it = 0;
                     if (lane == 0) it = atomicAdd(&S.item, 1);
@@ -397,28 +488,44 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     if (SPECIAL && special) {
                         int x, y;
                         xy_of_tile_id(id, tw, x, y);
-                        found = special_hit(P, F, x, y, &nr);
+                        const unsigned long long sp_t0 = __builtin_amdgcn_s_memtime();
+                        found = special_hit(P, FV, id, x, y, &nr);
+                        if (lane == 0) { c_spec += __builtin_amdgcn_s_memtime() - sp_t0; n_spec++; }
                         if (lane == 0) runs_tested += (unsigned long long)nr;
                     } else {
                         const int64_t rs = P.tscan_start[id];
                         nr = P.tnruns[id];
-                        int base = KH + BEXT;   // the first KH + BEXT runs were tested in phase B
-                        bool pruned_now = false;
+                        int base = KH + P.bext;   // the first KH + bext runs were tested in phase B
+                        bool pruned_now = false, certain = false;
                         if (P.tvis) {
-                            // no tile the cell sees holds a frontier cell: no run can hit (one
-                            // coalesced 2 KB row instead of the whole run list; most cells that
-                            // would scan everything without a hit stop here)
+                            // A frontier tile the cell sees completely is a certain hit (regular cell:
+                            // in-set == out-set); no tile the cell sees holding a frontier cell means
+                            // no run can hit.  Both rows (tvw <= 256: 4 words a lane) are loaded at once.
                             const unsigned long long* tv = P.tvis + (size_t)id * P.tvw;
-                            bool any = false;
-                            for (int w = lane; w < P.tvw; w += 64) any |= (tv[w] & Fsr[w]) != 0ull;
+                            const unsigned long long* ftv = P.ftvis ? P.ftvis + (size_t)id * P.tvw : nullptr;
+                            unsigned long long fa = 0ull, ta = 0ull;
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                const int w = j * 64 + lane;
+                                if (w < P.tvw) {
+                                    const unsigned long long fs = Fsr[w];
+                                    ta |= tv[w] & fs;
+                                    if (ftv) fa |= ftv[w] & fs;
+                                }
+                            }
+                            certain = __ballot(fa != 0ull) != 0ull;
                             if (lane == 0) tv_tests++;
-                            if (__ballot(any) == 0ull) {
+                            if (certain) {
+                                found = true;
+                                if (lane == 0) { ftv_hits++; hard_hits++; }
+                            } else if (__ballot(ta != 0ull) == 0ull) {
                                 base = nr;
                                 pruned_now = true;
                                 if (lane == 0) pruned++;
                             }
                         }
                         // 4 runs per lane per step (256 per wave): four independent loads in flight
+                        const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
                         for (; base < nr && !found; base += 256) {
                             Run rr[4];
 #pragma unroll
@@ -436,8 +543,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                             found = fmin != (1 << 30);
                             if (found && lane == 0) Hn[id] = (uint16_t)min(fmin, 0xFFFE);
                         }
-                        if (lane == 0 && !(P.tvis && base == nr && !found && nr > KH + BEXT && pruned_now)) {
-                            const unsigned long long sc = (unsigned long long)max(min(base, nr) - KH - BEXT, 0);
+                        if (lane == 0) c_scan += __builtin_amdgcn_s_memtime() - s_t0;
+                        if (lane == 0 && !certain && !(P.tvis && base == nr && !found && nr > KH + P.bext && pruned_now)) {
+                            const unsigned long long sc = (unsigned long long)max(min(base, nr) - KH - P.bext, 0);
                             runs_tested += sc;
                             hard_runs += sc;
                             hard_hits += found ? 1ull : 0ull;
@@ -448,6 +556,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                         else { fail_cells++; fail_runs += (unsigned long long)nr; }
                     }
                 }
+                if (lane == 0) c_busy += __builtin_amdgcn_s_memtime() - c_t0;
             } else {
                 // ---- top-down from the frontier F (small frontier): list it, then reuse F's LDS as
                 // the bitmap the frontier's runs are pushed into
@@ -485,7 +594,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             {
                 const unsigned long long n = __builtin_amdgcn_s_memtime();
                 if (bottom_up) cyc[3] += n - tmark;
-                else cyc[0] += n - tmark;
+                else cyc[level == 0 ? 0 : 5] += n - tmark;
                 tmark = n;
             }
             // ---- level bookkeeping: count X, publish the expandable part as the next frontier
@@ -546,6 +655,14 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
         tv_tests += __shfl_xor(tv_tests, off);
         hard_runs += __shfl_xor(hard_runs, off);
         hard_hits += __shfl_xor(hard_hits, off);
+        ftv_hits += __shfl_xor(ftv_hits, off);
+        b_tiles += __shfl_xor(b_tiles, off);
+        b_cells += __shfl_xor(b_cells, off);
+        tt_tiles += __shfl_xor(tt_tiles, off);
+        c_busy += __shfl_xor(c_busy, off);
+        c_scan += __shfl_xor(c_scan, off);
+        c_spec += __shfl_xor(c_spec, off);
+        n_spec += __shfl_xor(n_spec, off);
     }
     if (lane == 0) {
         if (runs_tested) atomicAdd(&P.stats[0], runs_tested);
@@ -555,9 +672,17 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
         if (tv_tests) atomicAdd(&P.stats[14], tv_tests);
         if (hard_hits) atomicAdd(&P.stats[1], hard_hits);
         if (hard_runs) atomicAdd(&P.stats[15], hard_runs);
+        if (ftv_hits) atomicAdd(&P.stats[16], ftv_hits);
+        if (b_tiles) { atomicAdd(&P.stats[18], b_tiles); atomicAdd(&P.stats[19], b_cells); }
+        if (tt_tiles) atomicAdd(&P.stats[20], tt_tiles);
+        if (c_busy) atomicAdd(&P.stats[21], c_busy);
+        if (c_scan) atomicAdd(&P.stats[22], c_scan);
+        if (n_spec) { atomicAdd(&P.stats[23], c_spec); atomicAdd(&P.stats[24], n_spec); }
     }
-    if (tid == 0)
+    if (tid == 0) {
         for (int i = 0; i < 5; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
+        atomicAdd(&P.stats[17], cyc[5]);
+    }
 }
 
 // ---------------------------------------------------------------- prep: tile-ordered cell arrays
@@ -583,37 +708,76 @@ __global__ void tile_heads_kernel(int rows, int tw, const int32_t* node_cell, in
 
 // Tile-visibility rows: bit (ty, tx) of cell id's row is set iff the cell sees some cell of tile
 // (tx, ty); same [th][ceil(tw/64)] word layout as the kernel's Fsr summary, so one AND per word
-// tells whether any frontier tile is in view.  One wave per node, the row built in LDS.
+// tells whether any frontier tile is in view.  The full-visibility row (ftvis) sets the bit only
+// when the cell sees EVERY discoverable (non-seed) cell of the tile: a frontier tile under such a
+// bit is a certain hit for a regular cell (in-set == out-set), so phase C resolves it without a run
+// scan.  One wave per node; the rows and the per-tile covered-cell counts (bytes) are built in LDS.
 constexpr int TV_WAVES = 4;
+__device__ __forceinline__ void tv_count(uint32_t* cnt, int t, int c) {
+    atomicAdd(&cnt[t >> 2], (uint32_t)c << (8 * (t & 3)));
+}
 __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int tw, int th, const int32_t* node_cell,
                                                                  int64_t n, const int64_t* node_run_start,
                                                                  const int32_t* node_nruns, const Run* pool,
-                                                                 unsigned long long* tvis) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long tvrow[];
+                                                                 const unsigned long long* seed_tiles,
+                                                                 unsigned long long* tvis, unsigned long long* ftvis) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long tvlds[];
+    const int nt = tw * th, ncw = (nt + 3) / 4;
     const int wr = (tw + 63) / 64, tvw = th * wr;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long* row = tvrow + (size_t)wave * tvw;
+    uint8_t* nsc = (uint8_t*)tvlds;                                   // [nt] non-seed cells per tile
+    unsigned long long* row = tvlds + (ncw + 1) / 2 + (size_t)wave * (tvw + (ncw + 1) / 2);
+    uint32_t* cnt = (uint32_t*)(row + tvw);                            // [nt] covered non-seed cells (bytes)
+    if (ftvis)
+        for (int t = threadIdx.x; t < nt; t += 64 * TV_WAVES) nsc[t] = (uint8_t)__popcll(~seed_tiles[t]);
+    __syncthreads();
     for (int64_t k = (int64_t)blockIdx.x * TV_WAVES + wave; k < n; k += (int64_t)gridDim.x * TV_WAVES) {
         for (int w = lane; w < tvw; w += 64) row[w] = 0ull;
+        if (ftvis)
+            for (int w = lane; w < ncw; w += 64) cnt[w] = 0u;
         __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
         const int64_t rs = node_run_start[k];
         const int nr = node_nruns[k];
         for (int r = lane; r < nr; r += 64) {
             const Run ru = pool[rs + r];
             if (ru.y0 == ru.y1) {
-                const int ty = ru.y0 >> 3, t0 = ru.x0 >> 3, t1 = ru.x1 >> 3;
+                const int y = ru.y0, ty = y >> 3, t0 = ru.x0 >> 3, t1 = ru.x1 >> 3;
                 for (int w = t0 >> 6; w <= (t1 >> 6); w++) {
                     const int lo = max(t0 - w * 64, 0), hi = min(t1 - w * 64, 63);
                     atomicOr(&row[ty * wr + w], (~0ull << lo) & (~0ull >> (63 - hi)));
                 }
+                if (ftvis)
+                    for (int tx = t0; tx <= t1; tx++) {
+                        const int a = max((int)ru.x0, tx * 8) & 7, b = min((int)ru.x1, tx * 8 + 7) & 7;
+                        const unsigned long long m = (unsigned long long)((0xFFu >> (7 - b)) & (0xFFu << a) & 0xFFu) << ((y & 7) * 8);
+                        const int t = ty * tw + tx;
+                        const int c = __popcll(m & ~seed_tiles[t]);
+                        if (c) tv_count(cnt, t, c);
+                    }
             } else if (ru.x0 == ru.x1) {
-                const int tx = ru.x0 >> 3;
-                for (int ty = ru.y0 >> 3; ty <= (ru.y1 >> 3); ty++) atomicOr(&row[ty * wr + (tx >> 6)], 1ull << (tx & 63));
+                const int x = ru.x0, tx = x >> 3;
+                const unsigned long long colm = 0x0101010101010101ull << (x & 7);
+                for (int ty = ru.y0 >> 3; ty <= (ru.y1 >> 3); ty++) {
+                    atomicOr(&row[ty * wr + (tx >> 6)], 1ull << (tx & 63));
+                    if (ftvis) {
+                        const int a = max((int)ru.y0, ty * 8) & 7, b = min((int)ru.y1, ty * 8 + 7) & 7;
+                        const unsigned long long m = colm & (~0ull >> (8 * (7 - b))) & (~0ull << (8 * a));
+                        const int t = ty * tw + tx;
+                        const int c = __popcll(m & ~seed_tiles[t]);
+                        if (c) tv_count(cnt, t, c);
+                    }
+                }
             } else {
                 const int dy = (ru.y1 > ru.y0) ? 1 : -1;
                 int y = ru.y0;
-                for (int x = ru.x0; x <= ru.x1; x++, y += dy)
+                for (int x = ru.x0; x <= ru.x1; x++, y += dy) {
                     atomicOr(&row[(y >> 3) * wr + (x >> 6 >> 3)], 1ull << ((x >> 3) & 63));
+                    if (ftvis) {
+                        const int t = (y >> 3) * tw + (x >> 3);
+                        if (!((seed_tiles[t] >> ((y & 7) * 8 + (x & 7))) & 1ull)) tv_count(cnt, t, 1);
+                    }
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -622,7 +786,42 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int t
         const int id = tile_id_of(c / rows, c % rows, tw);
         unsigned long long* out = tvis + (size_t)id * tvw;
         for (int w = lane; w < tvw; w += 64) out[w] = row[w];
+        if (ftvis) {
+            // a tile is fully seen when the covered count reaches its non-seed count (a node's runs
+            // are disjoint, so no cell is counted twice)
+            unsigned long long* fout = ftvis + (size_t)id * tvw;
+            for (int w = lane; w < tvw; w += 64) {
+                unsigned long long m = row[w], f = 0ull;
+                const int tyw = w / wr, tx0 = (w % wr) * 64;
+                while (m) {
+                    const int j = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    const int t = tyw * tw + tx0 + j;
+                    const int cv = (cnt[t >> 2] >> (8 * (t & 3))) & 0xFF;
+                    if (cv == nsc[t] && cv > 0) f |= 1ull << j;
+                }
+                fout[w] = f;
+            }
+        }
         __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// Tile-to-tile full visibility: row t = AND of the ftvis rows of tile t's regular cells (bit u set
+// iff every regular cell of t sees every non-seed cell of tile u).  One wave per tile.
+__global__ void tile_tt_kernel(int nt, int tvw, const unsigned long long* regular_tiles, const unsigned long long* ftvis,
+                               unsigned long long* ttvis) {
+    const int lane = threadIdx.x & 63;
+    const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (t >= nt) return;
+    const unsigned long long R = regular_tiles[t];
+    for (int w = lane; w < tvw; w += 64) {
+        unsigned long long acc = R ? ~0ull : 0ull;
+        for (unsigned long long m = R; m && acc; m &= m - 1) {
+            const int b = __ffsll((long long)m) - 1;
+            acc &= ftvis[((size_t)t * 64 + b) * tvw + w];
+        }
+        ttvis[(size_t)t * tvw + w] = acc;
     }
 }
 

@@ -42,8 +42,13 @@ for k, v in configs:
                       "fail_runs_per_src": st["vga_fail_runs"] / nsrc, "cr_tiles_per_src": st["vga_cr_tiles"] / nsrc,
                       "pruned_cells_per_src": st["vga_pruned_cells"] / nsrc,
                       "hard_cells_per_src": st["vga_hard_cells"] / nsrc, "hard_hits_per_src": st["vga_hard_hits"] / nsrc,
-                      "hard_runs_per_src": st["vga_hard_runs"] / nsrc,
-                      "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc, "kernel": st["vga_kernel"],
+                      "hard_runs_per_src": st["vga_hard_runs"] / nsrc, "hard_certain_per_src": st["vga_hard_certain"] / nsrc,
+                      "topdown_cycles_per_src": st["vga_topdown_cycles"] / nsrc,
+                      "b_tiles_per_src": st["vga_b_tiles"] / nsrc, "b_cells_per_src": st["vga_b_cells"] / nsrc,
+                      "tt_tiles_per_src": st["vga_tt_tiles"] / nsrc,
+                      "c_busy_per_src": st["vga_c_busy"] / nsrc, "c_scan_per_src": st["vga_c_scan"] / nsrc,
+                      "c_spec_per_src": st["vga_c_spec"] / nsrc, "n_spec_per_src": st["vga_n_spec"] / nsrc,
+                      "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc, "kernel": st["vga_kernel"], "special_nodes": st["vga_special_nodes"],
                       "launch_blocks": st["vga_launch"] & 0xFFFFFFFF,
                       "phase_cycles_per_src": {kk: vv / nsrc for kk, vv in ctx.last_phase_cycles().items()}}),
           flush=True)
