@@ -1026,6 +1026,8 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
     Q.bext = BEXT_DEFAULT;
     if (const char* b = getenv("DMX_VGA_BEXT")) Q.bext = std::max(0, atoi(b));
+    Q.crk = 2;   // the 2 longest common runs: the next two rarely resolve a tile the TT rows miss
+    if (const char* c = getenv("DMX_VGA_CRK")) Q.crk = std::min(CRK, std::max(0, atoi(c)));
     Q.work_counter = ctx->counters.p + 0; Q.error = ctx->counters.p + 1;
     DevBuf<int32_t> d_hist, d_nlev;
     HIPCHK(d_hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));

@@ -66,6 +66,7 @@ struct VgaTileParams {
     int32_t* list;            // per workgroup [nt*64]: hard cells / frontier cells
     int maxlev;
     int bext;                 // phase-B runs after the heads (BEXT_DEFAULT)
+    int crk;                  // tile-common runs tested in phase A (<= CRK)
     int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
     int32_t* nlev_out;        // [N] levels (0: source skipped)
     int* error;
@@ -291,9 +292,13 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
     int4* Q = P.queue + (size_t)blockIdx.x * nt;
     int32_t* L = P.list + (size_t)blockIdx.x * nt * 64;
     const size_t hstride = (size_t)nt * 64;
-    unsigned long long runs_tested = 0, fail_cells = 0, fail_runs = 0, cr_tiles = 0, pruned = 0, tv_tests = 0, hard_runs = 0, hard_hits = 0, ftv_hits = 0, b_tiles = 0, b_cells = 0, tt_tiles = 0, c_busy = 0, c_scan = 0, c_spec = 0, n_spec = 0;
-    unsigned long long cyc[6] = {0, 0, 0, 0, 0, 0};   // leader-thread phase clocks ([5]: top-down levels > 1)
-    unsigned long long tmark = 0;
+    // work counters live in LDS (flushed to P.stats at exit) so they cost no registers: a 1024-thread
+    // workgroup has 128 VGPRs a lane and every spill is a scratch round trip
+    __shared__ unsigned long long SC[32];
+#define ST(k, v) atomicAdd(&SC[k], (unsigned long long)(v))
+    unsigned rt = 0;                  // runs tested by this lane (flushed per source)
+    unsigned long long tmark = 0;     // leader-thread phase clock
+    for (int i = tid; i < 32; i += NT) SC[i] = 0ull;
 
     uint16_t* Hn = P.hint;
     if (tid == 0) { S.qn = 0; S.hn = 0; S.item = 0; S.cnt = 0; S.mass = 0; S.src = -1; }
@@ -344,27 +349,31 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 const int64_t rs = P.node_run_start[src];
                 const int nr = P.node_nruns[src];
                 for (int r = tid; r < nr; r += NT) run_or(F, tw, P.pool[rs + r]);
-                if (tid < nr) runs_tested += (unsigned long long)((nr - tid + NT - 1) / NT);
+                if (tid < nr) rt += (unsigned)((nr - tid + NT - 1) / NT);
                 sync_global();
                 for (int t = tid; t < nt; t += NT) Xg[t] = F[t] & ~Vg[t];
-                { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[0] += n - tmark; tmark = n; }
+                if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(8, n - tmark); tmark = n; }
             } else if (bottom_up) {
                 // ---- A: tile-common runs
                 for (int t0 = 0; t0 < nt; t0 += NT) {
                     const int t = t0 + tid;
                     unsigned long long U = 0ull;
                     if (t < nt) {
+                        // V, the regular mask and the CRK common runs in one round trip
+                        Run c[CRK];
+#pragma unroll
+                        for (int j = 0; j < CRK; j++) c[j] = P.cr[CRK * t + j];
                         U = ~Vg[t];
                         const unsigned long long R = U & P.regular_tiles[t];
                         if (R) {
                             bool hit = false;
-                            for (int j = 0; j < CRK && !hit; j++) {
-                                const Run c = P.cr[CRK * t + j];
-                                if (c.x0 < 0) break;
-                                runs_tested++;
-                                hit = run_hits_fs(FV, c);
-                            }
-                            if (hit) { Xg[t] = R; U &= ~R; cr_tiles++; }
+#pragma unroll 1
+                            for (int j = 0; j < CRK; j++)
+                                if (!hit && j < P.crk && c[j].x0 >= 0) {
+                                    rt++;
+                                    hit = run_hits_fs(FV, c[j]);
+                                }
+                            if (hit) { Xg[t] = R; U &= ~R; ST(7, 1); }
                         }
                     }
                     const unsigned long long want = __ballot(U != 0ull);
@@ -379,7 +388,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     }
                 }
                 sync_global();
-                { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[1] += n - tmark; tmark = n; }
+                if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(9, n - tmark); tmark = n; }
                 const int qn = S.qn;
                 // ---- B: head runs, one wave per queued tile, lane = cell
                 for (int it = wave; it < qn; it += NW) {
@@ -388,7 +397,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     unsigned long long mask = (unsigned long long)(unsigned)e.z | ((unsigned long long)(unsigned)e.w << 32);
                     bool hit = false, to_hard = false;
                     int hard_val = 0;
-                    if (lane == 0) { b_tiles++; b_cells += (unsigned long long)__popcll(mask); }
+                    if (lane == 0) { ST(18, 1); ST(19, __popcll(mask)); }
                     // every load that depends only on (t, lane) is issued up front, so the tile costs
                     // about two memory round trips before the LDS tests instead of one per decision
                     const unsigned long long reg = P.regular_tiles[t];
@@ -397,13 +406,14 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     const bool lane_reg = !SPECIAL || ((reg >> lane) & 1ull);
                     int64_t ss = 0;
                     int nr = 0, hp = 0xFFFF;
-                    Run hd[KH];
+                    constexpr int KH0 = 4;   // heads preloaded with the TT row (register budget)
+                    Run hd[KH0];
                     if (mine && lane_reg) {
                         ss = P.tscan_start[id];
                         nr = P.tnruns[id];
                         hp = Hn[id];
 #pragma unroll
-                        for (int r = 0; r < KH; r++) hd[r] = P.heads[r * hstride + id];
+                        for (int r = 0; r < KH0; r++) hd[r] = P.heads[r * hstride + id];
                     }
                     if (P.ttvis) {
                         // a frontier tile that every regular cell of t sees completely: all of t's
@@ -417,7 +427,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                         }
                         if (__ballot(acc != 0ull) != 0ull) {
                             const unsigned long long R = mask & reg;
-                            if (lane == 0) { or_wg(&Xg[t], R); tt_tiles++; }
+                            if (lane == 0) { or_wg(&Xg[t], R); ST(20, 1); }
                             mask &= ~R;
                         }
                     }
@@ -427,36 +437,40 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                             hard_val = -1 - id;   // special node: exact path
                         } else {
                             if (hp >= KH && hp < nr) {   // the run that hit for a recent source
-                                runs_tested++;
+                                rt++;
                                 hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
                             }
                             // heads (already in registers), then the next runs of the scan order on
                             // this lane, 4 loads in flight per batch
-#pragma unroll
-                            for (int r = 0; r < KH; r++)
+#pragma unroll 1
+                            for (int r = 0; r < KH0; r++)
                                 if (!hit && r < nr) {
-                                    runs_tested++;
+                                    rt++;
                                     if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != r) Hn[id] = (uint16_t)r; }
                                 }
                             const int lim = min(nr, KH + P.bext);
-                            for (int base = KH; base < lim && !hit; base += 4) {
+                            for (int base = KH0; base < lim && !hit; base += 4) {
                                 Run rr[4];
 #pragma unroll
                                 for (int j = 0; j < 4; j++) {
                                     const int r = base + j;
-                                    if (r < lim) rr[j] = P.scan_pool[ss + r];
+                                    if (r < KH) rr[j] = P.heads[r * hstride + id];
+                                    else if (r < lim) rr[j] = P.scan_pool[ss + r];
                                     else rr[j].x0 = -1;
                                 }
+                                bool h4[4];
 #pragma unroll
-                                for (int j = 0; j < 4; j++)
-                                    if (!hit && rr[j].x0 >= 0) {
-                                        runs_tested++;
-                                        if (run_hits_fs(FV, rr[j])) { hit = true; if (hp != base + j) Hn[id] = (uint16_t)(base + j); }
-                                    }
+                                for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
+                                int fj = -1;
+#pragma unroll
+                                for (int j = 3; j >= 0; j--)
+                                    if (h4[j]) fj = j;
+                                rt += (unsigned)min(4, lim - base);
+                                if (fj >= 0) { hit = true; if (hp != base + fj) Hn[id] = (uint16_t)(base + fj); }
                             }
                             if (!hit) {
                                 if (nr > KH + P.bext) { to_hard = true; hard_val = id; }
-                                else { fail_cells++; fail_runs += nr; }
+                                else { ST(5, 1); ST(6, nr); }
                             }
                         }
                     }
@@ -471,7 +485,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     }
                 }
                 sync_global();
-                { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[2] += n - tmark; tmark = n; }
+                if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(10, n - tmark); tmark = n; }
                 const int hn = S.hn;
                 // ---- C: hard cells, a wave scans 64 runs at a time (dynamic work counter)
                 const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
@@ -490,8 +504,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                         xy_of_tile_id(id, tw, x, y);
                         const unsigned long long sp_t0 = __builtin_amdgcn_s_memtime();
                         found = special_hit(P, FV, id, x, y, &nr);
-                        if (lane == 0) { c_spec += __builtin_amdgcn_s_memtime() - sp_t0; n_spec++; }
-                        if (lane == 0) runs_tested += (unsigned long long)nr;
+                        if (lane == 0) { ST(23, __builtin_amdgcn_s_memtime() - sp_t0); ST(24, 1); }
+                        if (lane == 0) rt += (unsigned)nr;
                     } else {
                         const int64_t rs = P.tscan_start[id];
                         nr = P.tnruns[id];
@@ -514,14 +528,14 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                                 }
                             }
                             certain = __ballot(fa != 0ull) != 0ull;
-                            if (lane == 0) tv_tests++;
+                            if (lane == 0) ST(14, 1);
                             if (certain) {
                                 found = true;
-                                if (lane == 0) { ftv_hits++; hard_hits++; }
+                                if (lane == 0) { ST(16, 1); ST(1, 1); }
                             } else if (__ballot(ta != 0ull) == 0ull) {
                                 base = nr;
                                 pruned_now = true;
-                                if (lane == 0) pruned++;
+                                if (lane == 0) ST(13, 1);
                             }
                         }
                         // 4 runs per lane per step (256 per wave): four independent loads in flight
@@ -535,28 +549,33 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                                 else rr[j].x0 = -1;
                             }
                             int first = 1 << 30;
+                            // the four tests are independent (no early-out between them), so their
+                            // LDS round trips overlap
+                            bool h4[4];
 #pragma unroll
-                            for (int j = 0; j < 4; j++)
-                                if (first == (1 << 30) && rr[j].x0 >= 0 && run_hits_fs(FV, rr[j])) first = base + j * 64 + lane;
+                            for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
+#pragma unroll
+                            for (int j = 3; j >= 0; j--)
+                                if (h4[j]) first = base + j * 64 + lane;
                             int fmin = first;
                             for (int off = 32; off >= 1; off >>= 1) fmin = min(fmin, __shfl_xor(fmin, off));
                             found = fmin != (1 << 30);
                             if (found && lane == 0) Hn[id] = (uint16_t)min(fmin, 0xFFFE);
                         }
-                        if (lane == 0) c_scan += __builtin_amdgcn_s_memtime() - s_t0;
+                        if (lane == 0) ST(22, __builtin_amdgcn_s_memtime() - s_t0);
                         if (lane == 0 && !certain && !(P.tvis && base == nr && !found && nr > KH + P.bext && pruned_now)) {
                             const unsigned long long sc = (unsigned long long)max(min(base, nr) - KH - P.bext, 0);
-                            runs_tested += sc;
-                            hard_runs += sc;
-                            hard_hits += found ? 1ull : 0ull;
+                            rt += (unsigned)sc;
+                            ST(15, sc);
+                            if (found) ST(1, 1);
                         }
                     }
                     if (lane == 0) {
                         if (found) or_wg(&Xg[id >> 6], 1ull << (id & 63));
-                        else { fail_cells++; fail_runs += (unsigned long long)nr; }
+                        else { ST(5, 1); ST(6, nr); }
                     }
                 }
-                if (lane == 0) c_busy += __builtin_amdgcn_s_memtime() - c_t0;
+                if (lane == 0) ST(21, __builtin_amdgcn_s_memtime() - c_t0);
             } else {
                 // ---- top-down from the frontier F (small frontier): list it, then reuse F's LDS as
                 // the bitmap the frontier's runs are pushed into
@@ -585,7 +604,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     const int64_t rs = P.node_run_start[node];
                     const int nr = P.node_nruns[node];
                     for (int r = lane; r < nr; r += 64) run_or(F, tw, P.pool[rs + r]);
-                    if (lane == 0) runs_tested += (unsigned long long)nr;
+                    if (lane == 0) rt += (unsigned)nr;
                 }
                 sync_global();
                 for (int t = tid; t < nt; t += NT) Xg[t] = F[t] & ~Vg[t];
@@ -593,8 +612,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             sync_global();
             {
                 const unsigned long long n = __builtin_amdgcn_s_memtime();
-                if (bottom_up) cyc[3] += n - tmark;
-                else cyc[level == 0 ? 0 : 5] += n - tmark;
+                if (tid == 0) {
+                    if (bottom_up) ST(11, n - tmark);
+                    else ST(level == 0 ? 8 : 17, n - tmark);
+                }
                 tmark = n;
             }
             // ---- level bookkeeping: count X, publish the expandable part as the next frontier
@@ -624,7 +645,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             if (lane == 0 && c_loc) { atomicAdd(&S.cnt, c_loc); atomicAdd(&S.mass, m_loc); }
             sync_global();
             const long long cnt = (long long)S.cnt, mass = (long long)S.mass;
-            { const unsigned long long n = __builtin_amdgcn_s_memtime(); cyc[4] += n - tmark; tmark = n; }
+            if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(12, n - tmark); tmark = n; }
             __syncthreads();
             if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; }
             if (cnt == 0) break;
@@ -635,54 +656,29 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             m_f = mass;
             level++;
             nlev = level + 1;
-            if (tid == 0) atomicAdd(&P.stats[bottom_up ? 3 : 4], 1ull);
+            if (tid == 0) ST(bottom_up ? 3 : 4, 1);
         }
         __syncthreads();
         if (overflow) {
             if (tid == 0) atomicOr(P.error, KERR_LEVELS);
             continue;
         }
+        {   // flush this lane-group's run-test count (32-bit per lane, per source)
+            unsigned r = rt;
+            for (int off = 32; off >= 1; off >>= 1) r += __shfl_xor(r, off);
+            if (lane == 0 && r) ST(0, r);
+            rt = 0;
+        }
         for (int l = tid; l < nlev; l += NT) P.hist_out[src * VGA_HMAX + l] = hist[l];
         if (tid == 0) P.nlev_out[src] = nlev;
         __syncthreads();
     }
-    for (int off = 32; off >= 1; off >>= 1) {
-        runs_tested += __shfl_xor(runs_tested, off);
-        fail_cells += __shfl_xor(fail_cells, off);
-        fail_runs += __shfl_xor(fail_runs, off);
-        cr_tiles += __shfl_xor(cr_tiles, off);
-        pruned += __shfl_xor(pruned, off);
-        tv_tests += __shfl_xor(tv_tests, off);
-        hard_runs += __shfl_xor(hard_runs, off);
-        hard_hits += __shfl_xor(hard_hits, off);
-        ftv_hits += __shfl_xor(ftv_hits, off);
-        b_tiles += __shfl_xor(b_tiles, off);
-        b_cells += __shfl_xor(b_cells, off);
-        tt_tiles += __shfl_xor(tt_tiles, off);
-        c_busy += __shfl_xor(c_busy, off);
-        c_scan += __shfl_xor(c_scan, off);
-        c_spec += __shfl_xor(c_spec, off);
-        n_spec += __shfl_xor(n_spec, off);
-    }
-    if (lane == 0) {
-        if (runs_tested) atomicAdd(&P.stats[0], runs_tested);
-        if (fail_cells) { atomicAdd(&P.stats[5], fail_cells); atomicAdd(&P.stats[6], fail_runs); }
-        if (cr_tiles) atomicAdd(&P.stats[7], cr_tiles);
-        if (pruned) atomicAdd(&P.stats[13], pruned);
-        if (tv_tests) atomicAdd(&P.stats[14], tv_tests);
-        if (hard_hits) atomicAdd(&P.stats[1], hard_hits);
-        if (hard_runs) atomicAdd(&P.stats[15], hard_runs);
-        if (ftv_hits) atomicAdd(&P.stats[16], ftv_hits);
-        if (b_tiles) { atomicAdd(&P.stats[18], b_tiles); atomicAdd(&P.stats[19], b_cells); }
-        if (tt_tiles) atomicAdd(&P.stats[20], tt_tiles);
-        if (c_busy) atomicAdd(&P.stats[21], c_busy);
-        if (c_scan) atomicAdd(&P.stats[22], c_scan);
-        if (n_spec) { atomicAdd(&P.stats[23], c_spec); atomicAdd(&P.stats[24], n_spec); }
-    }
-    if (tid == 0) {
-        for (int i = 0; i < 5; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
-        atomicAdd(&P.stats[17], cyc[5]);
-    }
+    for (int off = 32; off >= 1; off >>= 1) rt += __shfl_xor(rt, off);
+    if (lane == 0 && rt) ST(0, rt);
+    __syncthreads();
+    for (int i = tid; i < 32; i += NT)
+        if (SC[i]) atomicAdd(&P.stats[i], SC[i]);
+#undef ST
 }
 
 // ---------------------------------------------------------------- prep: tile-ordered cell arrays
