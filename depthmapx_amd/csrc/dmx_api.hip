@@ -442,6 +442,8 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.fail_list = fail_list.p;
             P.fail_count = ctx->counters.p + 4;
             P.profile = verbose() ? 1 : 0;
+            // the first pass certifies parallel moment sums; re-runs (list mode) use the serial chains
+            P.exact_moments = (list_n >= 0 || getenv("DMX_MK_EXACT")) ? 1 : 0;
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
                 hipLaunchKernelGGL(makegraph_kernel, dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);

@@ -56,6 +56,7 @@ struct MakeGraphParams {
     int64_t* fail_list;
     int* fail_count;
     int profile;               // 1: accumulate per-phase clocks into stats[8..13]
+    int exact_moments;         // 1: the reference's serial FP64 moment chains; 0: certified parallel sums
 };
 
 // phase clocks (profile builds of a run only; wave-uniform scalar reads)
@@ -181,6 +182,36 @@ __device__ __forceinline__ uint32_t pack_open(int slot, int s, int l) {
     return 1u | ((uint32_t)slot << 1) | ((uint32_t)s << 3) | ((uint32_t)l << 17);
 }
 
+// ---- certified moment sums
+// The reference accumulates sum(d) and sum(d*d) as two serial FP64 chains in addlist order
+// (pointdata.cpp:1490-1495) and stores them as floats.  The fast path sums each lane's share in
+// double-double (error-free TwoSum), reduces the wave, and bounds the serial chain's rounding error
+// by gamma_(n-1) * sum (non-negative summands): when every double within that bound rounds to the
+// same float, that float IS the reference's value.  Otherwise the source is re-run with the serial
+// chains (exact_moments), which happens for ~0.2 % of sources at 1000^2.
+__device__ __forceinline__ void dd_add(double& h, double& l, double v) {
+    const double s = h + v;
+    const double bb = s - h;
+    l += (h - (s - bb)) + (v - bb);
+    h = s;
+}
+__device__ __forceinline__ void dd_merge(double& h, double& l, double bh, double bl) {
+    const double s = h + bh;
+    const double bb = s - h;
+    const double e = (h - (s - bb)) + (bh - bb);
+    const double t = (l + bl) + e;
+    h = s + t;
+    l = t - (h - s);
+}
+__device__ __forceinline__ bool certified_float(double h, double l, long long n, float* out) {
+    const double u = 0x1p-53;
+    const double g = (double)n * u / (1.0 - (double)n * u);
+    const double E = 2.0 * g * h + 2.0 * fabs(l) + h * 0x1p-50;
+    const float a = (float)(h - E), b = (float)(h + E);
+    *out = a;
+    return a == b;
+}
+
 struct Lds {
     double2* gaps;    // [gcap]
     double2* gaps2;   // [gcap] merge output
@@ -269,7 +300,8 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
         if (lane < 32) { L.binc[lane] = 0; L.bfar[lane] = 0; L.bnr[lane] = 0; }
         __syncthreads();
 
-        double tsum = 0.0, tsum2 = 0.0; // wave-uniform, reference order
+        double tsum = 0.0, tsum2 = 0.0; // wave-uniform, reference order (exact_moments)
+        double s1h = 0.0, s1l = 0.0, s2h = 0.0, s2l = 0.0;   // per-lane double-double (fast path)
         int nsize = 0;
         unsigned long long examined = 0;
         int bpos = 0;        // next free run slot in stageB
@@ -491,18 +523,23 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                             atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
                         }
                         MK_T(3);
-                        // serial sums in lane order = reference addlist order
-                        // (the lane index is wave-uniform: v_readlane into SGPRs keeps the serial
-                        // chain on two dependent FP64 adds per cell instead of an LDS round trip)
-                        const int d_lo = __double2loint(this_dist), d_hi = __double2hiint(this_dist);
-                        unsigned long long mm = am;
-                        while (mm) {
-                            const int l = __ffsll((long long)mm) - 1;
-                            const double v = __hiloint2double(__builtin_amdgcn_readlane(d_hi, l),
-                                                              __builtin_amdgcn_readlane(d_lo, l));
-                            tsum += v;
-                            tsum2 += v * v;
-                            mm &= mm - 1;
+                        if (P.exact_moments) {
+                            // serial sums in lane order = reference addlist order
+                            // (the lane index is wave-uniform: v_readlane into SGPRs keeps the serial
+                            // chain on two dependent FP64 adds per cell instead of an LDS round trip)
+                            const int d_lo = __double2loint(this_dist), d_hi = __double2hiint(this_dist);
+                            unsigned long long mm = am;
+                            while (mm) {
+                                const int l = __ffsll((long long)mm) - 1;
+                                const double v = __hiloint2double(__builtin_amdgcn_readlane(d_hi, l),
+                                                                  __builtin_amdgcn_readlane(d_lo, l));
+                                tsum += v;
+                                tsum2 += v * v;
+                                mm &= mm - 1;
+                            }
+                        } else if (add) {
+                            dd_add(s1h, s1l, this_dist);
+                            dd_add(s2h, s2l, this_dist * this_dist);
                         }
                         MK_T(4);
                         nsize += __popcll(am);
@@ -664,6 +701,25 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
             __syncthreads();
             MK_T(6);
         }
+        float m1f = 0.0f, m2f = 0.0f;
+        if (!failed) {
+            if (P.exact_moments) {
+                m1f = (float)tsum;
+                m2f = (float)tsum2;
+            } else {
+                for (int off = 32; off >= 1; off >>= 1) {
+                    const double a = __shfl_xor(s1h, off), b = __shfl_xor(s1l, off);
+                    const double c = __shfl_xor(s2h, off), d = __shfl_xor(s2l, off);
+                    dd_merge(s1h, s1l, a, b);
+                    dd_merge(s2h, s2l, c, d);
+                }
+                // lanes reduce in different orders: take lane 0's pair
+                s1h = __shfl(s1h, 0); s1l = __shfl(s1l, 0); s2h = __shfl(s2h, 0); s2l = __shfl(s2l, 0);
+                const bool ok1 = certified_float(s1h, s1l, nsize, &m1f);
+                const bool ok2 = certified_float(s2h, s2l, nsize, &m2f);
+                if (!(ok1 && ok2)) failed = true;   // re-run with the serial chains (no capacity error)
+            }
+        }
         if (failed) {
             if (lane == 0) P.fail_list[atomicAdd(P.fail_count, 1)] = node;
             // leave the wave in a clean LDS state and drop this source
@@ -703,8 +759,8 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
             if (P.profile)
                 for (int i = 0; i < 8; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
             P.attrs[k * 3 + 0] = (float)nsize;
-            P.attrs[k * 3 + 1] = (float)tsum;
-            P.attrs[k * 3 + 2] = (float)tsum2;
+            P.attrs[k * 3 + 1] = m1f;
+            P.attrs[k * 3 + 2] = m2f;
         }
         __syncthreads();
         for (int i = 0; i < 8; i++) cyc[i] = 0;

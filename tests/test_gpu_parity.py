@@ -304,3 +304,16 @@ def test_makegraph_capacity_retries_are_exact(ctx, monkeypatch, gcap, bcap, spil
     pm = _map(meta)
     g = pm.make_graph(ctx)
     _assert_graph_equal(g.copy(runs=True), A, True)
+
+
+def test_makegraph_certified_moments_equal_serial_chains(ctx, monkeypatch):
+    """The first makeGraph pass sums the moments in parallel (double-double) and keeps a float only
+    when the reference's serial FP64 chain provably rounds to it; the rest are re-run with the
+    serial chains.  Both modes must give the same bits on every node (65k sources)."""
+    meta, A = load_case("syn256mk")
+    pm = _map(meta)
+    fast = pm.make_graph(ctx).copy(runs=False)["attrs"]
+    monkeypatch.setenv("DMX_MK_EXACT", "1")
+    serial = pm.make_graph(ctx).copy(runs=False)["attrs"]
+    np.testing.assert_array_equal(fast.view(np.uint32), serial.view(np.uint32))
+    np.testing.assert_array_equal(fast.view(np.uint32), A["attrs"].view(np.uint32))
