@@ -957,17 +957,17 @@ static int prepare_tiles(dmx_graph* g) {
     return DMX_OK;
 }
 
-extern "C++" template <int NT, bool SPECIAL>
+extern "C++" template <int NT, bool SPECIAL, bool RBM>
 static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_t lds, int64_t* blocks_out,
                        DevBuf<unsigned long long>& xg, DevBuf<int4>& queue, DevBuf<int32_t>& list) {
     int occ = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT, SPECIAL>, NT, lds));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT, SPECIAL, RBM>, NT, lds));
     if (occ < 1) occ = 1;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cu * occ, nsrc));
     const int64_t nt = (int64_t)Q.tw * Q.th;
     HIPCHK(xg.alloc((size_t)blocks * 2 * nt));
     HIPCHK(queue.alloc((size_t)blocks * nt));
-    HIPCHK(list.alloc((size_t)blocks * nt * 64));
+    HIPCHK(list.alloc((size_t)blocks * nt * 64 * 2));
     DevBuf<uint16_t> hint;
     HIPCHK(hint.alloc((size_t)nt * 64));
     HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 2, ctx->stream));
@@ -980,7 +980,7 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
     if (const char* c = getenv("DMX_VGA_CHUNK")) P.chunk = std::max(1, atoi(c));
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-    hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
+    hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL, RBM>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(ctx->stream));   // hint freed on return
     *blocks_out = blocks;
@@ -1035,7 +1035,12 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     HIPCHK(d_hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));
     HIPCHK(d_nlev.alloc(std::max<int64_t>(N, 1)));
     Q.maxlev = maxlev; Q.hist_out = d_hist.p; Q.nlev_out = d_nlev.p; Q.stats = ctx->stats.p;
-    const size_t lds = (size_t)nt * 8 + (size_t)(th * ((tw + 63) / 64) + tw * ((th + 63) / 64)) * 8 + (size_t)VGA_HMAX * 4;
+    const size_t wr_ = (tw + 63) / 64, wc_ = (th + 63) / 64;
+    const size_t lds = (size_t)nt * 8 + (size_t)(th * wr_ + tw * wc_) * 8 + (size_t)VGA_HMAX * 4;
+    // line-resolved summaries when they fit next to the frontier bitmap (~1010^2 cells and below)
+    const size_t lds_rb = (size_t)nt * 8 + (size_t)(th * wr_ + th * 8 * wr_ + tw * 8 * wc_) * 8 + (size_t)VGA_HMAX * 4;
+    const char* rb_env = getenv("DMX_VGA_RB");
+    const bool rbm = !(rb_env && atoi(rb_env) == 0) && lds_rb + 1024 <= (size_t)160 * 1024;
     DevBuf<unsigned long long> xg;
     DevBuf<int4> queue;
     DevBuf<int32_t> list;
@@ -1044,13 +1049,18 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     (void)kt;
     if (nsrc > 0) {
         const bool sp = g->nspecial > 0;
+        const size_t L = rbm ? lds_rb : lds;
         if (nt <= 4096) {
-            rc = sp ? launch_tile<256, true>(ctx, Q, nsrc, lds, &blocks, xg, queue, list)
-                    : launch_tile<256, false>(ctx, Q, nsrc, lds, &blocks, xg, queue, list);
+            rc = sp ? (rbm ? launch_tile<256, true, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<256, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
+                    : (rbm ? launch_tile<256, false, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<256, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
             ntpb = 256;
         } else {
-            rc = sp ? launch_tile<1024, true>(ctx, Q, nsrc, lds, &blocks, xg, queue, list)
-                    : launch_tile<1024, false>(ctx, Q, nsrc, lds, &blocks, xg, queue, list);
+            rc = sp ? (rbm ? launch_tile<1024, true, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<1024, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
+                    : (rbm ? launch_tile<1024, false, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<1024, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
             ntpb = 1024;
         }
         if (rc) return rc;

@@ -63,7 +63,7 @@ struct VgaTileParams {
                               // none); shared by all workgroups: a stale value only costs one test
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
-    int32_t* list;            // per workgroup [nt*64]: hard cells / frontier cells
+    int32_t* list;            // per workgroup [2][nt*64]: hard cells / frontier cells, then phase-B2 cells
     int maxlev;
     int bext;                 // phase-B runs after the heads (BEXT_DEFAULT)
     int crk;                  // tile-common runs tested in phase A (<= CRK)
@@ -99,6 +99,17 @@ __device__ __forceinline__ void or_wg(unsigned long long* p, unsigned long long 
 }
 __device__ __forceinline__ void sync_global() { __syncthreads(); }
 
+// The n cells (x + i, y + dy*i) of a diagonal run that stay inside the tile of (x, y), as that
+// tile's bit mask (bit (y&7)*8 + (x&7)); n is bounded by the tile edges and the run's end xe.
+__device__ __forceinline__ unsigned long long diag_tile_mask(int x, int y, int dy, int xe, int& n) {
+    const int lx = x & 7, ly = y & 7;
+    n = min(min(8 - lx, dy > 0 ? 8 - ly : ly + 1), xe - x + 1);
+    const int b0 = ly * 8 + lx;
+    if (dy > 0) return (0x8040201008040201ull << b0) & (~0ull >> (63 - (b0 + 9 * (n - 1))));   // bits b0 + 9i
+    const int first = b0 - 7 * (n - 1);                                                        // bits b0 - 7i
+    const unsigned long long a = 0x0102040810204080ull;                                        // bits 7, 14, .., 56
+    return (first >= 7 ? (a << (first - 7)) : (a >> (7 - first))) & (~0ull << first) & (~0ull >> (63 - b0));
+}
 // OR all cells of run `ru` into the tiled bitmap `bm` (LDS or HBM, atomic).
 __device__ __forceinline__ void run_or(unsigned long long* bm, int tw, Run ru) {
     if (ru.y0 == ru.y1 && ru.x0 != ru.x1) {
@@ -115,9 +126,15 @@ __device__ __forceinline__ void run_or(unsigned long long* bm, int tw, Run ru) {
             or_wg(&bm[ty * tw + tx], col & (~0ull >> (8 * (7 - hi))) & (~0ull << (8 * lo)));
         }
     } else {
-        const int dy = (ru.y1 > ru.y0) ? 1 : ((ru.y1 < ru.y0) ? -1 : 0);
-        int y = ru.y0;
-        for (int x = ru.x0; x <= ru.x1; x++, y += dy) or_wg(&bm[(y >> 3) * tw + (x >> 3)], 1ull << ((y & 7) * 8 + (x & 7)));
+        const int dy = (ru.y1 > ru.y0) ? 1 : -1;
+        int x = ru.x0, y = ru.y0;
+        while (x <= ru.x1) {
+            int n;
+            const unsigned long long m = diag_tile_mask(x, y, dy, ru.x1, n);
+            or_wg(&bm[(y >> 3) * tw + (x >> 3)], m);
+            x += n;
+            y += dy * n;
+        }
     }
 }
 
@@ -132,10 +149,15 @@ struct FView {
     const unsigned long long* F;
     const unsigned long long* Fsr;
     const unsigned long long* Fsc;
+    const unsigned long long* RB;   // [th*8][wr]: bit tx of row y: tile (tx, y>>3) has a frontier cell in row y
+    const unsigned long long* CB;   // [tw*8][wc]: bit ty of column x: tile (x>>3, ty) has one in column x
     int tw, wr, wc;
 };
 // Tiles [t0, t1] of one summary line (bit per tile, <= 2 words: grids up to 1024 cells a side):
 // OR of F[base + tx * stride] & (cell mask of tile tx), 8 frontier tiles per round.
+#ifndef LH_COUNT
+#define LH_COUNT()
+#endif
 template <bool VERT>
 __device__ __forceinline__ bool line_hits(const unsigned long long* F, const unsigned long long* sum, int base, int stride,
                                           int t0, int t1, int a, int b, int sh) {
@@ -145,6 +167,7 @@ __device__ __forceinline__ bool line_hits(const unsigned long long* F, const uns
         if (w == w0) m &= ~0ull << (t0 & 63);
         if (w == w1) m &= ~0ull >> (63 - (t1 & 63));
         while (m) {
+            LH_COUNT();
             const int p = __ffsll((long long)m) - 1;
             unsigned long long acc = 0ull;
 #pragma unroll
@@ -164,7 +187,56 @@ __device__ __forceinline__ bool line_hits(const unsigned long long* F, const uns
     }
     return false;
 }
+// Diagonal run (Bin::make's single first-to-last span, ngraph.cpp:243-258): walked tile by tile;
+// the run's cells inside one 8x8 tile are a shifted (anti-)diagonal bit pattern, so a tile costs
+// one summary bit and at most one frontier word instead of up to 8 per-cell tests.
+__device__ __forceinline__ bool diag_hits(const FView& V, Run ru) {
+    const int dy = (ru.y1 > ru.y0) ? 1 : -1;
+    int x = ru.x0, y = ru.y0;
+    while (x <= ru.x1) {
+        int n;
+        const unsigned long long m = diag_tile_mask(x, y, dy, ru.x1, n);
+        const int tx = x >> 3, ty = y >> 3;
+        if (((V.Fsr[ty * V.wr + (tx >> 6)] >> (tx & 63)) & 1ull) && (V.F[ty * V.tw + tx] & m)) return true;
+        x += n;
+        y += dy * n;
+    }
+    return false;
+}
+
+// Line-resolved summaries (RB / CB): a run along one row (column) covers every cell of its interior
+// tiles in that row (column), so a summary bit there is a hit; only the two end tiles need their
+// frontier word.  At most 2 summary reads + 2 frontier reads per run (grids <= 1024 a side).
+__device__ __forceinline__ bool line_hits_rb(const unsigned long long* F, const unsigned long long* sum, int fbase, int fstride,
+                                             int t0, int t1, unsigned long long m_first, unsigned long long m_last) {
+    const int w0 = t0 >> 6, w1 = t1 >> 6;
+    unsigned long long a = sum[w0] & (~0ull << (t0 & 63));
+    unsigned long long b = 0ull;
+    if (w1 == w0) a &= ~0ull >> (63 - (t1 & 63));
+    else b = sum[w1] & (~0ull >> (63 - (t1 & 63)));
+    if (!(a | b)) return false;
+    const bool f0 = (a >> (t0 & 63)) & 1ull;
+    const bool f1 = ((w1 == w0 ? a : b) >> (t1 & 63)) & 1ull;
+    unsigned long long ia = a & ~(1ull << (t0 & 63)), ib = b;
+    if (w1 == w0) ia &= ~(1ull << (t1 & 63));
+    else ib &= ~(1ull << (t1 & 63));
+    if (ia | ib) return true;   // an interior tile: its whole row (column) segment is on the run
+    if (t0 == t1) return f0 && (F[fbase + t0 * fstride] & m_first & m_last);
+    return (f0 && (F[fbase + t0 * fstride] & m_first)) || (f1 && (F[fbase + t1 * fstride] & m_last));
+}
 __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
+    if (V.RB && ru.y0 == ru.y1) {
+        const int y = ru.y0, sh = (y & 7) * 8;
+        return line_hits_rb(V.F, V.RB + y * V.wr, (y >> 3) * V.tw, 1, ru.x0 >> 3, ru.x1 >> 3,
+                            (unsigned long long)((0xFFu << (ru.x0 & 7)) & 0xFFu) << sh,
+                            (unsigned long long)(0xFFu >> (7 - (ru.x1 & 7))) << sh);
+    }
+    if (V.RB && ru.x0 == ru.x1) {
+        const int x = ru.x0;
+        const unsigned long long colm = 0x0101010101010101ull << (x & 7);
+        return line_hits_rb(V.F, V.CB + x * V.wc, x >> 3, V.tw, ru.y0 >> 3, ru.y1 >> 3,
+                            colm & (~0ull << (8 * (ru.y0 & 7))), colm & (~0ull >> (8 * (7 - (ru.y1 & 7)))));
+    }
     if (ru.y0 == ru.y1) {   // horizontal (or a single cell): tile row ty, tiles x0>>3 .. x1>>3
         const int y = ru.y0, ty = y >> 3;
         return line_hits<false>(V.F, V.Fsr + ty * V.wr, ty * V.tw, 1, ru.x0 >> 3, ru.x1 >> 3, ru.x0 & 7, ru.x1 & 7,
@@ -172,20 +244,13 @@ __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
     } else if (ru.x0 == ru.x1) {   // vertical: tile column tx, tiles y0>>3 .. y1>>3
         const int x = ru.x0, tx = x >> 3;
         return line_hits<true>(V.F, V.Fsc + tx * V.wc, tx, V.tw, ru.y0 >> 3, ru.y1 >> 3, ru.y0 & 7, ru.y1 & 7, x & 7);
-    } else {                       // diagonal: cell by cell, skipping empty tiles
-        const int dy = (ru.y1 > ru.y0) ? 1 : -1;
-        int y = ru.y0;
-        for (int x = ru.x0; x <= ru.x1; x++, y += dy) {
-            const int tx = x >> 3, ty = y >> 3;
-            if (!((V.Fsr[ty * V.wr + (tx >> 6)] >> (tx & 63)) & 1ull)) continue;
-            if (V.F[ty * V.tw + tx] & (1ull << ((y & 7) * 8 + (x & 7)))) return true;
-        }
-        return false;
+    } else {
+        return diag_hits(V, ru);
     }
 }
 
 struct TileShared {
-    int src, qn, hn, item;
+    int src, qn, hn, item, bn;
     unsigned long long cnt, mass;
 };
 
@@ -273,24 +338,30 @@ __device__ __forceinline__ bool special_hit(const VgaTileParams& P, const FView&
 // V (visited) and X (next level) are per-workgroup bitmaps in HBM (they stay in the L2/MALL; a
 // source touches each word a few times), F (frontier, read by every run test) is in LDS.
 // SPECIAL = false: the graph has no asymmetric nodes (every U_f cell is regular), no exact path.
-template <int NT, bool SPECIAL>
+// RBM: line-resolved summaries RB / CB in LDS (replace Fsc; need ~32 KB more LDS, grids <= ~1010^2).
+template <int NT, bool SPECIAL, bool RBM>
 __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long F[];
     __shared__ TileShared S;
     constexpr int NW = NT / 64;
     const int nt = P.tw * P.th;
-    const int wr = (P.tw + 63) / 64, wc = (P.th + 63) / 64, nfs = P.th * wr + P.tw * wc;
+    const int wr = (P.tw + 63) / 64, wc = (P.th + 63) / 64;
+    const int nfs = RBM ? P.th * wr : P.th * wr + P.tw * wc;   // summary words rebuilt by atomics per level
     unsigned long long* Fsr = F + nt;           // [th][wr]
-    unsigned long long* Fsc = Fsr + P.th * wr;  // [tw][wc]
-    int* hist = (int*)(Fsc + P.tw * wc);
+    unsigned long long* Fsc = Fsr + P.th * wr;  // [tw][wc] (!RBM)
+    unsigned long long* RB = Fsr + P.th * wr;   // [th*8][wr] (RBM)
+    unsigned long long* CB = RB + P.th * 8 * wr; // [tw*8][wc] (RBM)
+    int* hist = (int*)(RBM ? (CB + P.tw * 8 * wc) : (Fsc + P.tw * wc));
     FView FV;
-    FV.F = F; FV.Fsr = Fsr; FV.Fsc = Fsc; FV.tw = P.tw; FV.wr = wr; FV.wc = wc;
+    FV.F = F; FV.Fsr = Fsr; FV.Fsc = RBM ? nullptr : Fsc; FV.tw = P.tw; FV.wr = wr; FV.wc = wc;
+    FV.RB = RBM ? RB : nullptr;
+    FV.CB = RBM ? CB : nullptr;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int tw = P.tw, rows = P.rows;
     unsigned long long* Vg = P.xg + (size_t)blockIdx.x * 2 * nt;
     unsigned long long* Xg = Vg + nt;
     int4* Q = P.queue + (size_t)blockIdx.x * nt;
-    int32_t* L = P.list + (size_t)blockIdx.x * nt * 64;
+    int32_t* L = P.list + (size_t)blockIdx.x * nt * 64 * 2;
     const size_t hstride = (size_t)nt * 64;
     // work counters live in LDS (flushed to P.stats at exit) so they cost no registers: a 1024-thread
     // workgroup has 128 VGPRs a lane and every spill is a scratch round trip
@@ -301,7 +372,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
     for (int i = tid; i < 32; i += NT) SC[i] = 0ull;
 
     uint16_t* Hn = P.hint;
-    if (tid == 0) { S.qn = 0; S.hn = 0; S.item = 0; S.cnt = 0; S.mass = 0; S.src = -1; }
+    if (tid == 0) { S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.cnt = 0; S.mass = 0; S.src = -1; }
     int64_t chunk_end = 0;
     int64_t src = -1;
     for (;;) {
@@ -390,58 +461,77 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 sync_global();
                 if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(9, n - tmark); tmark = n; }
                 const int qn = S.qn;
-                // ---- B: head runs, one wave per queued tile, lane = cell
-                for (int it = wave; it < qn; it += NW) {
-                    const int4 e = Q[it];
-                    const int t = e.x;
-                    unsigned long long mask = (unsigned long long)(unsigned)e.z | ((unsigned long long)(unsigned)e.w << 32);
-                    bool hit = false, to_hard = false;
-                    int hard_val = 0;
-                    if (lane == 0) { ST(18, 1); ST(19, __popcll(mask)); }
-                    // every load that depends only on (t, lane) is issued up front, so the tile costs
-                    // about two memory round trips before the LDS tests instead of one per decision
-                    const unsigned long long reg = P.regular_tiles[t];
-                    const int id = (t << 6) | lane;
-                    const bool mine = (mask >> lane) & 1ull;
-                    const bool lane_reg = !SPECIAL || ((reg >> lane) & 1ull);
-                    int64_t ss = 0;
-                    int nr = 0, hp = 0xFFFF;
-                    constexpr int KH0 = 4;   // heads preloaded with the TT row (register budget)
-                    Run hd[KH0];
-                    if (mine && lane_reg) {
-                        ss = P.tscan_start[id];
-                        nr = P.tnruns[id];
-                        hp = Hn[id];
+                // ---- B1: tile-to-tile certain test, a wave per queued tile, 4 tiles per step (their
+                // TT rows in flight together); the cells of tiles it does not resolve go to B2
+                int32_t* LB = L + (size_t)nt * 64;
+                for (int it0 = wave * 4; it0 < qn; it0 += NW * 4) {
+                    int4 e[4];
 #pragma unroll
-                        for (int r = 0; r < KH0; r++) hd[r] = P.heads[r * hstride + id];
-                    }
+                    for (int j = 0; j < 4; j++) e[j] = (it0 + j < qn) ? Q[it0 + j] : make_int4(-1, 0, 0, 0);
+                    unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
                     if (P.ttvis) {
-                        // a frontier tile that every regular cell of t sees completely: all of t's
-                        // unvisited regular cells are at the next level (tvw <= 256: 4 words a lane)
-                        const unsigned long long* tt = P.ttvis + (size_t)t * P.tvw;
-                        unsigned long long acc = 0ull;
 #pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const int w = j * 64 + lane;
-                            if (w < P.tvw) acc |= tt[w] & Fsr[w];
+                        for (int k = 0; k < 4; k++) {
+                            const int w = k * 64 + lane;
+                            if (w < P.tvw) {
+                                const unsigned long long fs = Fsr[w];
+#pragma unroll
+                                for (int j = 0; j < 4; j++)
+                                    if (e[j].x >= 0) acc[j] |= P.ttvis[(size_t)e[j].x * P.tvw + w] & fs;
+                            }
                         }
-                        if (__ballot(acc != 0ull) != 0ull) {
+                    }
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const int t = e[j].x;
+                        if (t < 0) break;
+                        unsigned long long mask = (unsigned long long)(unsigned)e[j].z | ((unsigned long long)(unsigned)e[j].w << 32);
+                        const unsigned long long reg = P.regular_tiles[t];
+                        if (lane == 0) { ST(18, 1); ST(19, __popcll(mask)); }
+                        if (__ballot(acc[j] != 0ull) != 0ull) {
+                            // a frontier tile every regular cell of t sees completely
                             const unsigned long long R = mask & reg;
                             if (lane == 0) { or_wg(&Xg[t], R); ST(20, 1); }
                             mask &= ~R;
                         }
+                        const bool mine = (mask >> lane) & 1ull;
+                        const unsigned long long bm = __ballot(mine);
+                        if (bm) {
+                            int base = 0;
+                            if (lane == 0) base = atomicAdd(&S.bn, __popcll(bm));
+                            base = __shfl(base, 0);
+                            const int id = (t << 6) | lane;
+                            const bool lreg = !SPECIAL || ((reg >> lane) & 1ull);
+                            if (mine) LB[base + __popcll(bm & ((1ull << lane) - 1ull))] = lreg ? id : (-1 - id);
+                        }
                     }
-                    if ((mask >> lane) & 1ull) {
-                        if (!lane_reg) {
+                }
+                sync_global();
+                const int bn = S.bn;
+                // ---- B2: per cell (lane = cell, full waves): the hint run, the heads, then the next
+                // bext runs of the scan order; misses go to the hard list
+                for (int b0 = wave * 64; b0 < bn; b0 += NW * 64) {
+                    const int i = b0 + lane;
+                    bool hit = false, to_hard = false;
+                    int hard_val = 0;
+                    if (i < bn) {
+                        const int v = LB[i];
+                        if (v < 0) {
                             to_hard = true;
-                            hard_val = -1 - id;   // special node: exact path
+                            hard_val = v;   // special node: exact path
                         } else {
+                            const int id = v;
+                            const int64_t ss = P.tscan_start[id];
+                            const int nr = P.tnruns[id];
+                            const int hp = Hn[id];
+                            constexpr int KH0 = 4;
+                            Run hd[KH0];
+#pragma unroll
+                            for (int r = 0; r < KH0; r++) hd[r] = P.heads[r * hstride + id];
                             if (hp >= KH && hp < nr) {   // the run that hit for a recent source
                                 rt++;
                                 hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
                             }
-                            // heads (already in registers), then the next runs of the scan order on
-                            // this lane, 4 loads in flight per batch
 #pragma unroll 1
                             for (int r = 0; r < KH0; r++)
                                 if (!hit && r < nr) {
@@ -468,14 +558,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                                 rt += (unsigned)min(4, lim - base);
                                 if (fj >= 0) { hit = true; if (hp != base + fj) Hn[id] = (uint16_t)(base + fj); }
                             }
-                            if (!hit) {
-                                if (nr > KH + P.bext) { to_hard = true; hard_val = id; }
-                                else { ST(5, 1); ST(6, nr); }
-                            }
+                            if (hit) or_wg(&Xg[id >> 6], 1ull << (id & 63));
+                            else if (nr > KH + P.bext) { to_hard = true; hard_val = id; }
+                            else { ST(5, 1); ST(6, nr); }
                         }
                     }
-                    const unsigned long long hm = __ballot(hit);
-                    if (lane == 0 && hm) or_wg(&Xg[t], hm);
                     const unsigned long long hw = __ballot(to_hard);
                     if (hw) {
                         int base = 0;
@@ -633,7 +720,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     if (x) {
                         const int tx = t % tw, ty = t / tw;
                         atomicOr(&Fsr[ty * wr + (tx >> 6)], 1ull << (tx & 63));
-                        atomicOr(&Fsc[tx * wc + (ty >> 6)], 1ull << (ty & 63));
+                        if (!RBM) atomicOr(&Fsc[tx * wc + (ty >> 6)], 1ull << (ty & 63));
                     }
                 }
                 F[t] = x;
@@ -643,11 +730,32 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 m_loc += __shfl_xor(m_loc, off);
             }
             if (lane == 0 && c_loc) { atomicAdd(&S.cnt, c_loc); atomicAdd(&S.mass, m_loc); }
+            if (RBM) {
+                // line-resolved summaries from the published frontier (plain stores, no atomics)
+                __syncthreads();
+                const int th = P.th;
+                for (int i = tid; i < th * 8 * wr; i += NT) {
+                    const int w = i % wr, r = (i / wr) & 7, ty = i / (8 * wr);
+                    const unsigned long long* fr = F + ty * tw + w * 64;
+                    const int n = min(64, tw - w * 64);
+                    unsigned long long bits = 0ull;
+                    for (int j = 0; j < n; j++) bits |= (unsigned long long)(((fr[j] >> (8 * r)) & 0xFFull) != 0ull) << j;
+                    RB[(ty * 8 + r) * wr + w] = bits;
+                }
+                for (int i = tid; i < tw * 8 * wc; i += NT) {
+                    const int w = i % wc, c = (i / wc) & 7, tx = i / (8 * wc);
+                    const unsigned long long cm = 0x0101010101010101ull << c;
+                    const int n = min(64, th - w * 64);
+                    unsigned long long bits = 0ull;
+                    for (int j = 0; j < n; j++) bits |= (unsigned long long)((F[(w * 64 + j) * tw + tx] & cm) != 0ull) << j;
+                    CB[(tx * 8 + c) * wc + w] = bits;
+                }
+            }
             sync_global();
             const long long cnt = (long long)S.cnt, mass = (long long)S.mass;
             if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(12, n - tmark); tmark = n; }
             __syncthreads();
-            if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; }
+            if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; }
             if (cnt == 0) break;
             if (level + 1 >= VGA_HMAX) { overflow = true; break; }
             if (tid == 0) hist[level + 1] = (int)cnt;

@@ -29,13 +29,19 @@ t0 = time.time()
 g.vga_visual_global(src_begin=b, src_end=b + 1)   # prep (uf, symmetry, tiles)
 print(json.dumps({"prep_wall_s": time.time() - t0}), flush=True)
 configs = [c.split("=") for c in (sys.argv[4:] if len(sys.argv) > 4 else ["DMX_VGA_CHUNK=1"])]
+ref_out = None
 for k, v in configs:
     os.environ[k] = v
     out = g.vga_visual_global(src_begin=b, src_end=e)
+    same = None
+    if ref_out is None:
+        ref_out = out.copy()
+    else:
+        same = bool((out.view("u4") == ref_out.view("u4")).all())
     st = ctx.last_stats()
     nsrc = e - b
     tk = ctx.last_timing()[1]
-    print(json.dumps({"config": "%s=%s" % (k, v), "vga_sources": nsrc, "vga_kernel_s": tk,
+    print(json.dumps({"config": "%s=%s" % (k, v), "same_as_first": same, "vga_sources": nsrc, "vga_kernel_s": tk,
                       "vga_s_per_source": tk / nsrc, "est_full_vga_s": tk / nsrc * N,
                       "runs_read_per_src": st["vga_runs_expanded"] / nsrc,
                       "fail_cells_per_src": st["vga_fail_cells"] / nsrc,
