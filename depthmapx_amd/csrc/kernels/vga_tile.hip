@@ -874,13 +874,19 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int t
                 }
             } else {
                 const int dy = (ru.y1 > ru.y0) ? 1 : -1;
-                int y = ru.y0;
-                for (int x = ru.x0; x <= ru.x1; x++, y += dy) {
-                    atomicOr(&row[(y >> 3) * wr + (x >> 6 >> 3)], 1ull << ((x >> 3) & 63));
+                int x = ru.x0, y = ru.y0;
+                while (x <= ru.x1) {
+                    int n;
+                    const unsigned long long m = diag_tile_mask(x, y, dy, ru.x1, n);
+                    const int tx = x >> 3, ty = y >> 3;
+                    atomicOr(&row[ty * wr + (tx >> 6)], 1ull << (tx & 63));
                     if (ftvis) {
-                        const int t = (y >> 3) * tw + (x >> 3);
-                        if (!((seed_tiles[t] >> ((y & 7) * 8 + (x & 7))) & 1ull)) tv_count(cnt, t, 1);
+                        const int t = ty * tw + tx;
+                        const int c = __popcll(m & ~seed_tiles[t]);
+                        if (c) tv_count(cnt, t, c);
                     }
+                    x += n;
+                    y += dy * n;
                 }
             }
         }
