@@ -1,6 +1,6 @@
 // dmxcli -- command-line front-end of the MI355X engine with the depthmapXcli mode-parser surface
 // for the accelerated path: VISPREP (grid, fill, makeGraph), VGA (-vm visibility -vg -vr) and
-// STEPDEPTH (-sdt metric).  Flags, validation messages, the "-t" timing CSV and the exit status
+// STEPDEPTH (-sdt metric, -sdt visual).  Flags, validation messages, the "-t" timing CSV and the exit status
 // follow the reference CLI:
 //   depthmapXcli/main.cpp:22-54, commandlineparser.cpp:51-142, visprepparser.cpp:26-172,
 //   vgaparser.cpp:29-106, radiusconverter.cpp:24-61, stepdepthparser.cpp:26-100,
@@ -586,16 +586,28 @@ struct StepDepth : Mode {
             sel.push_back(x * rows + y);
         }
         std::cout << "ok\nCalculating step-depth... " << std::flush;
-        if (type != METRIC) throw RuntimeException("Only -sdt metric is part of the accelerated path");
+        if (type == ANGULAR) throw RuntimeException("Only -sdt metric and -sdt visual are part of the accelerated path");
         std::vector<float> out((size_t)m.nnodes * 3, -1.0f);
         int rc = DMX_OK;
-        timed(perf, "Calculating step-depth",
-              [&] { rc = dmx_metric_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data()); });
+        timed(perf, "Calculating step-depth", [&] {
+            rc = type == METRIC ? dmx_metric_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data())
+                                : dmx_visual_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data());
+        });
         if (rc != DMX_OK && rc != DMX_ERR_STATE) check(rc);   // no selection: analyseGraph returns false
         std::cout << " ok\nWriting out result..." << std::flush;
         timed(perf, "Writing graph", [&] {
             int displayed = -1;
-            if (rc == DMX_OK) {
+            if (rc == DMX_OK && type == VISUAL) {
+                // VGAVisualGlobalDepth::run: one column, reset to -1, set on every reached cell
+                // (vgavisualglobaldepth.cpp:28, :49)
+                Column c;
+                c.name = "Visual Step Depth";
+                c.values.assign(out.begin(), out.begin() + m.nnodes);
+                c.set.resize((size_t)m.nnodes);
+                for (int64_t k = 0; k < m.nnodes; k++) c.set[k] = out[k] >= 0.0f ? 1 : 0;
+                displayed = (int)m.columns.size();
+                m.columns.push_back(c);
+            } else if (rc == DMX_OK) {
                 // VGAMetricDepth::run column order (vgametricdepth.cpp:27-33); cells it never pops keep -1
                 const bool single = [&] {   // PointMap::setCurSel keeps FILLED cells only
                     std::vector<int32_t> st((size_t)cols * rows);
@@ -635,7 +647,7 @@ void print_help() {
                  "Modes (the accelerated depthmapXcli path):\n"
                  "  VISPREP   -pg <grid spacing> -pp <x,y> | -pf <points file> [-pr <max visibility>] [-pb] [-pm]\n"
                  "  VGA       -vm visibility -vg -vr <radius|n>\n"
-                 "  STEPDEPTH -sdt metric -sdp <x,y> | -sdf <points file>\n"
+                 "  STEPDEPTH -sdt metric|visual -sdp <x,y> | -sdf <points file>\n"
                  "Input: a CSV drawing (x1,y1,x2,y2) or a .dmxg written by this tool; output: .dmxg\n";
 }
 

@@ -988,7 +988,8 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
 }
 
 static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
-                         bool out_on_device, int64_t* levels, int tw, int th) {
+                         bool out_on_device, int64_t* levels, int tw, int th, const int32_t* d_seeds = nullptr,
+                         int nseeds = 0, int32_t* d_cell_level = nullptr) {
     int rc = prepare_tiles(g);
     if (rc) return rc;
     PointMapHost& h = *g->pm->host;
@@ -1023,6 +1024,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.missing = corr ? g->missing.p : nullptr;
     Q.src_begin = sb; Q.src_end = se; Q.radius = (int)radius; Q.gates_only = gates_only;
     Q.uf_count = g->uf_count;
+    Q.seeds = d_seeds; Q.nseeds = nseeds; Q.cell_level = d_cell_level;
     // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
     Q.alpha = 60;   // top-down costs a frontier cell its whole run list (~R/N runs): keep it rare
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
@@ -1064,9 +1066,11 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
             ntpb = 1024;
         }
         if (rc) return rc;
-        hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsrc + 255) / 256)), dim3(256), 0, ctx->stream, sb, se,
-                           d_hist.p, d_nlev.p, outp, levels ? d_lv.p : nullptr, ctx->stats.p);
-        HIPCHK(hipGetLastError());
+        if (nseeds == 0) {
+            hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsrc + 255) / 256)), dim3(256), 0, ctx->stream, sb,
+                               se, d_hist.p, d_nlev.p, outp, levels ? d_lv.p : nullptr, ctx->stats.p);
+            HIPCHK(hipGetLastError());
+        }
         HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
     } else {
         HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
@@ -1106,6 +1110,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[15] = (long long)st[15];                          // runs scanned in phase C
     ctx->last_stats[16] = (long long)st[1];                           // phase-C cells that hit
     ctx->last_stats[17] = (long long)st[14];                          // phase-C cells (regular)
+    if (nseeds > 0) return DMX_OK;
     if (!out_on_device && nsrc > 0)
         HIPCHK(hipMemcpy(out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
     if (levels && nsrc > 0)
@@ -1333,6 +1338,66 @@ int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
 int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {
     if (!ctx || !out5) return fail(DMX_ERR_ARG, "bad arguments");
     for (int i = 0; i < 5; i++) out5[i] = ctx->phase_cycles[i];
+    return DMX_OK;
+}
+
+// STEPDEPTH -sdt visual: MetaGraph::analyseGraph(point_depth_selection = 1) -> VGAVisualGlobalDepth::run
+// (depthmapXcli/runmethods.cpp:767-769, salalib/vgamodules/vgavisualglobaldepth.cpp:23-77).  One
+// breadth-first search from every selected filled cell at once (level 0, always expanded); cells are
+// discovered through run membership (Bin::extractUnseen, ngraph.cpp:308-326: set semantics, the
+// extent short-cut only skips already-covered suffixes); contextfilled odd cells get their level but
+// are not expanded.  Runs on the tile-resolved BFS in seed mode (one workgroup).
+int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
+    if (g->node_begin != 0 || g->node_end != g->nnodes)
+        return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
+    HIPCHK(hipSetDevice(ctx->device));
+    PointMapHost& h = *g->pm->host;
+    const int cols = h.cols(), rows = h.rows();
+    const int64_t C = (int64_t)cols * rows, N = g->nnodes;
+    for (int64_t k = 0; k < N; k++) out[k] = -1.0f;
+    const auto& st = h.state();
+    std::vector<int32_t> seeds;   // nodes, selection order = std::set<int> PixelRef order, unique
+    {
+        std::vector<int32_t> sel;
+        for (int64_t i = 0; i < nsel; i++) {
+            const int32_t c = sel_cells[i];
+            if (c < 0 || c >= C) return fail(DMX_ERR_ARG, "selected cell outside the grid");
+            if (st[c] & CELL_FILLED) sel.push_back(c);
+        }
+        std::sort(sel.begin(), sel.end());
+        sel.erase(std::unique(sel.begin(), sel.end()), sel.end());
+        const auto& nc = g->pm->node_cell;   // ascending x-major cell index = node order
+        for (int32_t c : sel) {
+            const auto it = std::lower_bound(nc.begin(), nc.end(), c);
+            if (it != nc.end() && *it == c) seeds.push_back((int32_t)(it - nc.begin()));
+        }
+    }
+    if (seeds.empty()) return fail(DMX_ERR_STATE, "no filled cell selected");
+    int rc = prepare_uf(g);
+    if (rc) return rc;
+    rc = prepare_symmetry(g);
+    if (rc) return rc;
+    const int tw = (cols + 7) / 8, th = (rows + 7) / 8, nt = tw * th;
+    if (g->symmetric != 1 || nt > 16 * 1024)
+        return fail(DMX_ERR_UNSUPPORTED, "visual step depth needs the tile-resolved BFS (grid <= 1024^2, symmetric graph)");
+    DevBuf<int32_t> d_seeds, d_level;
+    HIPCHK(d_seeds.alloc(seeds.size()));
+    HIPCHK(d_level.alloc((size_t)nt * 64));
+    HIPCHK(hipMemcpyAsync(d_seeds.p, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemsetAsync(d_level.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
+    std::vector<float> dummy(7);
+    rc = vga_tile_impl(ctx, g, -1.0, 0, 0, 1, dummy.data(), false, nullptr, tw, th, d_seeds.p, (int)seeds.size(), d_level.p);
+    if (rc) return rc;
+    std::vector<int32_t> lv((size_t)nt * 64);
+    HIPCHK(hipMemcpy(lv.data(), d_level.p, lv.size() * 4, hipMemcpyDeviceToHost));
+    for (int64_t k = 0; k < N; k++) {
+        const int c = g->pm->node_cell[k];
+        const int x = c / rows, y = c % rows;
+        const int v = lv[(size_t)((((y >> 3) * tw + (x >> 3)) << 6) | ((y & 7) << 3) | (x & 7))];
+        if (v >= 0) out[k] = (float)v;
+    }
+    for (int32_t k : seeds) out[k] = 0.0f;
     return DMX_OK;
 }
 

@@ -65,6 +65,12 @@ struct VgaTileParams {
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
     int32_t* list;            // per workgroup [2][nt*64]: hard cells / frontier cells, then phase-B2 cells
     int maxlev;
+    // seed mode (visual step depth, vgavisualglobaldepth.cpp:23-77): one BFS from nseeds seed nodes
+    // (level 0, always expanded); contextfilled odd cells are never expanded at later levels;
+    // cell_level[tile id] receives the level of every cell reached (launch one source, one block)
+    const int32_t* seeds;
+    int nseeds;
+    int32_t* cell_level;
     int bext;                 // phase-B runs after the heads (BEXT_DEFAULT)
     int crk;                  // tile-common runs tested in phase A (<= CRK)
     int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
@@ -388,10 +394,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             src++;
         }
         if (src >= P.src_end) break;
-        const int scell = P.node_cell[src];
+        const bool seeded = P.nseeds > 0;
+        const int scell = P.node_cell[seeded ? P.seeds[0] : src];
         const int sx = scell / rows, sy = scell % rows;
         // VGAVisualGlobal::run: context-filled odd sources and gates_only are skipped (:72-75)
-        if (((P.node_flags[src] & 1) && !((sx % 2) == 0 && (sy % 2) == 0)) || P.gates_only) {
+        if (!seeded && (((P.node_flags[src] & 1) && !((sx % 2) == 0 && (sy % 2) == 0)) || P.gates_only)) {
             if (tid == 0) P.nlev_out[src] = 0;
             continue;
         }
@@ -403,24 +410,43 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             F[t] = 0ull;
         }
         for (int i = tid; i < VGA_HMAX; i += NT) hist[i] = 0;
-        const bool s_in_uf = !(P.seed_tiles[stile] & sbit);
-        const long long target = P.uf_count - (s_in_uf ? 1 : 0);
-        long long m_f = 1, m_u = target, discovered = 0;
+        long long n_in_uf = (P.seed_tiles[stile] & sbit) ? 0 : 1;
+        if (seeded) {
+            // every seed is visited at level 0; count those inside U_f for the early exit
+            __syncthreads();
+            for (int i = tid; i < P.nseeds; i += NT) {
+                const int c = P.node_cell[P.seeds[i]];
+                const int x = c / rows, y = c % rows;
+                const int t = (y >> 3) * tw + (x >> 3);
+                const unsigned long long b = 1ull << ((y & 7) * 8 + (x & 7));
+                if (!(P.seed_tiles[t] & b) && !(t == stile && b == sbit)) atomicAdd(&S.cnt, 1ull);   // seeds[0] counted above
+                or_wg(&Vg[t], b);
+            }
+            __syncthreads();
+            n_in_uf += (long long)S.cnt;
+            __syncthreads();
+            if (tid == 0) S.cnt = 0;
+        }
+        const long long target = P.uf_count - n_in_uf;
+        long long m_f = seeded ? P.nseeds : 1, m_u = target, discovered = 0;
         int level = 0, nlev = 1;
         bool overflow = false;
         __syncthreads();
-        if (tid == 0) hist[0] = 1;
+        if (tid == 0) hist[0] = seeded ? P.nseeds : 1;
         for (;;) {
             if (P.radius != -1 && level >= P.radius) break;
             if (discovered >= target) break;
             const bool bottom_up = level > 0 && (m_f * (long long)P.alpha > m_u);
             tmark = __builtin_amdgcn_s_memtime();
             if (level == 0) {
-                // ---- level 1: rasterise the source's runs (top-down from {s})
-                const int64_t rs = P.node_run_start[src];
-                const int nr = P.node_nruns[src];
-                for (int r = tid; r < nr; r += NT) run_or(F, tw, P.pool[rs + r]);
-                if (tid < nr) rt += (unsigned)((nr - tid + NT - 1) / NT);
+                // ---- level 1: rasterise the source's runs (top-down from {s}, or from every seed)
+                for (int i = 0; i < (seeded ? P.nseeds : 1); i++) {
+                    const int64_t sn = seeded ? P.seeds[i] : src;
+                    const int64_t rs = P.node_run_start[sn];
+                    const int nr = P.node_nruns[sn];
+                    for (int r = tid; r < nr; r += NT) run_or(F, tw, P.pool[rs + r]);
+                    if (tid < nr) rt += (unsigned)((nr - tid + NT - 1) / NT);
+                }
                 sync_global();
                 for (int t = tid; t < nt; t += NT) Xg[t] = F[t] & ~Vg[t];
                 if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(8, n - tmark); tmark = n; }
@@ -715,7 +741,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     c_loc += (unsigned long long)__popcll(x);
                     Vg[t] |= x;
                     Xg[t] = 0ull;
-                    if (P.radius != -1) x &= ~P.nonexp_tiles[t];
+                    if (P.cell_level)
+                        for (unsigned long long m = x; m; m &= m - 1) P.cell_level[t * 64 + __ffsll((long long)m) - 1] = level + 1;
+                    // VGA global expands every cell when radius == n (vgavisualglobal.cpp:98-104);
+                    // step depth never expands contextfilled odd cells (vgavisualglobaldepth.cpp:53)
+                    if (P.radius != -1 || seeded) x &= ~P.nonexp_tiles[t];
                     m_loc += (unsigned long long)__popcll(x);
                     if (x) {
                         const int tx = t % tw, ty = t / tw;

@@ -218,6 +218,22 @@ class Graph:
         N.check(N.lib().dmx_metric_stepdepth(self.ctx.h, self.h, N.ptr(arr), len(arr), N.ptr(out)))
         return out
 
+    def visual_step_depth(self, points=None, cells=None):
+        """STEPDEPTH -sdt visual (dm_runmethods::runStepDepth, depthmapXcli/runmethods.cpp:767-769):
+        select the cell under each point, then VGAVisualGlobalDepth::run
+        (salalib/vgamodules/vgavisualglobaldepth.cpp:23-77) on the GPU.  Returns [N] float32
+        "Visual Step Depth" (-1: not reached)."""
+        sel = [] if cells is None else [int(c) for c in cells]
+        for (x, y) in (points or []):
+            if not self.pm.region_contains(x, y):
+                raise N.DmxError(-6, "Point outside of target region")
+            sel.append(self.pm.pixelate(x, y))
+        arr = np.ascontiguousarray(sel, dtype=np.int32)
+        n = self.info()["nnodes"]
+        out = np.full(n, -1.0, dtype=np.float32)
+        N.check(N.lib().dmx_visual_stepdepth(self.ctx.h, self.h, N.ptr(arr), len(arr), N.ptr(out)))
+        return out
+
     def vga_visual_global_device(self, out_dev_ptr, radius=-1.0, gates_only=False, src_begin=0, src_end=-1):
         N.check(N.lib().dmx_vga_global_device(self.ctx.h, self.h, float(radius), int(bool(gates_only)),
                                               int(src_begin), int(src_end), ctypes.c_void_p(out_dev_ptr)))

@@ -130,6 +130,13 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
  * Metric Straight-Line Distance (single selected cell only, else -1); unreached cells -1.
  * DMX_ERR_STATE if no filled cell is selected (the reference then skips the analysis). */
 int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out);
+/* ---- VGA visual step depth (GPU) ----------------------------------------------------------- */
+/* dm_runmethods::runStepDepth with -sdt visual -> MetaGraph::analyseGraph(point_depth_selection=1)
+ * -> VGAVisualGlobalDepth::run (depthmapXcli/runmethods.cpp:767-769, salalib/mgraph.cpp:312-314,
+ * vgamodules/vgavisualglobaldepth.cpp:23-77).  sel_cells as for dmx_metric_stepdepth.  out: host
+ * [N] "Visual Step Depth" in node order (unreached cells -1).  DMX_ERR_STATE if no filled cell is
+ * selected; DMX_ERR_UNSUPPORTED for grids above 1024^2 or graphs too asymmetric for the tile BFS. */
+int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out);
 /* Kernel time of the last step-depth call, expanders popped, cells relaxed. */
 int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_popped, int64_t* cells_relaxed);
 

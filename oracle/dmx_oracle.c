@@ -1108,3 +1108,48 @@ int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
     free(ins); free(h.a); free(mdist); free(cum); free(misc);
     return 0;
 }
+
+/* VGAVisualGlobalDepth::run (salalib/vgamodules/vgavisualglobaldepth.cpp:23-77) with
+ * Node::extractUnseen -> Bin::extractUnseen (ngraph.cpp:60-65, :308-326): one search tree from the
+ * whole selection (std::set<int> PixelRef order), each level walked in reverse; Point::m_misc and
+ * m_extent are reset for the attribute rows (filled cells) only (:31-35) -- every other point keeps
+ * its freshly loaded state (misc 0, extent PixelRef() = (-1, -1), point.h:67). */
+int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out) {
+    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
+    for (int64_t i = 0; i < N; i++) out[i] = -1.0f;
+    if (nsel <= 0) return -1;
+    int32_t* miscs = (int32_t*)calloc(C, sizeof(int32_t));
+    int16_t* extx = (int16_t*)malloc(C * sizeof(int16_t));
+    int16_t* exty = (int16_t*)malloc(C * sizeof(int16_t));
+    for (int x = 0; x < m->cols; x++)
+        for (int y = 0; y < m->rows; y++) {
+            const int64_t idx = (int64_t)x + (int64_t)y * m->cols;
+            const int filled = (m->state[cidx(m, x, y)] & ST_FILLED) != 0;
+            extx[idx] = (int16_t)(filled ? x : -1);
+            exty[idx] = (int16_t)(filled ? y : -1);
+        }
+    Vec cur = {0, 0, 0}, next = {0, 0, 0};
+    for (int64_t i = 0; i < nsel; i++) {
+        Pix* p = (Pix*)vec_push(&cur, sizeof(Pix));
+        p->x = sel_cells[i] / m->rows;
+        p->y = sel_cells[i] % m->rows;
+    }
+    int level = 0;
+    while (cur.n) {
+        next.n = 0;
+        for (int64_t i = cur.n - 1; i >= 0; i--) {
+            const Pix pc = ((Pix*)cur.p)[i];
+            const int64_t cc = cidx(m, pc.x, pc.y), idx = (int64_t)pc.x + (int64_t)pc.y * m->cols;
+            if ((m->state[cc] & ST_FILLED) && miscs[idx] != ~0) {
+                out[m->node_of_cell[cc]] = (float)level;
+                if (!(m->state[cc] & ST_CONTEXTFILLED) || (pc.x % 2 == 0 && pc.y % 2 == 0) || level == 0)
+                    extract_unseen(m, &m->nodes[m->node_of_cell[cc]], &next, miscs, extx, exty);
+                miscs[idx] = ~0;
+            }
+        }
+        Vec t = cur; cur = next; next = t;
+        level++;
+    }
+    free(cur.p); free(next.p); free(miscs); free(extx); free(exty);
+    return 0;
+}

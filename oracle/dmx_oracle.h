@@ -59,6 +59,8 @@ int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t node_beg
  * Angle, Metric Step Shortest-Path Length, Metric Straight-Line Distance (single selection only;
  * otherwise -1); unreached cells keep -1.  Returns -1 for an empty selection. */
 int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
+/* VGAVisualGlobalDepth::run (vgamodules/vgavisualglobaldepth.cpp:23-77): out [N], -1 unreached. */
+int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
 
 #ifdef __cplusplus
 }

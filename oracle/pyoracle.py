@@ -46,6 +46,8 @@ def lib():
         L.dmxo_set_graph.argtypes = [vp, vp, vp, i64]
         L.dmxo_metric_stepdepth.restype = i32
         L.dmxo_metric_stepdepth.argtypes = [vp, vp, i64, vp]
+        L.dmxo_visual_stepdepth.restype = i32
+        L.dmxo_visual_stepdepth.argtypes = [vp, vp, i64, vp]
         L.dmxo_vga_global.restype = i32
         L.dmxo_vga_global.argtypes = [vp, dbl, i32, i64, i64, i32, vp, vp]
         _lib = L
@@ -128,4 +130,12 @@ class OracleMap:
         sel = np.ascontiguousarray(sel_cells, dtype=np.int32)
         out = np.full((self.num_nodes, 3), -1.0, dtype=np.float32)
         lib().dmxo_metric_stepdepth(self.h, _p(sel), len(sel), _p(out))
+        return out
+
+    def visual_stepdepth(self, sel_cells):
+        """VGAVisualGlobalDepth::run from x-major cell indices of the (filled) selection, in
+        std::set<int> PixelRef order.  [N] Visual Step Depth, -1 where not reached."""
+        sel = np.ascontiguousarray(sel_cells, dtype=np.int32)
+        out = np.full(self.num_nodes, -1.0, dtype=np.float32)
+        lib().dmxo_visual_stepdepth(self.h, _p(sel), len(sel), _p(out))
         return out

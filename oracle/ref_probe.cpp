@@ -213,7 +213,7 @@ int main(int argc, char** argv) {
     dump(outDir + "/runs.bin", runs);
     dump(outDir + "/gridconn.bin", gconn);
 
-    double tsd = 0;
+    double tsd = 0, tvsd = 0;
     if (!stepPoints.empty()) {
         // dm_runmethods::runStepDepth (depthmapXcli/runmethods.cpp:735-778), metric step type
         for (auto& p : stepPoints) {
@@ -238,6 +238,18 @@ int main(int argc, char** argv) {
         for (auto it = at.begin(); it != at.end(); ++it)
             for (int c : cols3) sd.push_back(c >= 0 ? it->getRow().getValue(c) : -1.0f);
         dump(outDir + "/stepdepth.bin", sd);
+        // the same selection, -sdt visual (runmethods.cpp:767-769 -> VGAVisualGlobalDepth::run)
+        Options vopt;
+        vopt.global = 0;
+        vopt.point_depth_selection = 1;
+        a = std::chrono::steady_clock::now();
+        bool vdone = mg.analyseGraph(nullptr, vopt, false);
+        b = std::chrono::steady_clock::now();
+        tvsd = std::chrono::duration<double>(b - a).count();
+        std::vector<float> vsd;
+        const int vcol = vdone && at.hasColumn("Visual Step Depth") ? (int)at.getColumnIndex("Visual Step Depth") : -1;
+        for (auto it = at.begin(); it != at.end(); ++it) vsd.push_back(vcol >= 0 ? it->getRow().getValue(vcol) : -1.0f);
+        dump(outDir + "/vstepdepth.bin", vsd);
         pm.clearSel();
     }
 
@@ -281,8 +293,8 @@ int main(int argc, char** argv) {
     fprintf(f, "region %.17g %.17g %.17g %.17g\n", reg.bottom_left.x, reg.bottom_left.y, reg.top_right.x,
             reg.top_right.y);
     fprintf(f, "filled %d\nnodes %ld\nruns %zu\n", pm.m_filled_point_count, nodes, runs.size() / 4);
-    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\nt_stepdepth %.6f\n",
-            std::chrono::duration<double>(t1 - t0).count(), tv, tvrt, tsd);
+    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\nt_stepdepth %.6f\nt_vstepdepth %.6f\n",
+            std::chrono::duration<double>(t1 - t0).count(), tv, tvrt, tsd, tvsd);
     fclose(f);
     printf("ok nodes %ld runs %zu t_makegraph %.3f t_vga %.3f\n", nodes, runs.size() / 4,
            std::chrono::duration<double>(t1 - t0).count(), tv);

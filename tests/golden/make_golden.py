@@ -30,9 +30,11 @@ CASES = {
     "barnsbury": (REF + "/testdata/barnsbury_drawing.graph", 2.0, ["531000,184000"], True, False, False),
     "syn128": ("inputs/syn128.csv", 1.0, ["0.5,0.5"], True, False, False),
     "syn256mk": ("inputs/syn256.csv", 1.0, ["0.5,0.5"], False, False, False),
+    "syn128sd": ("inputs/syn128.csv", 1.0, ["0.5,0.5"], False, False, False),   # step depths only
 }
 
-# metric step depth selections per case (STEPDEPTH -sdt metric -sdp x,y [-sdp ...])
+# step depth selections per case (STEPDEPTH -sdt metric|visual -sdp x,y [-sdp ...]); the probe runs
+# both step types on the same selection
 STEPDEPTH = {
     "kat": ["0.25,0.25"],
     "syn16": ["8.5,8.5"],
@@ -40,6 +42,7 @@ STEPDEPTH = {
     "syn64": ["32.5,32.5", "10.5,50.5"],
     "gallery": ["1.32,7.24"],
     "barnsbury": ["531000,184000"],
+    "syn128sd": ["64.5,64.5", "3.5,120.5"],
 }
 
 
@@ -112,6 +115,7 @@ def run_case(name):
         if name in STEPDEPTH:
             arrays["stepdepth"] = rd("stepdepth.bin", np.float32).reshape(N, 3)
             arrays["stepdepth_sel"] = rd("stepdepth_sel.bin", np.int32)
+            arrays["vstepdepth"] = rd("vstepdepth.bin", np.float32)
     lines_npy = name + "_lines.npy"
     np.save(os.path.join(HERE, lines_npy), lines)
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **arrays)
@@ -119,7 +123,8 @@ def run_case(name):
                 region=g["region"], cols=int(g["cols"]), rows=int(g["rows"]), bottom_left=g["bottom_left"],
                 nodes=N, runs=int(g["runs"]), lines_npy=lines_npy, vga=vga, roundtrip=rt, full_runs=keep,
                 stepdepth=STEPDEPTH.get(name, []),
-                ref_seconds=dict(makegraph=g["t_makegraph"], vga=g["t_vga"], stepdepth=g.get("t_stepdepth", 0.0)))
+                ref_seconds=dict(makegraph=g["t_makegraph"], vga=g["t_vga"], stepdepth=g.get("t_stepdepth", 0.0),
+                                 vstepdepth=g.get("t_vstepdepth", 0.0)))
     return meta
 
 

@@ -121,3 +121,10 @@ def test_cli_pipeline_matches_reference(tmp_path):
     np.testing.assert_array_equal(cols["Metric Step Shortest-Path Length"], ref[:, 1])
     np.testing.assert_array_equal(cols["Metric Straight-Line Distance"], ref[:, 2])
     assert np.allclose(cols["Metric Step Shortest-Path Angle"], ref[:, 0], rtol=1e-6, atol=1e-6)
+    # STEPDEPTH -sdt visual on the same graph (VGAVisualGlobalDepth::run): one column, -1 unreached
+    g4 = str(tmp_path / "d.dmxg")
+    rc, out = run("-m", "STEPDEPTH", "-f", g2, "-o", g4, "-sdt", "visual", "-sdp", "16.5,16.5")
+    assert rc == 0, out
+    cols4 = {c[0]: c[1] for c in graphio.read_chunk(chunk(g4))["columns"]}
+    want = om.visual_stepdepth(np.array([17 * rows + 17], np.int32))
+    np.testing.assert_array_equal(cols4["Visual Step Depth"], want)

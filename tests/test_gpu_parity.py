@@ -245,6 +245,41 @@ def test_metric_stepdepth_random_matches_oracle(ctx, seed):
         _assert_stepdepth(got, want)
 
 
+@pytest.mark.parametrize("name", SD_CASES + ["barnsbury", "syn128sd"])
+def test_visual_stepdepth_matches_reference(ctx, name):
+    """STEPDEPTH -sdt visual: the tile-resolved BFS in seed mode against the reference's column."""
+    meta, A = load_case(name)
+    if "vstepdepth" not in A:
+        pytest.skip("fixture without visual step depth")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    pts = [tuple(float(v) for v in p.split(",")) for p in meta["stepdepth"]]
+    got = g.visual_step_depth(points=pts)
+    np.testing.assert_array_equal(got.view(np.uint32), A["vstepdepth"].view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", [3, 7])
+def test_visual_stepdepth_random_matches_oracle(ctx, seed):
+    from pyoracle import OracleMap
+    from golden.gen_synthetic import make_lines
+    W = 64
+    lines = np.array(make_lines(W, 120, seed=seed, lmin=0.02, lmax=0.3), dtype=np.float64)
+    region = [0.0, 0.0, float(W), float(W)]
+    pm = dmx.PointMap(region, lines, 1.0)
+    om = OracleMap(region, 1.0, lines)
+    assert pm.make_points(0.5, 0.5) and om.fill(0.5, 0.5)
+    g = pm.make_graph(ctx)
+    om.make_graph(threads=8)
+    filled = np.nonzero(pm.state() & 2)[0]
+    rng = np.random.default_rng(seed)
+    for nsel in (1, 4, 32):
+        cells = np.sort(rng.choice(filled, nsel, replace=False))
+        got = g.visual_step_depth(cells=cells)
+        want = om.visual_stepdepth(cells)
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+        assert got.max() >= 2
+
+
 def test_metric_stepdepth_errors(ctx):
     meta, _ = load_case("syn32")
     pm = _map(meta)

@@ -133,3 +133,19 @@ def test_metric_stepdepth_matches_reference_bitexact(name):
     got = om.metric_stepdepth(cells)
     np.testing.assert_array_equal(got.view(np.uint32), A["stepdepth"].view(np.uint32))
     assert (A["stepdepth"][:, 1] >= 0).sum() > 0
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery", "syn128sd"])
+def test_visual_stepdepth_matches_reference_bitexact(name):
+    """VGAVisualGlobalDepth::run restatement vs the reference's STEPDEPTH -sdt visual column
+    (ref_probe --stepdepth runs both step types on the same setCurSel selection)."""
+    meta, A = load_case(name)
+    if "vstepdepth" not in A:
+        pytest.skip("fixture without visual step depth")
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    sel = A["stepdepth_sel"]
+    cells = (sel >> 16) * meta["rows"] + (sel & 0xFFFF)
+    got = om.visual_stepdepth(cells)
+    np.testing.assert_array_equal(got.view(np.uint32), A["vstepdepth"].view(np.uint32))
+    assert (A["vstepdepth"] >= 1).sum() > 0
