@@ -11,6 +11,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -51,19 +52,86 @@ int fail(int code, const std::string& msg) {
         if (e_ != hipSuccess) return fail(DMX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
     } while (0)
 
+// Caching device allocator for the large per-graph buffers (run pool, scan order, visibility rows:
+// tens of GB at 1000^2).  hipMalloc/hipFree of such blocks costs seconds per graph; repeated
+// analyses of same-sized maps reuse them instead.  Blocks >= 64 MiB are kept per device on free and
+// handed out again for requests of at most that size and at least 7/8 of it; an allocation that
+// fails releases the whole cache and retries.  All users work on one stream per context, so a
+// reused block is ordered after every kernel that touched it before.
+struct BlockCache {
+    static constexpr size_t kMin = 64ull << 20;
+    std::mutex m;
+    std::multimap<std::pair<int, size_t>, void*> free_blocks;   // (device, bytes) -> block
+    std::map<void*, std::pair<int, size_t>> live;                // cached-size blocks handed out
+    size_t cached = 0;
+    void release_all() {
+        for (auto& kv : free_blocks) (void)hipFree(kv.second);
+        free_blocks.clear();
+        cached = 0;
+    }
+};
+BlockCache& block_cache() {
+    static BlockCache* c = new BlockCache();   // never destroyed: frees at exit would race the runtime
+    return *c;
+}
+hipError_t cached_malloc(void** p, size_t bytes) {
+    BlockCache& c = block_cache();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (bytes >= BlockCache::kMin) {
+        std::lock_guard<std::mutex> g(c.m);
+        auto it = c.free_blocks.lower_bound({dev, bytes});
+        if (it != c.free_blocks.end() && it->first.first == dev && it->first.second - it->first.second / 8 <= bytes) {
+            *p = it->second;
+            c.cached -= it->first.second;
+            c.live[*p] = it->first;
+            c.free_blocks.erase(it);
+            return hipSuccess;
+        }
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) {
+        std::lock_guard<std::mutex> g(c.m);
+        if (c.cached) {
+            (void)hipGetLastError();
+            c.release_all();
+            e = hipMalloc(p, bytes);
+        }
+    }
+    if (e == hipSuccess && bytes >= BlockCache::kMin) {
+        std::lock_guard<std::mutex> g(c.m);
+        c.live[*p] = {dev, bytes};
+    }
+    return e;
+}
+void cached_free(void* p) {
+    BlockCache& c = block_cache();
+    {
+        std::lock_guard<std::mutex> g(c.m);
+        auto it = c.live.find(p);
+        if (it != c.live.end()) {
+            c.free_blocks.insert({it->second, p});
+            c.cached += it->second.second;
+            c.live.erase(it);
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+
 template <typename T> struct DevBuf {
     T* p = nullptr;
     size_t n = 0;
     ~DevBuf() { reset(); }
     void reset() {
-        if (p) (void)hipFree(p);
+        if (p) cached_free(p);
         p = nullptr;
         n = 0;
     }
     hipError_t alloc(size_t count) {
         if (count <= n && p) return hipSuccess;
         reset();
-        hipError_t e = hipMalloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
+        hipError_t e = cached_malloc((void**)&p, std::max<size_t>(count, 1) * sizeof(T));
         if (e == hipSuccess) n = count;
         return e;
     }
@@ -250,6 +318,13 @@ int dmx_ctx_create(int device, dmx_ctx** out) {
     HIPCHK(c->counters.alloc(16));
     HIPCHK(c->stats.alloc(32));
     *out = c;
+    return DMX_OK;
+}
+
+int dmx_release_cached_memory(void) {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.m);
+    c.release_all();
     return DMX_OK;
 }
 

@@ -130,6 +130,10 @@ __device__ __forceinline__ bool zone_less(double as, double ae, double bs, doubl
 }
 
 __device__ __forceinline__ unsigned long long ballot(bool p) { return __ballot(p); }
+// lane j's double (j wave-uniform)
+__device__ __forceinline__ double readlane_d(double v, int j) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), j), __builtin_amdgcn_readlane(__double2loint(v), j));
+}
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int prefix_popc(unsigned long long m) {
     return __popcll(m & ((1ull << lane_id()) - 1ull));
@@ -351,7 +355,71 @@ __global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
                 int nb = L.misc[1];
                 if (nb > bcap + P.spill_cap) { failed = true; if (lane == 0) atomicOr(P.error, KERR_BLOCK_CAPACITY); }
                 if (failed) break;
-                if (nb > 0) {
+                if (nb > 0 && nb <= 64 && nb <= bcap && ng <= 64) {
+                    // Register path (the common case): lane i holds block i and lane g gap g; the
+                    // dedup, the ranks and the serial merge read other lanes through v_readlane
+                    // (wave-uniform indices) instead of chains of dependent LDS reads.
+                    const bool valid = lane < nb;
+                    double bx = 0.0, by = 0.0;
+                    if (valid) { const double2 v = L.blocks[lane]; bx = v.x; by = v.y; }
+                    int first = valid ? 1 : 0;
+                    for (int j = 0; j < nb; j++) {
+                        const double ox = readlane_d(bx, j), oy = readlane_d(by, j);
+                        if (j < lane && ox == bx && oy == by) first = 0;
+                    }
+                    int rank = 0;
+                    for (int j = 0; j < nb; j++) {
+                        const int fj = __builtin_amdgcn_readlane(first, j);
+                        const double ox = readlane_d(bx, j), oy = readlane_d(by, j);
+                        if (fj && zone_less(ox, oy, bx, by)) rank++;
+                    }
+                    const int nu = __popcll(ballot(valid && first));
+                    if (valid && first) L.bsorted[rank] = make_double2(bx, by);
+                    double gx = 0.0, gy = 0.0;
+                    if (lane < ng) { const double2 v = L.gaps[lane]; gx = v.x; gy = v.y; }
+                    __syncthreads();
+                    double sx = 0.0, sy = 0.0;
+                    if (lane < nu) { const double2 v = L.bsorted[lane]; sx = v.x; sy = v.y; }
+                    // sparkSieve2::collectgarbage (sparksieve2.cpp:89-132), wave-uniform
+                    int gi = 0, bi = 0, no = 0;
+                    double cx_ = readlane_d(gx, 0), cy_ = readlane_d(gy, 0);
+                    while (bi < nu && gi < ng) {
+                        const double kx = readlane_d(sx, bi), ky = readlane_d(sy, bi);
+                        if (ky < cx_) { bi++; continue; }
+                        bool create = true;
+                        if (kx <= cx_) { create = false; if (ky > cx_) cx_ = ky; }
+                        if (ky >= cy_) { create = false; if (kx < cy_) cy_ = kx; }
+                        if (cy_ <= cx_ + 1e-10) {
+                            gi++;
+                            if (gi < ng) { cx_ = readlane_d(gx, gi); cy_ = readlane_d(gy, gi); }
+                            continue;
+                        } else if (ky > cy_) {
+                            if (lane == 0 && no < gcap) L.gaps2[no] = make_double2(cx_, cy_);
+                            no++;
+                            gi++;
+                            if (gi < ng) { cx_ = readlane_d(gx, gi); cy_ = readlane_d(gy, gi); }
+                            continue;
+                        } else if (create) {
+                            if (lane == 0 && no < gcap) L.gaps2[no] = make_double2(cx_, kx);
+                            no++;
+                            cx_ = ky;
+                        }
+                        bi++;
+                    }
+                    if (gi < ng) {
+                        if (lane == 0 && no < gcap) L.gaps2[no] = make_double2(cx_, cy_);
+                        no++;
+                        // the untouched gaps gi+1 .. ng-1, in parallel from their lanes
+                        if (lane > gi && lane < ng && no + (lane - gi - 1) < gcap) L.gaps2[no + (lane - gi - 1)] = make_double2(gx, gy);
+                        no += ng - gi - 1;
+                    }
+                    if (no > gcap) { if (lane == 0) atomicOr(P.error, KERR_GAP_CAPACITY); failed = true; break; }
+                    __syncthreads();
+                    ng = no;
+                    for (int i = lane; i < ng; i += 64) L.gaps[i] = L.gaps2[i];
+                    if (lane == 0) L.misc[1] = 0;
+                    __syncthreads();
+                } else if (nb > 0) {
                     // std::sort (start asc, end desc) + std::unique: first-occurrence flags, then
                     // each distinct block lands at its rank among the distinct blocks.  Blocks past
                     // the LDS capacity live in this wave's HBM spill area (rare: long walls across

@@ -42,6 +42,10 @@ const char* dmx_last_error(void);
  * salalib is single-threaded CPU code. */
 int dmx_ctx_create(int device, dmx_ctx** out);
 int dmx_ctx_free(dmx_ctx* ctx);
+/* Return the device blocks the engine keeps cached for reuse by the next graph of the same size
+ * (run pool, scan order, visibility rows) to the HIP runtime.  Optional; allocation failures do it
+ * automatically. */
+int dmx_release_cached_memory(void);
 /* Wall time of the kernels of the last makegraph / vga call, measured with HIP events on the
  * context stream (seconds); kernel_ms receives per-kernel averages. */
 int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
