@@ -1020,9 +1020,9 @@ static int prepare_tiles(dmx_graph* g) {
         HIPCHK(hipGetLastError());
         const char* tt_env = getenv("DMX_VGA_TTVIS");
         if (ftv_on && !(tt_env && atoi(tt_env) == 0)) {
-            HIPCHK(g->ttvis.alloc((size_t)nt * tvw));
+            HIPCHK(g->ttvis.alloc((size_t)2 * nt * tvw));   // ttvis, then ttany
             hipLaunchKernelGGL(tile_tt_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, nt, tvw, g->regular_tiles.p,
-                               g->ftvis.p, g->ttvis.p);
+                               g->ftvis.p, g->tvis.p, g->ttvis.p, g->ttvis.p + (size_t)nt * tvw);
             HIPCHK(hipGetLastError());
         }
         g->tvw = tvw;
@@ -1089,6 +1089,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.tvis = g->tvw ? g->tvis.p : nullptr; Q.tvw = g->tvw;
     Q.ftvis = (g->tvw && g->ftvis.p) ? g->ftvis.p : nullptr;
     Q.ttvis = (g->tvw && g->ttvis.p) ? g->ttvis.p : nullptr;
+    Q.ttany = Q.ttvis ? g->ttvis.p + (size_t)tw * th * g->tvw : nullptr;
     Q.node_cell = g->pm->d_node_cell.p; Q.cell_node = g->pm->d_cell_node.p; Q.node_flags = g->pm->d_node_flags.p;
     Q.node_run_start = g->node_run_start.p; Q.node_nruns = g->node_nruns.p; Q.pool = g->pool.p;
     const bool corr = g->nspecial > 0;
@@ -1166,6 +1167,8 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[20] = (long long)st[18];                          // phase-B tiles
     ctx->last_stats[21] = (long long)st[19];                          // phase-B cells
     ctx->last_stats[22] = (long long)st[20];                          // phase-B tiles resolved by ttvis
+    ctx->last_stats[27] = (long long)st[25];                          // phase-B tiles pruned by ttany
+    ctx->last_stats[28] = (long long)st[26];                          // phase-B1 clocks
     ctx->last_stats[23] = (long long)st[21];                          // phase-C busy clocks summed over waves
     ctx->last_stats[24] = (long long)st[22];                          // phase-C run-scan clocks summed over waves
     ctx->last_stats[25] = (long long)st[23];                          // phase-C special-node clocks

@@ -41,6 +41,7 @@ struct VgaTileParams {
     const unsigned long long* tvis;           // [nt*64][tvw] tiles seen by each cell, Fsr layout (null: off)
     const unsigned long long* ftvis;          // [nt*64][tvw] tiles whose every non-seed cell the cell sees (null: off)
     const unsigned long long* ttvis;          // [nt][tvw] AND of ftvis over the tile's regular cells (null: off)
+    const unsigned long long* ttany;          // [nt][tvw] OR of tvis over the tile's regular cells
     int tvw;                                  // th * ceil(tw / 64)
     const int32_t* node_cell;
     const int32_t* cell_node;
@@ -81,7 +82,7 @@ struct VgaTileParams {
                                 // [8..12] phase clocks, [13] hard cells rejected by their tile-visibility row,
                                 // [14] tile-visibility rows read, [1] phase-C hits, [15] phase-C runs,
                                 // [16] phase-C hits certified by a fully seen frontier tile, [17] top-down clocks,
-                                // [18] phase-B tiles, [19] phase-B cells, [20] phase-B tiles resolved by ttvis
+                                // [18] phase-B tiles, [19] phase-B cells, [20] phase-B tiles resolved by ttvis, [25] pruned by ttany
 };
 
 __device__ __forceinline__ int tile_id_of(int x, int y, int tw) {
@@ -494,16 +495,21 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     int4 e[4];
 #pragma unroll
                     for (int j = 0; j < 4; j++) e[j] = (it0 + j < qn) ? Q[it0 + j] : make_int4(-1, 0, 0, 0);
-                    unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull};
+                    unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull}, acca[4] = {~0ull, ~0ull, ~0ull, ~0ull};
                     if (P.ttvis) {
+#pragma unroll
+                        for (int j = 0; j < 4; j++) acca[j] = 0ull;
 #pragma unroll
                         for (int k = 0; k < 4; k++) {
                             const int w = k * 64 + lane;
-                            if (w < P.tvw) {
-                                const unsigned long long fs = Fsr[w];
+                            const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
+                            if (fs) {
 #pragma unroll
                                 for (int j = 0; j < 4; j++)
-                                    if (e[j].x >= 0) acc[j] |= P.ttvis[(size_t)e[j].x * P.tvw + w] & fs;
+                                    if (e[j].x >= 0) {
+                                        acc[j] |= P.ttvis[(size_t)e[j].x * P.tvw + w] & fs;
+                                        acca[j] |= P.ttany[(size_t)e[j].x * P.tvw + w] & fs;
+                                    }
                             }
                         }
                     }
@@ -519,6 +525,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                             const unsigned long long R = mask & reg;
                             if (lane == 0) { or_wg(&Xg[t], R); ST(20, 1); }
                             mask &= ~R;
+                        } else if (__ballot(acca[j] != 0ull) == 0ull) {
+                            // no regular cell of t sees any frontier tile: none is at the next level
+                            if (lane == 0) ST(25, 1);
+                            mask &= ~reg;
                         }
                         const bool mine = (mask >> lane) & 1ull;
                         const unsigned long long bm = __ballot(mine);
@@ -533,6 +543,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                     }
                 }
                 sync_global();
+                if (tid == 0) ST(26, __builtin_amdgcn_s_memtime() - tmark);   // B1 share of the heads clock
                 const int bn = S.bn;
                 // ---- B2: per cell (lane = cell, full waves): the hint run, the heads, then the next
                 // bext runs of the scan order; misses go to the hard list
@@ -634,8 +645,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
 #pragma unroll
                             for (int j = 0; j < 4; j++) {
                                 const int w = j * 64 + lane;
-                                if (w < P.tvw) {
-                                    const unsigned long long fs = Fsr[w];
+                                const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
+                                if (fs) {   // rows are read only under frontier tile rows
                                     ta |= tv[w] & fs;
                                     if (ftv) fa |= ftv[w] & fs;
                                 }
@@ -661,19 +672,19 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                                 if (r < nr) rr[j] = P.scan_pool[rs + r];
                                 else rr[j].x0 = -1;
                             }
-                            int first = 1 << 30;
                             // the four tests are independent (no early-out between them), so their
                             // LDS round trips overlap
                             bool h4[4];
 #pragma unroll
                             for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
+                            int fpos = -1;
 #pragma unroll
-                            for (int j = 3; j >= 0; j--)
-                                if (h4[j]) first = base + j * 64 + lane;
-                            int fmin = first;
-                            for (int off = 32; off >= 1; off >>= 1) fmin = min(fmin, __shfl_xor(fmin, off));
-                            found = fmin != (1 << 30);
-                            if (found && lane == 0) Hn[id] = (uint16_t)min(fmin, 0xFFFE);
+                            for (int j = 3; j >= 0; j--) {
+                                const unsigned long long hm = __ballot(h4[j]);
+                                if (hm) fpos = base + j * 64 + __ffsll((long long)hm) - 1;
+                            }
+                            found = fpos >= 0;
+                            if (found && lane == 0) Hn[id] = (uint16_t)min(fpos, 0xFFFE);
                         }
                         if (lane == 0) ST(22, __builtin_amdgcn_s_memtime() - s_t0);
                         if (lane == 0 && !certain && !(P.tvis && base == nr && !found && nr > KH + P.bext && pruned_now)) {
@@ -949,19 +960,23 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int t
 
 // Tile-to-tile full visibility: row t = AND of the ftvis rows of tile t's regular cells (bit u set
 // iff every regular cell of t sees every non-seed cell of tile u).  One wave per tile.
+// ttany row t = OR of the tvis rows of t's regular cells (tiles some regular cell of t sees at all):
+// no frontier tile under it means no regular cell of t can be reached at this level.
 __global__ void tile_tt_kernel(int nt, int tvw, const unsigned long long* regular_tiles, const unsigned long long* ftvis,
-                               unsigned long long* ttvis) {
+                               const unsigned long long* tvis, unsigned long long* ttvis, unsigned long long* ttany) {
     const int lane = threadIdx.x & 63;
     const int t = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (t >= nt) return;
     const unsigned long long R = regular_tiles[t];
     for (int w = lane; w < tvw; w += 64) {
-        unsigned long long acc = R ? ~0ull : 0ull;
-        for (unsigned long long m = R; m && acc; m &= m - 1) {
+        unsigned long long acc = R ? ~0ull : 0ull, any = 0ull;
+        for (unsigned long long m = R; m; m &= m - 1) {
             const int b = __ffsll((long long)m) - 1;
             acc &= ftvis[((size_t)t * 64 + b) * tvw + w];
+            any |= tvis[((size_t)t * 64 + b) * tvw + w];
         }
         ttvis[(size_t)t * tvw + w] = acc;
+        ttany[(size_t)t * tvw + w] = any;
     }
 }
 

@@ -51,7 +51,8 @@ for k, v in configs:
                       "hard_runs_per_src": st["vga_hard_runs"] / nsrc, "hard_certain_per_src": st["vga_hard_certain"] / nsrc,
                       "topdown_cycles_per_src": st["vga_topdown_cycles"] / nsrc,
                       "b_tiles_per_src": st["vga_b_tiles"] / nsrc, "b_cells_per_src": st["vga_b_cells"] / nsrc,
-                      "tt_tiles_per_src": st["vga_tt_tiles"] / nsrc,
+                      "tt_tiles_per_src": st["vga_tt_tiles"] / nsrc, "tt_pruned_per_src": st["vga_tt_pruned"] / nsrc,
+                      "b1_cycles_per_src": st["vga_b1_cycles"] / nsrc,
                       "c_busy_per_src": st["vga_c_busy"] / nsrc, "c_scan_per_src": st["vga_c_scan"] / nsrc,
                       "c_spec_per_src": st["vga_c_spec"] / nsrc, "n_spec_per_src": st["vga_n_spec"] / nsrc,
                       "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc, "kernel": st["vga_kernel"], "special_nodes": st["vga_special_nodes"],
