@@ -440,7 +440,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     HIPCHK(g->gridconn.alloc(std::max<int64_t>(n, 1)));
 
     // capacities (retried on overflow)
-    int gcap = 128, bcap = 128;
+    int gcap = 64, bcap = 64;   // (10 waves per CU; larger lists spill to HBM or retry)
     int spill_cap = 4096;      // per-wave HBM blocks past bcap
     int64_t capB = 32 * (int64_t)D + 2048;
     if (const char* e = getenv("DMX_MK_GCAP")) gcap = std::max(2, atoi(e));   // test hooks for the retry path

@@ -232,7 +232,7 @@ struct Lds {
     int* bflag;       // [bcap] first-occurrence flags
 };
 
-__global__ void __launch_bounds__(64) makegraph_kernel(MakeGraphParams P) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) makegraph_kernel(MakeGraphParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int gcap = P.gcap, bcap = P.bcap, D = P.dmax;
