@@ -207,6 +207,17 @@ __device__ __forceinline__ void dd_merge(double& h, double& l, double bh, double
     h = s + t;
     l = t - (h - s);
 }
+// Plain per-lane double sums reduced by a 6-level butterfly: |S~ - S| <= gamma_(m+6) S with m the
+// largest per-lane count; the reference's serial chain is within gamma_(n-1) S of S.
+__device__ __forceinline__ bool certified_float_sum(double S, long long n, long long m, float* out) {
+    const double u = 0x1p-53;
+    const double g1 = (double)n * u / (1.0 - (double)n * u);
+    const double g2 = (double)(m + 7) * u / (1.0 - (double)(m + 7) * u);
+    const double E = 2.0 * (g1 + g2) * S + S * 0x1p-50;
+    const float a = (float)(S - E), b = (float)(S + E);
+    *out = a;
+    return a == b;
+}
 __device__ __forceinline__ bool certified_float(double h, double l, long long n, float* out) {
     const double u = 0x1p-53;
     const double g = (double)n * u / (1.0 - (double)n * u);
@@ -305,7 +316,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
         __syncthreads();
 
         double tsum = 0.0, tsum2 = 0.0; // wave-uniform, reference order (exact_moments)
-        double s1h = 0.0, s1l = 0.0, s2h = 0.0, s2l = 0.0;   // per-lane double-double (fast path)
+        double s1 = 0.0, s2 = 0.0;   // per-lane sums (fast path, certified at the end)
+        int mcnt = 0;                // this lane's summand count
         int nsize = 0;
         unsigned long long examined = 0;
         int bpos = 0;        // next free run slot in stageB
@@ -349,6 +361,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
             int diag_n = 0, diag_min = 0, diag_max = 0;
             int nA = 0;                 // emissions staged in this octant
             const int q_sector = c_sector_base[q], q_axis = c_axis_bin[q], q_diag = c_diag_bin[q];
+            // whichbin of this octant's directions by ratio class: axis, < tan15, < tan30, < 1, diagonal
+            int obin[5];
+            {
+                const double rr[5] = {0.0, 0.1, 0.4, 0.8, 1.0};
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    const double mj = 10.0, mn = 10.0 * rr[k];
+                    const double ax = (q >= 4 ? mn : mj), ay = (q >= 4 ? mj : mn);
+                    obin[k] = whichbin((q & 1) ? ax : -ax, (q <= 1 || q >= 6) ? ay : -ay);
+                }
+            }
             int depth = 0;
             for (;;) {
                 // ---------------- collectgarbage (sparksieve2.cpp:89-132) for the previous depth
@@ -583,8 +606,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                         int bin = -1;
                         double this_dist = 0.0;
                         if (add) {
-                            const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
-                            bin = whichbin(px - c0x, py - c0y);
+                            // whichbin(depixelate(c) - centre) (pointdata.h:432-520) decided on the exact
+                            // ratio ind/depth: 0 and 1 are the axis / diagonal; tan15 and tan30 are
+                            // irrational, so a float test with a 1e-6 margin decides every cell the
+                            // reference's FP64 ratio (error ~1e-15) decides; cells inside the margin take
+                            // the FP64 path
+                            int k;
+                            if (ind == 0) k = 0;
+                            else if (ind == depth) k = 4;
+                            else {
+                                const float fd = (float)depth, fi = (float)ind, mg = 1e-6f * fd;
+                                const float e15 = fi - 0.267949192f * fd, e30 = fi - 0.577350269f * fd;
+                                k = (fabsf(e15) < mg || fabsf(e30) < mg) ? -1 : 1 + (e15 >= 0.0f) + (e30 >= 0.0f);
+                            }
+                            if (k >= 0) {
+                                bin = obin[k];
+                            } else {
+                                const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
+                                bin = whichbin(px - c0x, py - c0y);
+                            }
                             const double dx = (double)(hx - cx), dy = (double)(hy - cy);
                             this_dist = sqrt(dx * dx + dy * dy) * sp;
                             atomicAdd(&L.binc[bin], 1u);
@@ -606,8 +646,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                                 mm &= mm - 1;
                             }
                         } else if (add) {
-                            dd_add(s1h, s1l, this_dist);
-                            dd_add(s2h, s2l, this_dist * this_dist);
+                            s1 += this_dist;
+                            s2 += this_dist * this_dist;
+                            mcnt++;
                         }
                         MK_T(4);
                         nsize += __popcll(am);
@@ -775,16 +816,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                 m1f = (float)tsum;
                 m2f = (float)tsum2;
             } else {
+                int mmax = mcnt;
                 for (int off = 32; off >= 1; off >>= 1) {
-                    const double a = __shfl_xor(s1h, off), b = __shfl_xor(s1l, off);
-                    const double c = __shfl_xor(s2h, off), d = __shfl_xor(s2l, off);
-                    dd_merge(s1h, s1l, a, b);
-                    dd_merge(s2h, s2l, c, d);
+                    s1 += __shfl_xor(s1, off);
+                    s2 += __shfl_xor(s2, off);
+                    mmax = max(mmax, __shfl_xor(mmax, off));
                 }
-                // lanes reduce in different orders: take lane 0's pair
-                s1h = __shfl(s1h, 0); s1l = __shfl(s1l, 0); s2h = __shfl(s2h, 0); s2l = __shfl(s2l, 0);
-                const bool ok1 = certified_float(s1h, s1l, nsize, &m1f);
-                const bool ok2 = certified_float(s2h, s2l, nsize, &m2f);
+                // lanes reduce in different orders: take lane 0's sums
+                s1 = __shfl(s1, 0); s2 = __shfl(s2, 0);
+                const bool ok1 = certified_float_sum(s1, nsize, mmax, &m1f);
+                const bool ok2 = certified_float_sum(s2, nsize, mmax, &m2f);
                 if (!(ok1 && ok2)) failed = true;   // re-run with the serial chains (no capacity error)
             }
         }
