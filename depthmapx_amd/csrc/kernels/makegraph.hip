@@ -523,7 +523,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                 // ---------------- sieve2 for this depth (pointdata.cpp:1512-1565)
                 // per-gap visit ranges with the monotone firstind rule
                 int carryF = 0, carryT = 0;
-                for (int base = 0; base < ng; base += 64) {
+                if (ng <= 8) {
+                    // few gaps (the common case): a wave-uniform loop over the gaps in order -- no
+                    // cross-lane scans.  F = the largest b of the earlier visited gaps (at least 0).
+                    int F = 0, T = 0;
+                    for (int g = 0; g < ng; g++) {
+                        const double2 z = L.gaps[g];
+                        const int lo = (int)ceil(z.x * (depth - 0.5) - 0.5);
+                        const int hi = (int)floor(z.y * (depth + 0.5) + 0.5);
+                        const int b = min(hi, depth);
+                        const int a = max(lo, F);
+                        const int c = (b >= a) ? (b - a + 1) : 0;
+                        if (lane == 0) { L.ga[g] = a; L.gpre[g] = T; }
+                        T += c;
+                        if (b >= lo) F = max(F, b);
+                    }
+                    carryT = T;
+                }
+                for (int base = 0; base < ng && ng > 8; base += 64) {
                     int g = base + lane;
                     int lo = 0, b = -1;
                     bool vis = false;
