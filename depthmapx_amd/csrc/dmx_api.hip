@@ -288,7 +288,7 @@ size_t makegraph_lds(int gcap, int bcap, int D) {
     b += 16 * (size_t)gcap * 2 + 16 * (size_t)bcap; // gaps, gaps2, blocks
     b += 4 * 32 * 3 + 4 * 32;                        // binc, bfar, bnr, misc
     b += 16 * (size_t)bcap;                          // bsorted
-    b += 4 * (size_t)gcap + 4 * (size_t)bcap + 4 * ((size_t)gcap + 4);
+    b += 4 * (size_t)gcap + 8 * (size_t)gcap + 4 * (size_t)bcap + 4 * ((size_t)gcap + 4);
     b += 4 * ((size_t)D + 4);
     b += 2 * (3 * ((size_t)D + 1) + 2);
     return (b + 15) & ~(size_t)15;

@@ -232,6 +232,7 @@ struct Lds {
     double2* gaps2;   // [gcap] merge output
     double2* blocks;  // [bcap]
     int* ga;          // [gcap] first visited ind per gap
+    int2* gc;         // [gcap] centregap ind range per gap: ceil(fl(start*depth)), floor(fl(end*depth))
     int* gpre;        // [gcap+1] exclusive prefix of visited counts
     uint32_t* openr;  // [dmax+2]
     uint16_t* cnt;    // [3*(dmax+1)]
@@ -258,6 +259,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
         L.bnr = (int*)p; p += 4 * 32;
         L.misc = (int*)p; p += 4 * 32;
         L.bsorted = (double2*)p; p += sizeof(double2) * bcap;
+        L.gc = (int2*)p; p += 8 * gcap;   // (8-aligned: follows the 16-byte arrays)
         L.ga = (int*)p; p += 4 * gcap;
         L.bflag = (int*)p; p += 4 * bcap;
         L.gpre = (int*)p; p += 4 * (gcap + 4);
@@ -534,7 +536,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                         const int b = min(hi, depth);
                         const int a = max(lo, F);
                         const int c = (b >= a) ? (b - a + 1) : 0;
-                        if (lane == 0) { L.ga[g] = a; L.gpre[g] = T; }
+                        if (lane == 0) {
+                            L.ga[g] = a;
+                            L.gpre[g] = T;
+                            L.gc[g] = make_int2((int)ceil(z.x * depth), (int)floor(z.y * depth));
+                        }
                         T += c;
                         if (b >= lo) F = max(F, b);
                     }
@@ -550,6 +556,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                         int hi = (int)floor(z.y * (depth + 0.5) + 0.5);
                         b = min(hi, depth);
                         vis = (b >= lo);
+                        L.gc[g] = make_int2((int)ceil(z.x * depth), (int)floor(z.y * depth));
                     }
                     int bp = vis ? b : INT_MIN;
                     int incl = wave_incl_max(bp);
@@ -574,14 +581,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                     int t = t0 + lane;
                     bool valid = t < T;
                     int ind = 0, hx = 0, hy = 0;
-                    double gst = 0, gen = 0;
+                    int2 gcr = make_int2(0, -1);
                     bool ingrid = false, add = false;
                     uint32_t w = 0;
                     if (valid) {
                         while (L.gpre[gcur + 1] <= t) gcur++;
                         ind = L.ga[gcur] + (t - L.gpre[gcur]);
-                        double2 z = L.gaps[gcur];
-                        gst = z.x; gen = z.y;
+                        gcr = L.gc[gcur];
                         octant_cell(q, cx, cy, depth, ind, hx, hy);
                         ingrid = (hx >= 0 && hx < P.cols && hy >= 0 && hy < P.rows);
                     }
@@ -589,7 +595,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                         const int hc = hx * P.rows + hy;
                         w = P.cellw[hc];
                         const int nl = cell_nseg(w), off = cell_seg_off(w);
-                        const bool centregap = ((double)ind >= gst * depth && (double)ind <= gen * depth);
+                        // (double)ind >= start*depth && (double)ind <= end*depth, on the integer
+                        // bounds of the two FP64 products (computed once per gap and depth)
+                        const bool centregap = ind >= gcr.x && ind <= gcr.y;
                         if (centregap && cell_filled(w) &&
                             (ind != 0 || q == 0 || q == 1 || q == 5 || q == 6) && (ind != depth || q < 4)) {
                             // sparkSieve2::testblock (sparksieve2.cpp:45-63)
