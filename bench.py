@@ -115,7 +115,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     import depthmapx_amd as dmx
-    from depthmapx_amd.sharded import allgather_blobs, allgather_rows, shard_range
+    from depthmapx_amd.sharded import allgather_blobs, allgather_rows_chunked, shard_range, vga_nodes
 
     W = args.grid
     mk_mode = args.mk_mode
@@ -129,7 +129,8 @@ def main():
     assert pm.make_points(*fill)
     info = pm.info()
     N = info["filled"]
-    b, e = shard_range(N, rank, world)
+    b, e = shard_range(N, rank, world)          # makeGraph sources of this rank
+    vnodes = vga_nodes(N, rank, world) if world > 1 else None   # VGA sources of this rank
     workload = "synthetic-%d/%d-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + VGA -vm visibility -vg -vr n" % (
         W, args.occluders)
 
@@ -155,13 +156,16 @@ def main():
             del flat, blob, shard
         else:
             g = shard
-        # 3. VGA global for this rank's sources
-        g.vga_visual_global_device(out_full.data_ptr(), src_begin=b, src_end=e)
+        # 3. VGA global for this rank's sources (node chunks dealt round-robin: balanced BFS cost)
+        if world > 1:
+            g.vga_visual_global_device_list(out_full.data_ptr(), vnodes)
+        else:
+            g.vga_visual_global_device(out_full.data_ptr())
         t_vga = ctx.last_timing()[1]
         st.update({k: v for k, v in ctx.last_stats().items() if k.startswith("vga")})
         # 4. all-gather the 7 float columns
         if world > 1:
-            allgather_rows(out_full, N, dist)
+            allgather_rows_chunked(out_full, N, dist)
         if record:
             kt["makegraph_s"] += t_mk
             kt["vga_s"] += t_vga
@@ -193,7 +197,7 @@ def main():
         steps = max(args.steps, 1)
         mk_s = kt["makegraph_s"] / max(kt["n"], 1)
         vga_s = kt["vga_s"] / max(kt["n"], 1)
-        nsrc = e - b
+        nsrc = len(vnodes) if world > 1 else N
         # algorithmic bytes per launch
         mk_bytes = 8 * stats.get("mk_runs", 0) + 4 * stats.get("mk_cells_examined", 0)
         tw, th = (info["cols"] + 7) // 8, (info["rows"] + 7) // 8
@@ -225,7 +229,7 @@ def main():
                        "runs": int(g.info()["nruns"]),
                        "parallelism": "source-shard x%d (makeGraph %s)" % (world, mk_mode)},
             "kernels": {"makegraph_s": mk_s, "vga_s": vga_s,
-                        "makegraph_cells_per_s": (N if mk_mode == "replicate" or world == 1 else nsrc) / mk_s
+                        "makegraph_cells_per_s": (N if mk_mode == "replicate" or world == 1 else e - b) / mk_s
                         if mk_s else None,
                         "visible_pairs": stats.get("mk_visible_pairs"),
                         "vga_kernel": stats.get("vga_kernel"),

@@ -1064,7 +1064,7 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
 
 static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
                          bool out_on_device, int64_t* levels, int tw, int th, const int32_t* d_seeds = nullptr,
-                         int nseeds = 0, int32_t* d_cell_level = nullptr) {
+                         int nseeds = 0, int32_t* d_cell_level = nullptr, const int32_t* d_src_list = nullptr) {
     int rc = prepare_tiles(g);
     if (rc) return rc;
     PointMapHost& h = *g->pm->host;
@@ -1101,6 +1101,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.src_begin = sb; Q.src_end = se; Q.radius = (int)radius; Q.gates_only = gates_only;
     Q.uf_count = g->uf_count;
     Q.seeds = d_seeds; Q.nseeds = nseeds; Q.cell_level = d_cell_level;
+    Q.src_list = d_src_list;   // [sb, se) index this list of source nodes (out must be on the device)
     // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
     Q.alpha = 60;   // top-down costs a frontier cell its whole run list (~R/N runs): keep it rare
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
@@ -1144,7 +1145,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
         if (rc) return rc;
         if (nseeds == 0) {
             hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsrc + 255) / 256)), dim3(256), 0, ctx->stream, sb,
-                               se, d_hist.p, d_nlev.p, outp, levels ? d_lv.p : nullptr, ctx->stats.p);
+                               se, d_hist.p, d_nlev.p, outp, levels ? d_lv.p : nullptr, ctx->stats.p, d_src_list);
             HIPCHK(hipGetLastError());
         }
         HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
@@ -1320,6 +1321,34 @@ int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se,
                           float* out_device) {
     return vga_impl(ctx, g, radius, gates_only, sb, se, out_device, true, nullptr);
+}
+
+// VGA global for an arbitrary set of source nodes (multi-GPU shards interleaved over the grid so that
+// every rank gets the same mix of cheap and expensive sources).  Tile-resolved BFS only.
+int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
+                               int64_t n, float* out_device) {
+    if (!ctx || !g || !out_device || (n > 0 && !nodes)) return fail(DMX_ERR_ARG, "bad arguments");
+    if (g->node_begin != 0 || g->node_end != g->nnodes)
+        return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int64_t N = g->nnodes;
+    std::vector<int32_t> lst((size_t)std::max<int64_t>(n, 1));
+    for (int64_t i = 0; i < n; i++) {
+        if (nodes[i] < 0 || nodes[i] >= N) return fail(DMX_ERR_ARG, "source node out of range");
+        lst[i] = (int32_t)nodes[i];
+    }
+    int rc = prepare_uf(g);
+    if (rc) return rc;
+    rc = prepare_symmetry(g);
+    if (rc) return rc;
+    PointMapHost& h = *g->pm->host;
+    const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
+    if (g->symmetric != 1 || tw * th > 16 * 1024 || ctx->tile_disabled)
+        return fail(DMX_ERR_UNSUPPORTED, "source lists need the tile-resolved BFS (grid <= 1024^2, symmetric graph)");
+    DevBuf<int32_t> d_list;
+    HIPCHK(d_list.alloc(lst.size()));
+    HIPCHK(hipMemcpyAsync(d_list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    return vga_tile_impl(ctx, g, radius, gates_only, 0, n, out_device, true, nullptr, tw, th, nullptr, 0, nullptr, d_list.p);
 }
 
 // ---------------------------------------------------------------- metric step depth

@@ -71,6 +71,7 @@ struct VgaTileParams {
     // cell_level[tile id] receives the level of every cell reached (launch one source, one block)
     const int32_t* seeds;
     int nseeds;
+    const int32_t* src_list;  // optional: work index i -> source node src_list[i] (multi-GPU interleaved shards)
     int32_t* cell_level;
     int bext;                 // phase-B runs after the heads (BEXT_DEFAULT)
     int crk;                  // tile-common runs tested in phase A (<= CRK)
@@ -395,12 +396,13 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             src++;
         }
         if (src >= P.src_end) break;
+        const int64_t node = P.src_list ? (int64_t)P.src_list[src] : src;   // the source node
         const bool seeded = P.nseeds > 0;
-        const int scell = P.node_cell[seeded ? P.seeds[0] : src];
+        const int scell = P.node_cell[seeded ? P.seeds[0] : node];
         const int sx = scell / rows, sy = scell % rows;
         // VGAVisualGlobal::run: context-filled odd sources and gates_only are skipped (:72-75)
-        if (!seeded && (((P.node_flags[src] & 1) && !((sx % 2) == 0 && (sy % 2) == 0)) || P.gates_only)) {
-            if (tid == 0) P.nlev_out[src] = 0;
+        if (!seeded && (((P.node_flags[node] & 1) && !((sx % 2) == 0 && (sy % 2) == 0)) || P.gates_only)) {
+            if (tid == 0) P.nlev_out[node] = 0;
             continue;
         }
         const int stile = (sy >> 3) * tw + (sx >> 3);
@@ -442,7 +444,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             if (level == 0) {
                 // ---- level 1: rasterise the source's runs (top-down from {s}, or from every seed)
                 for (int i = 0; i < (seeded ? P.nseeds : 1); i++) {
-                    const int64_t sn = seeded ? P.seeds[i] : src;
+                    const int64_t sn = seeded ? P.seeds[i] : node;
                     const int64_t rs = P.node_run_start[sn];
                     const int nr = P.node_nruns[sn];
                     for (int r = tid; r < nr; r += NT) run_or(F, tw, P.pool[rs + r]);
@@ -818,8 +820,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
             if (lane == 0 && r) ST(0, r);
             rt = 0;
         }
-        for (int l = tid; l < nlev; l += NT) P.hist_out[src * VGA_HMAX + l] = hist[l];
-        if (tid == 0) P.nlev_out[src] = nlev;
+        for (int l = tid; l < nlev; l += NT) P.hist_out[node * VGA_HMAX + l] = hist[l];
+        if (tid == 0) P.nlev_out[node] = nlev;
         __syncthreads();
     }
     for (int off = 32; off >= 1; off >>= 1) rt += __shfl_xor(rt, off);
@@ -1120,9 +1122,10 @@ __global__ void __launch_bounds__(CR_THREADS) tile_cr_kernel(int cols, int rows,
 
 // K4: the 7 VGA measures per source from its level histogram (vgavisualglobal.cpp:131-193).
 __global__ void vga_measures_kernel(int64_t sb, int64_t se, const int32_t* hist_all, const int32_t* nlev_all, float* out,
-                                    int64_t* levels_out, unsigned long long* stats) {
-    const int64_t src = sb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (src >= se) return;
+                                    int64_t* levels_out, unsigned long long* stats, const int32_t* src_list = nullptr) {
+    const int64_t i = sb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= se) return;
+    const int64_t src = src_list ? (int64_t)src_list[i] : i;
     const int nlev = nlev_all[src];
     float* o = out + src * 7;
     if (nlev == 0) {   // skipped source (context-filled odd cell / gates_only)

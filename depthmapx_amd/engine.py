@@ -234,6 +234,12 @@ class Graph:
         N.check(N.lib().dmx_visual_stepdepth(self.ctx.h, self.h, N.ptr(arr), len(arr), N.ptr(out)))
         return out
 
+    def vga_visual_global_device_list(self, out_dev_ptr, nodes, radius=-1.0, gates_only=False):
+        """VGA global for the listed source nodes only (rows of the others untouched); device output."""
+        arr = np.ascontiguousarray(nodes, dtype=np.int64)
+        N.check(N.lib().dmx_vga_global_device_list(self.ctx.h, self.h, float(radius), int(bool(gates_only)),
+                                                   N.ptr(arr), len(arr), ctypes.c_void_p(out_dev_ptr)))
+
     def vga_visual_global_device(self, out_dev_ptr, radius=-1.0, gates_only=False, src_begin=0, src_end=-1):
         N.check(N.lib().dmx_vga_global_device(self.ctx.h, self.h, float(radius), int(bool(gates_only)),
                                               int(src_begin), int(src_end), ctypes.c_void_p(out_dev_ptr)))

@@ -2,11 +2,13 @@
 
 The units are source cells: rank r owns the contiguous x-major node range shard_range(N, r, W).
 Per step
-  1. makeGraph for the owned sources (no communication);
+  1. makeGraph for the owned sources (no communication; its cost is about the same for every
+     source, so contiguous ranges balance);
   2. all-gather of the run-length graph shards (ragged byte blobs, padded to the largest) so every
      rank holds the whole graph -- VGA BFS from any source can reach any node;
-  3. VGA global for the owned sources;
-  4. all-gather of the owned rows of the 7 float columns.
+  3. VGA global for the rank's VGA sources: fixed-size node chunks dealt round-robin over the
+     ranks (vga_nodes), because the BFS cost of a source depends on where it sits in the plan;
+  4. all-gather of the owned rows of the 7 float columns (allgather_rows_chunked).
 Only 2 and 4 are collectives.  The helpers below take any torch.distributed backend, so the same
 code is exercised with gloo on CPU tensors in tests/test_sharded_gloo.py.
 """
@@ -59,4 +61,37 @@ def allgather_rows(full, n, dist):
     for r in range(world):
         rb, re_ = shard_range(n, r, world)
         full[rb:re_] = gathered[r * per: r * per + (re_ - rb)]
+    return full
+
+
+def vga_nodes(n, rank, world, chunk=4096):
+    """Node indices of `rank`'s VGA sources: chunks c = rank, rank + world, ... of `chunk` nodes."""
+    import numpy as np
+    starts = np.arange(rank * chunk, n, world * chunk, dtype=np.int64)
+    if len(starts) == 0:
+        return np.zeros(0, dtype=np.int64)
+    return np.concatenate([np.arange(b, min(b + chunk, n), dtype=np.int64) for b in starts])
+
+
+def allgather_rows_chunked(full, n, dist, chunk=4096):
+    """full: [n, k] tensor where this rank filled the rows vga_nodes(n, rank, world, chunk);
+    afterwards every rank holds all rows (pure data movement: the values are copied, not summed)."""
+    import numpy as np
+    world, rank = dist.get_world_size(), dist.get_rank()
+    lists = [torch.from_numpy(vga_nodes(n, r, world, chunk)) for r in range(world)]
+    per = max(len(l) for l in lists)
+    k = full.shape[1]
+    mine_idx = lists[rank].to(full.device)
+    mine = torch.zeros((per, k), dtype=full.dtype, device=full.device)
+    mine[: len(mine_idx)] = full[mine_idx]
+    if hasattr(dist, "all_gather_into_tensor") and full.device.type == "cuda":
+        gathered = torch.empty((world * per, k), dtype=full.dtype, device=full.device)
+        dist.all_gather_into_tensor(gathered, mine)
+    else:
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        gathered = torch.cat(parts)
+    for r in range(world):
+        idx = lists[r].to(full.device)
+        full[idx] = gathered[r * per: r * per + len(idx)]
     return full

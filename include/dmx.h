@@ -124,6 +124,10 @@ int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
                    float* out, int64_t* levels);
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin,
                           int64_t src_end, float* out_device);
+/* The same for an arbitrary list of source nodes (host array of n node indices); rows of other
+ * nodes in out_device are left untouched.  Used to interleave multi-GPU shards over the grid. */
+int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
+                               int64_t n, float* out_device);
 
 /* ---- VGA metric step depth (GPU) ----------------------------------------------------------- */
 /* dm_runmethods::runStepDepth with -sdt metric -> MetaGraph::analyseGraph(point_depth_selection=2)

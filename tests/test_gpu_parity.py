@@ -352,3 +352,23 @@ def test_makegraph_certified_moments_equal_serial_chains(ctx, monkeypatch):
     serial = pm.make_graph(ctx).copy(runs=False)["attrs"]
     np.testing.assert_array_equal(fast.view(np.uint32), serial.view(np.uint32))
     np.testing.assert_array_equal(fast.view(np.uint32), A["attrs"].view(np.uint32))
+
+
+def test_vga_source_list_matches_full_run(ctx):
+    """dmx_vga_global_device_list (the interleaved multi-GPU shards): listed rows equal the full
+    run's rows bit for bit, every other row is left untouched."""
+    import torch
+    meta, A = load_case("syn64")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    full = g.vga_visual_global()
+    n = full.shape[0]
+    rng = np.random.default_rng(5)
+    nodes = np.sort(rng.choice(n, n // 3, replace=False))
+    out = torch.full((n, 7), -7.0, dtype=torch.float32, device="cuda")
+    g.vga_visual_global_device_list(out.data_ptr(), nodes)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(got[nodes].view(np.uint32), full[nodes].view(np.uint32))
+    rest = np.setdiff1d(np.arange(n), nodes)
+    assert (got[rest] == -7.0).all()

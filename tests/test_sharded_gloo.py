@@ -43,7 +43,7 @@ def _worker(rank, world, port, q):
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle")):
         sys.path.insert(0, p)
-    from depthmapx_amd.sharded import allgather_blobs, allgather_rows, shard_range
+    from depthmapx_amd.sharded import allgather_blobs, allgather_rows_chunked, shard_range, vga_nodes
     from pyoracle import OracleMap
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -64,8 +64,12 @@ def _worker(rank, world, port, q):
     runs = np.concatenate([p[1] for p in parts])
     om.set_graph(bins, runs)
     out = torch.full((N, 7), -1.0)
-    out[b:e] = torch.from_numpy(om.vga_global(node_begin=b, node_end=e)[b:e])
-    allgather_rows(out, N, dist)
+    # VGA sources: 16-node chunks dealt round-robin (bench.py uses 4096)
+    mine = vga_nodes(N, rank, world, chunk=16)
+    for c0 in range(0, len(mine), 16):
+        cb, ce = int(mine[c0]), int(mine[min(c0 + 16, len(mine)) - 1]) + 1
+        out[cb:ce] = torch.from_numpy(om.vga_global(node_begin=cb, node_end=ce)[cb:ce])
+    allgather_rows_chunked(out, N, dist, chunk=16)
     q.put((rank, bins, runs, out.numpy()))
     dist.destroy_process_group()
 
@@ -94,6 +98,17 @@ def test_two_rank_gloo_matches_single_process():
         np.testing.assert_array_equal(runs, g["runs"])
         np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
         np.testing.assert_array_equal(out.view(np.uint32), A["vga"].view(np.uint32))
+
+
+@pytest.mark.parametrize("n,world,chunk", [(0, 2, 4), (1, 2, 4), (7, 3, 2), (65025, 8, 4096), (998001, 8, 4096)])
+def test_vga_node_chunks_partition(n, world, chunk):
+    from depthmapx_amd.sharded import vga_nodes
+    parts = [vga_nodes(n, r, world, chunk) for r in range(world)]
+    allv = np.sort(np.concatenate(parts)) if n else np.zeros(0, dtype=np.int64)
+    np.testing.assert_array_equal(allv, np.arange(n))
+    if n >= world * chunk * 4:
+        sizes = [len(p) for p in parts]
+        assert max(sizes) - min(sizes) <= chunk
 
 
 @pytest.mark.parametrize("n,world", [(0, 2), (1, 2), (7, 3), (65025, 8)])
