@@ -103,17 +103,25 @@ def main():
     ap.add_argument("--mk-mode", choices=["auto", "shard", "replicate"], default="auto")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-out", default=None, help="rank 0 saves the gathered [N][7] VGA columns (.npy)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (not used by the driver): several ranks on one GPU over gloo
+    if os.environ.get("DMX_FORCE_DEVICE") is not None:
+        local = int(os.environ["DMX_FORCE_DEVICE"])
+    backend = os.environ.get("DMX_DIST_BACKEND", "nccl")   # nccl = RCCL on ROCm
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     import depthmapx_amd as dmx
     from depthmapx_amd.sharded import allgather_blobs, allgather_rows_chunked, shard_range, vga_nodes
 
@@ -247,6 +255,8 @@ def main():
             rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, g, args.cpu_budget)
             rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
         print(json.dumps(rec), flush=True)
+        if args.dump_out:
+            np.save(args.dump_out, out_full.cpu().numpy())
     if world > 1:
         dist.destroy_process_group()
 

@@ -15,6 +15,14 @@ code is exercised with gloo on CPU tensors in tests/test_sharded_gloo.py.
 import torch
 
 
+def _rccl(dist):
+    """all_gather_into_tensor is the RCCL fast path; other backends take the list form."""
+    try:
+        return hasattr(dist, "all_gather_into_tensor") and dist.get_backend() == "nccl"
+    except Exception:
+        return False
+
+
 def shard_range(n, rank, world):
     """Contiguous, balanced split of n units over `world` ranks."""
     return (n * rank) // world, (n * (rank + 1)) // world
@@ -33,7 +41,7 @@ def allgather_blobs(blob, dist, device=None):
     mine = torch.zeros(mx, dtype=torch.uint8, device=device)
     mine[: blob.numel()] = blob
     flat = torch.empty(world * mx, dtype=torch.uint8, device=device)
-    if hasattr(dist, "all_gather_into_tensor") and device.type == "cuda":
+    if _rccl(dist) and device.type == "cuda":
         dist.all_gather_into_tensor(flat, mine)
     else:
         parts = list(flat.view(world, mx).unbind(0))
@@ -51,7 +59,7 @@ def allgather_rows(full, n, dist):
     k = full.shape[1]
     mine = torch.zeros((per, k), dtype=full.dtype, device=full.device)
     mine[: e - b] = full[b:e]
-    if hasattr(dist, "all_gather_into_tensor") and full.device.type == "cuda":
+    if _rccl(dist) and full.device.type == "cuda":
         gathered = torch.empty((world * per, k), dtype=full.dtype, device=full.device)
         dist.all_gather_into_tensor(gathered, mine)
     else:
@@ -84,7 +92,7 @@ def allgather_rows_chunked(full, n, dist, chunk=4096):
     mine_idx = lists[rank].to(full.device)
     mine = torch.zeros((per, k), dtype=full.dtype, device=full.device)
     mine[: len(mine_idx)] = full[mine_idx]
-    if hasattr(dist, "all_gather_into_tensor") and full.device.type == "cuda":
+    if _rccl(dist) and full.device.type == "cuda":
         gathered = torch.empty((world * per, k), dtype=full.dtype, device=full.device)
         dist.all_gather_into_tensor(gathered, mine)
     else:
