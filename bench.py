@@ -101,6 +101,8 @@ def main():
     ap.add_argument("--grid", type=int, default=1000, help="W: region [0,W]^2 at spacing 1 -> (W+1)^2 cells")
     ap.add_argument("--occluders", type=int, default=50)
     ap.add_argument("--mk-mode", choices=["auto", "shard", "replicate"], default="auto")
+    ap.add_argument("--prep-mode", choices=["shard", "replicate"], default="shard",
+                    help="N>1: split the VGA pre-passes by node range (partials all-reduced) or repeat them")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU baseline sampling")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dump-out", default=None, help="rank 0 saves the gathered [N][7] VGA columns (.npy)")
@@ -123,7 +125,8 @@ def main():
         else:
             dist.init_process_group(backend)
     import depthmapx_amd as dmx
-    from depthmapx_amd.sharded import allgather_blobs, allgather_rows_chunked, shard_range, vga_nodes
+    from depthmapx_amd.sharded import (allgather_blobs, allgather_rows_chunked, prep_allreduce, shard_range,
+                                       vga_nodes)
 
     W = args.grid
     mk_mode = args.mk_mode
@@ -164,8 +167,11 @@ def main():
             del flat, blob, shard
         else:
             g = shard
-        # 3. VGA global for this rank's sources (node chunks dealt round-robin: balanced BFS cost)
+        # 3. VGA global for this rank's sources (node chunks dealt round-robin: balanced BFS cost);
+        #    the O(runs) pre-passes are split by contiguous node range, partials all-reduced
         if world > 1:
+            if args.prep_mode == "shard":
+                g.set_prep_shard(b, e, prep_allreduce(dist, dev))
             g.vga_visual_global_device_list(out_full.data_ptr(), vnodes)
         else:
             g.vga_visual_global_device(out_full.data_ptr())
@@ -235,7 +241,8 @@ def main():
             "data": "synthetic (committed occluder CSV, seed 1)",
             "config": {"workload": workload, "grid": "%dx%d" % (info["cols"], info["rows"]), "filled_cells": N,
                        "runs": int(g.info()["nruns"]),
-                       "parallelism": "source-shard x%d (makeGraph %s)" % (world, mk_mode)},
+                       "parallelism": "source-shard x%d (makeGraph %s, VGA prep %s)" % (
+                           world, mk_mode, args.prep_mode if world > 1 else "local")},
             "kernels": {"makegraph_s": mk_s, "vga_s": vga_s,
                         "makegraph_cells_per_s": (N if mk_mode == "replicate" or world == 1 else e - b) / mk_s
                         if mk_s else None,

@@ -40,6 +40,7 @@ SIGNATURES = {
     "dmx_metric_stepdepth": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "dmx_visual_stepdepth": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "dmx_vga_global_device_list": (_i32, [_vp, _vp, _dbl, _i32, _vp, _i64, _vp]),
+    "dmx_graph_set_prep_shard": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "dmx_release_cached_memory": (_i32, []),
     "dmx_ctx_last_stepdepth": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_ctx_last_phase_cycles": (_i32, [_vp, _vp]),
@@ -53,6 +54,10 @@ SIGNATURES = {
     "dmx_chunk_load": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_graph_from_runs": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
 }
+
+
+# dmx_allreduce_fn (include/dmx.h): sum `count` elements of dtype DMX_I32 (0) / DMX_I64 (1) in place
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p)
 
 
 class DmxError(RuntimeError):

@@ -204,6 +204,11 @@ struct dmx_graph {
     DevBuf<unsigned long long> ttvis;  // tile-to-tile full visibility (AND of ftvis over regular cells)
     int tvw = 0;
     DevBuf<unsigned long long> regular_tiles;
+    // sharded VGA preparation (dmx_graph_set_prep_shard): the node scatters run over [prep_b, prep_e)
+    // and the partial buffers are summed across ranks by the caller's all-reduce
+    int64_t prep_b = 0, prep_e = -1;
+    dmx_allreduce_fn prep_fn = nullptr;
+    void* prep_user = nullptr;
 };
 
 namespace {
@@ -794,6 +799,20 @@ int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const*
 }
 
 // ---------------------------------------------------------------- VGA global
+// Node range of this rank's share of the preparation scatters ([0, N) when not sharded).
+static void prep_range(const dmx_graph* g, int64_t& b, int64_t& e) {
+    b = 0; e = g->nnodes;
+    if (g->prep_fn && g->prep_e >= 0) { b = g->prep_b; e = g->prep_e; }
+}
+// Sum a partial device buffer over the ranks (no-op when not sharded).  The stream is drained first:
+// the caller's collective runs on its own stream and returns only once the sum is in place.
+static int prep_allreduce(dmx_graph* g, void* p, int64_t count, int dtype) {
+    if (!g->prep_fn || count <= 0) return DMX_OK;
+    HIPCHK(hipStreamSynchronize(g->ctx->stream));
+    if (g->prep_fn(p, count, dtype, g->prep_user) != 0)
+        return fail(DMX_ERR_STATE, "prep all-reduce callback failed");
+    return DMX_OK;
+}
 // U_f (filled cells that appear in some run: the early-exit universe of every BFS) by range counts,
 // plus the longest-first scan pool.  O(runs) with a few line-prefix passes.
 static int prepare_uf(dmx_graph* g) {
@@ -812,11 +831,14 @@ static int prepare_uf(dmx_graph* g) {
     HIPCHK(g->notuf_tiles.alloc((size_t)tw * th));
     HIPCHK(hipMemsetAsync(cov.p, 0, (size_t)4 * C * 4, s));
     HIPCHK(hipMemsetAsync(cnt.p, 0, 8, s));
-    if (N) {
-        hipLaunchKernelGGL(cov_scatter_kernel, dim3((unsigned)std::min<int64_t>(N, 4096)), dim3(256), 0, s, cols, rows, N,
-                           g->node_run_start.p, g->node_nruns.p, g->pool.p, cov.p);
+    int64_t pb, pe;
+    prep_range(g, pb, pe);
+    if (pe > pb) {
+        hipLaunchKernelGGL(cov_scatter_kernel, dim3((unsigned)std::min<int64_t>(pe - pb, 4096)), dim3(256), 0, s, cols,
+                           rows, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb, g->pool.p, cov.p);
         HIPCHK(hipGetLastError());
     }
+    if (int rc = prep_allreduce(g, cov.p, (int64_t)4 * C, DMX_I32)) return rc;
     hipLaunchKernelGGL(cov_lines_kernel, dim3((cols + rows + 127) / 128, 4), dim3(128), 0, s, cols, rows, cov.p);
     HIPCHK(hipGetLastError());
     hipLaunchKernelGGL(cov_tiles_kernel, dim3((tw * th + 255) / 256), dim3(256), 0, s, cols, rows, tw, th,
@@ -869,17 +891,22 @@ static int prepare_symmetry(dmx_graph* g) {
     HIPCHK(flist.alloc(kSpecLimit));
     HIPCHK(fcount.alloc(1));
     HIPCHK(hipMemsetAsync(diff.p, 0, (size_t)4 * C * 8, s));
+    HIPCHK(hipMemsetAsync(ho.p, 0, (size_t)std::max<int64_t>(N, 1) * 8, s));
     HIPCHK(hipMemsetAsync(fcount.p, 0, 4, s));
     const int maxlines = cols + rows;
     hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
                        g->pm->d_cell_node.p, prefix.p, 0);
     HIPCHK(hipGetLastError());
-    if (N) {
-        hipLaunchKernelGGL(sym_scatter_kernel, dim3((unsigned)std::min<int64_t>(N, 4096)), dim3(256), 0, s, cols, rows,
-                           g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, prefix.p, diff.p,
-                           ho.p);
+    int64_t pb, pe;
+    prep_range(g, pb, pe);
+    if (pe > pb) {
+        hipLaunchKernelGGL(sym_scatter_kernel, dim3((unsigned)std::min<int64_t>(pe - pb, 4096)), dim3(256), 0, s, cols,
+                           rows, g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb,
+                           g->pool.p, prefix.p, diff.p, ho.p + pb);
         HIPCHK(hipGetLastError());
     }
+    if (int rc = prep_allreduce(g, diff.p, (int64_t)4 * C, DMX_I64)) return rc;
+    if (int rc = prep_allreduce(g, ho.p, N, DMX_I64)) return rc;
     hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
                        g->pm->d_cell_node.p, diff.p, 1);
     HIPCHK(hipGetLastError());
@@ -1003,7 +1030,19 @@ static int prepare_tiles(dmx_graph* g) {
     const bool ftv_on = !(ftv_env && atoi(ftv_env) == 0);
     // (the tile kernel reads a row as 4 words a lane: tvw <= 256, true for every grid whose frontier
     // bitmap fits the LDS)
-    if (tv_on && N && tvw <= 256 && tv_bytes * (ftv_on ? 2 : 1) <= free_b / 4 && tv_bytes <= (32ull << 30)) {
+    bool tv_build = tv_on && N && tvw <= 256 && tv_bytes * (ftv_on ? 2 : 1) <= free_b / 4 && tv_bytes <= (32ull << 30);
+    if (g->prep_fn) {
+        // every rank must take the same branch (the rows are all-reduced): build only if all can
+        DevBuf<int64_t> veto;
+        HIPCHK(veto.alloc(1));
+        const int64_t v = tv_build ? 0 : 1;
+        HIPCHK(hipMemcpyAsync(veto.p, &v, 8, hipMemcpyHostToDevice, s));
+        if (int rc = prep_allreduce(g, veto.p, 1, DMX_I64)) return rc;
+        int64_t vs = 0;
+        HIPCHK(hipMemcpy(&vs, veto.p, 8, hipMemcpyDeviceToHost));
+        tv_build = vs == 0;
+    }
+    if (tv_build) {
         HIPCHK(g->tvis.alloc(Ct * tvw));
         HIPCHK(hipMemsetAsync(g->tvis.p, 0, tv_bytes, s));
         if (ftv_on) {
@@ -1013,11 +1052,19 @@ static int prepare_tiles(dmx_graph* g) {
         const int ncw = (nt + 3) / 4;
         const size_t tv_lds = ((size_t)(ncw + 1) / 2 + (size_t)TV_WAVES * (tvw + (ncw + 1) / 2)) * 8;
         if (tv_lds > 150 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the tile-visibility pass");
-        const int64_t nb = std::min<int64_t>((N + TV_WAVES - 1) / TV_WAVES, (int64_t)ctx->num_cu * 16);
-        hipLaunchKernelGGL(tile_vis_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), tv_lds, s, rows, tw,
-                           th, g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p,
-                           g->notuf_tiles.p, g->tvis.p, ftv_on ? g->ftvis.p : nullptr);
-        HIPCHK(hipGetLastError());
+        int64_t pb, pe;
+        prep_range(g, pb, pe);
+        if (pe > pb) {
+            const int64_t nb = std::min<int64_t>((pe - pb + TV_WAVES - 1) / TV_WAVES, (int64_t)ctx->num_cu * 16);
+            hipLaunchKernelGGL(tile_vis_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), tv_lds, s, rows, tw, th,
+                               g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb,
+                               g->pool.p, g->notuf_tiles.p, g->tvis.p, ftv_on ? g->ftvis.p : nullptr);
+            HIPCHK(hipGetLastError());
+        }
+        // rows of distinct nodes are disjoint: the sum over ranks is their union
+        if (int rc = prep_allreduce(g, g->tvis.p, Ct * tvw, DMX_I64)) return rc;
+        if (ftv_on)
+            if (int rc = prep_allreduce(g, g->ftvis.p, Ct * tvw, DMX_I64)) return rc;
         const char* tt_env = getenv("DMX_VGA_TTVIS");
         if (ftv_on && !(tt_env && atoi(tt_env) == 0)) {
             HIPCHK(g->ttvis.alloc((size_t)2 * nt * tvw));   // ttvis, then ttany
@@ -1349,6 +1396,19 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
     HIPCHK(d_list.alloc(lst.size()));
     HIPCHK(hipMemcpyAsync(d_list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     return vga_tile_impl(ctx, g, radius, gates_only, 0, n, out_device, true, nullptr, tw, th, nullptr, 0, nullptr, d_list.p);
+}
+
+int dmx_graph_set_prep_shard(dmx_graph* g, int64_t node_begin, int64_t node_end, dmx_allreduce_fn fn, void* user) {
+    if (!g) return fail(DMX_ERR_ARG, "bad arguments");
+    if (fn && (node_begin < 0 || node_end < node_begin || node_end > g->nnodes))
+        return fail(DMX_ERR_ARG, "prep node range out of bounds");
+    if (g->uf_count >= 0 || g->symmetric >= 0 || g->tiles_ready)
+        return fail(DMX_ERR_STATE, "VGA preparation already done on this graph");
+    g->prep_fn = fn;
+    g->prep_user = fn ? user : nullptr;
+    g->prep_b = fn ? node_begin : 0;
+    g->prep_e = fn ? node_end : -1;
+    return DMX_OK;
 }
 
 // ---------------------------------------------------------------- metric step depth

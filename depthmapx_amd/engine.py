@@ -234,6 +234,26 @@ class Graph:
         N.check(N.lib().dmx_visual_stepdepth(self.ctx.h, self.h, N.ptr(arr), len(arr), N.ptr(out)))
         return out
 
+    def set_prep_shard(self, node_begin, node_end, allreduce):
+        """Split the VGA preparation over ranks (dmx_graph_set_prep_shard): this rank scatters nodes
+        [node_begin, node_end); allreduce(ptr, count, dtype) must sum the device buffer in place over
+        all ranks (dtype 0 = int32, 1 = int64) and return 0.  allreduce=None undoes it."""
+        if allreduce is None:
+            self._prep_cb = None
+            N.check(N.lib().dmx_graph_set_prep_shard(self.h, 0, 0, None, None))
+            return
+
+        def cb(ptr, count, dtype, user):
+            try:
+                return int(allreduce(ptr, count, dtype) or 0)
+            except Exception:                     # an exception must not unwind through C
+                import traceback
+                traceback.print_exc()
+                return -1
+        self._prep_cb = N.ALLREDUCE_FN(cb)        # kept alive as long as the graph
+        N.check(N.lib().dmx_graph_set_prep_shard(self.h, int(node_begin), int(node_end),
+                                                 ctypes.cast(self._prep_cb, ctypes.c_void_p), None))
+
     def vga_visual_global_device_list(self, out_dev_ptr, nodes, radius=-1.0, gates_only=False):
         """VGA global for the listed source nodes only (rows of the others untouched); device output."""
         arr = np.ascontiguousarray(nodes, dtype=np.int64)

@@ -6,7 +6,8 @@ Per step
      source, so contiguous ranges balance);
   2. all-gather of the run-length graph shards (ragged byte blobs, padded to the largest) so every
      rank holds the whole graph -- VGA BFS from any source can reach any node;
-  3. VGA global for the rank's VGA sources: fixed-size node chunks dealt round-robin over the
+  3. VGA global for the rank's VGA sources (its preparation pre-passes split by contiguous node
+     range, partial buffers all-reduced: Graph.set_prep_shard + prep_allreduce): fixed-size node chunks dealt round-robin over the
      ranks (vga_nodes), because the BFS cost of a source depends on where it sits in the plan;
   4. all-gather of the owned rows of the 7 float columns (allgather_rows_chunked).
 Only 2 and 4 are collectives.  The helpers below take any torch.distributed backend, so the same
@@ -70,6 +71,33 @@ def allgather_rows(full, n, dist):
         rb, re_ = shard_range(n, r, world)
         full[rb:re_] = gathered[r * per: r * per + (re_ - rb)]
     return full
+
+
+def device_view(ptr, count, dtype, device):
+    """Zero-copy torch view of `count` int32 (dtype 0) / int64 (dtype 1) elements of device memory
+    owned by libdmx (CUDA array interface; the memory stays libdmx's)."""
+    class _View:
+        pass
+    v = _View()
+    v.__cuda_array_interface__ = {"shape": (int(count),), "typestr": "<i4" if dtype == 0 else "<i8",
+                                  "data": (int(ptr), False), "version": 2, "strides": None}
+    return torch.as_tensor(v, device=device)
+
+
+def prep_allreduce(dist, device):
+    """The all-reduce callback of Graph.set_prep_shard: SUM over ranks in place (RCCL on the GPU;
+    other backends reduce through a staging copy)."""
+    def fn(ptr, count, dtype):
+        t = device_view(ptr, count, dtype, device)
+        if _rccl(dist):
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        else:
+            host = t.cpu()
+            dist.all_reduce(host, op=dist.ReduceOp.SUM)
+            t.copy_(host)
+        torch.cuda.synchronize(device)
+        return 0
+    return fn
 
 
 def vga_nodes(n, rank, world, chunk=4096):

@@ -128,6 +128,17 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
  * nodes in out_device are left untouched.  Used to interleave multi-GPU shards over the grid. */
 int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
                                int64_t n, float* out_device);
+/* Multi-GPU share of the VGA preparation (no reference counterpart: the reference prepares nothing;
+ * this splits our own O(runs) pre-passes).  Every rank holds the whole graph; the per-node scatters
+ * (covered-cell counts, in-set sums, tile-visibility rows) then run over nodes [node_begin, node_end)
+ * only and each partial device buffer is handed to fn, which must sum it in place over all ranks
+ * (an all-reduce SUM of `count` elements of dtype DMX_I32 / DMX_I64, returning 0 on success) before
+ * returning.  Every rank must call this with the same fn semantics before its first VGA call on g;
+ * fn is called the same number of times, in the same order, on every rank.  fn = NULL undoes it. */
+#define DMX_I32 0
+#define DMX_I64 1
+typedef int (*dmx_allreduce_fn)(void* device_ptr, int64_t count, int dtype, void* user);
+int dmx_graph_set_prep_shard(dmx_graph* g, int64_t node_begin, int64_t node_end, dmx_allreduce_fn fn, void* user);
 
 /* ---- VGA metric step depth (GPU) ----------------------------------------------------------- */
 /* dm_runmethods::runStepDepth with -sdt metric -> MetaGraph::analyseGraph(point_depth_selection=2)

@@ -372,3 +372,79 @@ def test_vga_source_list_matches_full_run(ctx):
     np.testing.assert_array_equal(got[nodes].view(np.uint32), full[nodes].view(np.uint32))
     rest = np.setdiff1d(np.arange(n), nodes)
     assert (got[rest] == -7.0).all()
+
+
+def test_vga_prep_shard_single_rank_identity(ctx):
+    """dmx_graph_set_prep_shard with a world of one (the all-reduce is the identity): same columns
+    as the unsharded run, and the callback sees the six partial buffers in the documented order."""
+    import torch
+    meta, A = load_case("gallery")
+    pm = _map(meta)
+    full = pm.make_graph(ctx).vga_visual_global()
+    g = pm.make_graph(ctx)
+    n = full.shape[0]
+    calls = []
+    g.set_prep_shard(0, n, lambda ptr, count, dtype: calls.append((count, dtype)) or 0)
+    out = torch.full((n, 7), -1.0, dtype=torch.float32, device="cuda")
+    g.vga_visual_global_device_list(out.data_ptr(), np.arange(n))
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), full.view(np.uint32))
+    C = meta["cols"] * meta["rows"]
+    assert calls[:4] == [(4 * C, 0), (4 * C, 1), (n, 1), (1, 1)]
+    assert len(calls) == 6 and calls[4] == calls[5] and calls[4][1] == 1
+
+
+@pytest.mark.parametrize("name", ["gallery", "syn64"])
+def test_vga_prep_shard_two_ranks_threads(ctx, name):
+    """Two emulated ranks (threads, each with its own context and stream on cuda:0) split the VGA
+    preparation by node range and sum the partial buffers through a barrier -- the all-reduce that
+    bench.py does with RCCL; each rank's interleaved source rows must equal the unsharded run."""
+    import threading
+    import torch
+    from depthmapx_amd.sharded import device_view, shard_range, vga_nodes
+    meta, A = load_case(name)
+    pm = _map(meta)
+    full = pm.make_graph(ctx).vga_visual_global()
+    n = full.shape[0]
+    ctxs = [dmx.Context(0), dmx.Context(0)]
+    graphs = [pm.make_graph(c) for c in ctxs]
+    bar = threading.Barrier(2, timeout=60)
+    slots = [None, None]
+    dev = torch.device("cuda", 0)
+
+    def make_fn(r):
+        def fn(ptr, count, dtype):
+            t = device_view(ptr, count, dtype, dev)
+            slots[r] = t.clone()
+            torch.cuda.synchronize()
+            bar.wait()
+            t.copy_(slots[0] + slots[1])
+            torch.cuda.synchronize()
+            bar.wait()
+            return 0
+        return fn
+
+    outs = [torch.full((n, 7), -1.0, dtype=torch.float32, device="cuda") for _ in range(2)]
+    lists = [vga_nodes(n, r, 2, chunk=256) for r in range(2)]
+    errs = [None, None]
+    for r in range(2):
+        graphs[r].set_prep_shard(*shard_range(n, r, 2), make_fn(r))
+
+    def run(r):
+        try:
+            graphs[r].vga_visual_global_device_list(outs[r].data_ptr(), lists[r])
+        except Exception as ex:   # surfaced below
+            errs[r] = ex
+            bar.abort()
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert errs == [None, None], errs
+    torch.cuda.synchronize()
+    got = np.full_like(full, -1.0)
+    for r in range(2):
+        got[lists[r]] = outs[r].cpu().numpy()[lists[r]]
+    np.testing.assert_array_equal(got.view(np.uint32), full.view(np.uint32))
