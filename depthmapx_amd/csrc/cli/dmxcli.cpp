@@ -479,7 +479,6 @@ struct Vga : Mode {
         load_map(C, d, m);
         std::cout << "Getting options..." << std::flush;
         if (mode != VISIBILITY) throw RuntimeException("Only -vm visibility is part of the accelerated path");
-        if (local) throw RuntimeException("-vl (visual local) is not part of the accelerated path yet");
         double r = -1.0;
         if (global) {
             if (radius != "n") {
@@ -491,8 +490,15 @@ struct Vga : Mode {
             }
         }
         std::cout << " ok\nAnalysing graph..." << std::flush;
-        std::vector<float> out((size_t)m.nnodes * 7, -1.0f);
-        if (global) timed(perf, "Run VGA", [&] { check(dmx_vga_global(C.ctx, m.g, r, 0, 0, -1, out.data(), nullptr)); });
+        std::vector<float> out((size_t)m.nnodes * 7, -1.0f), lout;
+        // analyseGraph runs VGAVisualLocal before VGAVisualGlobal (mgraph.cpp:349-356), one "Run VGA" span
+        timed(perf, "Run VGA", [&] {
+            if (local) {
+                lout.assign((size_t)m.nnodes * 3, -1.0f);
+                check(dmx_vga_local(C.ctx, m.g, 0, 0, -1, lout.data()));
+            }
+            if (global) check(dmx_vga_global(C.ctx, m.g, r, 0, 0, -1, out.data(), nullptr));
+        });
         std::cout << " ok\nWriting out result..." << std::flush;
         timed(perf, "Writing graph", [&] {
             // VGAVisualGlobal::run column insertion order and setValue pattern (vgavisualglobal.cpp:38-193)
@@ -503,6 +509,34 @@ struct Vga : Mode {
                                    {"Visual Mean Depth", 4, false}, {"Visual Node Count", 5, false},
                                    {"Visual Relativised Entropy", 6, false}};
             int displayed = -1;
+            if (local && !a.simple) {
+                // VGAVisualLocal: three columns (vgavisuallocal.cpp:31-35), set for every source it does
+                // not skip (context-filled odd cells), displayed = clustering coefficient (:109-112)
+                int32_t cols_ = 0, rows_ = 0;
+                check(dmx_pointmap_info(m.pm, &cols_, &rows_, nullptr, nullptr, nullptr));
+                std::vector<int32_t> st((size_t)cols_ * rows_);
+                check(dmx_pointmap_state(m.pm, st.data()));
+                std::vector<uint8_t> ran((size_t)m.nnodes, 0);
+                int64_t k = 0;
+                for (int64_t c = 0; c < (int64_t)st.size() && k < m.nnodes; c++) {
+                    if (!(st[c] & 0x2)) continue;   // Point::FILLED; nodes are the filled cells, x-major
+                    const int64_t x = c / rows_, y = c % rows_;
+                    ran[k++] = !((st[c] & 0x8) && !(x % 2 == 0 && y % 2 == 0));   // Point::CONTEXTFILLED
+                }
+                const char* lnames[3] = {"Visual Clustering Coefficient", "Visual Control", "Visual Controllability"};
+                for (int j = 0; j < 3; j++) {
+                    Column c;
+                    c.name = lnames[j];
+                    c.values.resize((size_t)m.nnodes);
+                    c.set.resize((size_t)m.nnodes);
+                    for (int64_t i = 0; i < m.nnodes; i++) {
+                        c.values[i] = ran[i] ? lout[i * 3 + j] : -1.0f;
+                        c.set[i] = ran[i];
+                    }
+                    if (j == 0) displayed = (int)m.columns.size();
+                    m.columns.push_back(c);
+                }
+            }
             if (global)
                 for (auto& sp : specs) {
                     if (a.simple && !sp.simple) continue;

@@ -25,6 +25,7 @@
 #include "kernels/vga_do.hip"
 #include "kernels/vga_tile.hip"
 #include "kernels/stepdepth.hip"
+#include "kernels/vga_local.hip"
 
 using namespace dmx;
 
@@ -1396,6 +1397,54 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
     HIPCHK(d_list.alloc(lst.size()));
     HIPCHK(hipMemcpyAsync(d_list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     return vga_tile_impl(ctx, g, radius, gates_only, 0, n, out_device, true, nullptr, tw, th, nullptr, 0, nullptr, d_list.p);
+}
+
+// ---------------------------------------------------------------- VGA visual local
+int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t sb, int64_t se, float* out) {
+    if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");
+    if (g->node_begin != 0 || g->node_end != g->nnodes)
+        return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
+    HIPCHK(hipSetDevice(ctx->device));
+    const int64_t N = g->nnodes;
+    if (se < 0 || se > N) se = N;
+    if (sb < 0 || sb > se) return fail(DMX_ERR_ARG, "source range out of bounds");
+    PointMapHost& h = *g->pm->host;
+    const int cols = h.cols(), rows = h.rows();
+    const int tw = (cols + 7) / 8, th = (rows + 7) / 8, nt = tw * th;
+    const size_t lds = (size_t)2 * nt * 8;
+    if (lds > 150 * 1024)
+        return fail(DMX_ERR_UNSUPPORTED, "grid too large for VGA visual local (two tile bitmaps must fit the LDS)");
+    hipStream_t s = ctx->stream;
+    DevBuf<int32_t> nsz;
+    DevBuf<float> d_out;
+    HIPCHK(nsz.alloc(std::max<int64_t>(N, 1)));
+    HIPCHK(d_out.alloc((size_t)std::max<int64_t>(N, 1) * 3));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * 8, s));
+    HIPCHK(hipEventRecord(ctx->ev0, s));
+    if (se > sb) {
+        hipLaunchKernelGGL(node_size_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, s, N, g->node_run_start.p,
+                           g->node_nruns.p, g->pool.p, nsz.p);
+        HIPCHK(hipGetLastError());
+        int occ = 0;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_local_kernel, VL_THREADS, lds));
+        const int64_t nb = std::min<int64_t>(se - sb, (int64_t)ctx->num_cu * std::max(occ, 1));
+        hipLaunchKernelGGL(vga_local_kernel, dim3((unsigned)nb), dim3(VL_THREADS), lds, s, cols, rows, tw, th,
+                           g->pm->d_node_cell.p, g->pm->d_cell_node.p, g->pm->d_node_flags.p, g->node_run_start.p,
+                           g->node_nruns.p, g->pool.p, nsz.p, sb, se, gates_only, d_out.p, ctx->stats.p);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ctx->ev1, s));
+    HIPCHK(hipStreamSynchronize(s));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_vga_s = ms * 1e-3;
+    if (se > sb)
+        HIPCHK(hipMemcpy(out + sb * 3, d_out.p + sb * 3, (size_t)(se - sb) * 3 * 4, hipMemcpyDeviceToHost));
+    unsigned long long st0 = 0;
+    HIPCHK(hipMemcpy(&st0, ctx->stats.p, 8, hipMemcpyDeviceToHost));
+    ctx->last_stats[4] = (long long)st0;   // neighbour runs walked
+    ctx->last_stats[7] = se - sb;
+    return DMX_OK;
 }
 
 int dmx_graph_set_prep_shard(dmx_graph* g, int64_t node_begin, int64_t node_end, dmx_allreduce_fn fn, void* user) {

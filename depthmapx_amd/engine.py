@@ -17,6 +17,8 @@ from . import _native as N
 MAKEGRAPH_COLUMNS = ["Connectivity", "Point First Moment", "Point Second Moment"]
 STEPDEPTH_COLUMNS = ["Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length",
                      "Metric Straight-Line Distance"]
+# VGAVisualLocal column insertion order (vgavisuallocal.cpp:31-35), also alphabetical
+VGA_LOCAL_COLUMNS = ["Visual Clustering Coefficient", "Visual Control", "Visual Controllability"]
 VGA_COLUMNS = ["Visual Entropy", "Visual Integration [HH]", "Visual Integration [P-value]",
                "Visual Integration [Tekl]", "Visual Mean Depth", "Visual Node Count",
                "Visual Relativised Entropy"]
@@ -201,6 +203,15 @@ class Graph:
         N.check(N.lib().dmx_vga_global(self.ctx.h, self.h, float(radius), int(bool(gates_only)), int(src_begin),
                                        int(src_end), N.ptr(out), N.ptr(lv)))
         return (out, lv) if levels else out
+
+    def vga_visual_local(self, gates_only=False, src_begin=0, src_end=-1):
+        """VGA -vm visibility -vl (VGAVisualLocal::run, vgamodules/vgavisuallocal.cpp:23-117) on the
+        GPU: [N][3] float32 in VGA_LOCAL_COLUMNS order (-1: skipped source or neighbourhood <= 1)."""
+        n = self.info()["nnodes"]
+        out = np.full((n, 3), -1.0, dtype=np.float32)
+        N.check(N.lib().dmx_vga_local(self.ctx.h, self.h, int(bool(gates_only)), int(src_begin), int(src_end),
+                                      N.ptr(out)))
+        return out
 
     def metric_step_depth(self, points=None, cells=None):
         """STEPDEPTH -sdt metric (dm_runmethods::runStepDepth, depthmapXcli/runmethods.cpp:735-778):

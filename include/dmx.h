@@ -128,6 +128,13 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
  * nodes in out_device are left untouched.  Used to interleave multi-GPU shards over the grid. */
 int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
                                int64_t n, float* out_device);
+/* ---- VGA visual local (GPU) ----------------------------------------------------------------- */
+/* MetaGraph::analyseGraph(OUTPUT_VISUAL, local) -> VGAVisualLocal(gates_only).run
+ * (salalib/mgraph.cpp:349-353, vgamodules/vgavisuallocal.cpp:23-117) for source nodes
+ * [src_begin, src_end) (src_end < 0: all).  out: host [N][3] in node order, rows outside the range
+ * untouched: Visual Clustering Coefficient, Visual Control, Visual Controllability (-1 for skipped
+ * sources and neighbourhoods of <= 1 cell).  DMX_ERR_UNSUPPORTED for grids above ~780^2 cells. */
+int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t src_begin, int64_t src_end, float* out);
 /* Multi-GPU share of the VGA preparation (no reference counterpart: the reference prepares nothing;
  * this splits our own O(runs) pre-passes).  Every rank holds the whole graph; the per-node scatters
  * (covered-cell counts, in-set sums, tile-visibility rows) then run over nodes [node_begin, node_end)

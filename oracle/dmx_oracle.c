@@ -1153,3 +1153,94 @@ int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
     free(cur.p); free(next.p); free(miscs); free(extx); free(exty);
     return 0;
 }
+
+/* ---------------------------------------------------------------- VGA visual local */
+/* Visit the cells of node nd in Node::first/next order (ngraph.cpp:158-190, Bin::first/next
+ * ngraph.cpp:392-416): bins 0..31, runs in order, each run from its start along the bin direction
+ * until col(dir) passes the run end (col = y for vertical bins, x otherwise). */
+#define WALK_NODE_CELLS(m, nd, CELL_BODY)                                                          \
+    do {                                                                                           \
+        const Run* r_ = (nd)->runs;                                                                \
+        for (int b_ = 0; b_ < 32; b_++) {                                                          \
+            const char dir_ = (nd)->dir[b_];                                                       \
+            for (int k_ = 0; k_ < (nd)->nruns[b_]; k_++, r_++) {                                   \
+                int px = r_->x0, py = r_->y0;                                                      \
+                const int endc_ = (dir_ & D_V) ? r_->y1 : r_->x1;                                  \
+                while (((dir_ & D_V) ? py : px) <= endc_) {                                        \
+                    const int64_t cell = cidx((m), px, py);                                        \
+                    CELL_BODY;                                                                     \
+                    switch (dir_) {                                                                \
+                    case D_PD: px++; py++; break;                                                  \
+                    case D_ND: px++; py--; break;                                                  \
+                    case D_V: py++; break;                                                         \
+                    default: px++; break;                                                          \
+                    }                                                                              \
+                }                                                                                  \
+            }                                                                                      \
+        }                                                                                          \
+    } while (0)
+
+static int cmp_i64(const void* a, const void* b) {
+    const int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
+    return x < y ? -1 : x > y;
+}
+
+/* VGAVisualLocal::run (vgavisuallocal.cpp:23-117).  Per source: neighbourhood = Node::contents
+ * (ngraph.cpp:184-191: cells of every run, addIfNotExists), sorted by PixelRef (x-major cell order,
+ * pixelref.h:95-98).  For each neighbour that is FILLED with a node: retro_size = cells iterated in
+ * its node, intersect_size = those in the neighbourhood, totalneighbourhood gains the ones not yet
+ * in it; control += 1.0f/float(retro_size) (float, sorted order), cluster += intersect_size (int).
+ * The std::find membership tests are restated with per-cell marks (same sets, same counts). */
+int dmxo_vga_local(dmxo_map* m, int gates_only, int64_t nb, int64_t ne, int nthreads, float* out) {
+    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
+    if (ne < 0 || ne > N) ne = N;
+    if (nb < 0) nb = 0;
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        uint8_t* inhood = (uint8_t*)calloc(C, 1);
+        uint8_t* intotal = (uint8_t*)calloc(C, 1);
+        int64_t* hood = (int64_t*)malloc((C + 1) * sizeof(int64_t));
+        int64_t* total = (int64_t*)malloc((C + 1) * sizeof(int64_t));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t k = nb; k < ne; k++) {
+            float* o = out + 3 * k;
+            for (int i = 0; i < 3; i++) o[i] = -1.0f;
+            const int32_t c = m->node_cell[k];
+            const int cx = c / m->rows, cy = c % m->rows;
+            if (((m->state[c] & ST_CONTEXTFILLED) && !(cx % 2 == 0 && cy % 2 == 0)) || gates_only) continue;
+            int64_t nh = 0, ntot = 0;
+            WALK_NODE_CELLS(m, &m->nodes[k], {
+                if (!inhood[cell]) { inhood[cell] = 1; hood[nh++] = cell; }
+            });
+            qsort(hood, (size_t)nh, sizeof(int64_t), cmp_i64);
+            int32_t cluster = 0;   /* int in the reference; wraps like it past 2^31 */
+            float control = 0.0f;
+            for (int64_t i = 0; i < nh; i++) {
+                const int64_t nc = hood[i];
+                if (!(m->state[nc] & ST_FILLED) || m->node_of_cell[nc] < 0) continue;
+                int32_t retro = 0, inter = 0;
+                WALK_NODE_CELLS(m, &m->nodes[m->node_of_cell[nc]], {
+                    retro++;
+                    if (inhood[cell]) inter++;
+                    if (!intotal[cell]) { intotal[cell] = 1; total[ntot++] = cell; }
+                });
+                control += 1.0f / (float)retro;
+                cluster = (int32_t)((uint32_t)cluster + (uint32_t)inter);
+            }
+            if (nh > 1) {
+                o[0] = (float)(cluster / ((double)nh * ((double)nh - 1.0)));
+                o[1] = control;
+                o[2] = (float)((double)nh / (double)ntot);
+            }
+            for (int64_t i = 0; i < nh; i++) inhood[hood[i]] = 0;
+            for (int64_t i = 0; i < ntot; i++) intotal[total[i]] = 0;
+        }
+        free(inhood); free(intotal); free(hood); free(total);
+    }
+    return 0;
+}

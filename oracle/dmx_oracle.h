@@ -61,6 +61,11 @@ int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t node_beg
 int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
 /* VGAVisualGlobalDepth::run (vgamodules/vgavisualglobaldepth.cpp:23-77): out [N], -1 unreached. */
 int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
+/* VGAVisualLocal::run (vgamodules/vgavisuallocal.cpp:23-117) for source nodes [node_begin,
+ * node_end).  out [N][3]: Visual Clustering Coefficient, Visual Control, Visual Controllability;
+ * -1 for skipped sources (context-filled odd cells, gates_only) and for neighbourhoods of <= 1 cell;
+ * rows outside the range untouched. */
+int dmxo_vga_local(dmxo_map* m, int gates_only, int64_t node_begin, int64_t node_end, int nthreads, float* out);
 
 #ifdef __cplusplus
 }

@@ -48,6 +48,8 @@ def lib():
         L.dmxo_metric_stepdepth.argtypes = [vp, vp, i64, vp]
         L.dmxo_visual_stepdepth.restype = i32
         L.dmxo_visual_stepdepth.argtypes = [vp, vp, i64, vp]
+        L.dmxo_vga_local.restype = i32
+        L.dmxo_vga_local.argtypes = [vp, i32, i64, i64, i32, vp]
         L.dmxo_vga_global.restype = i32
         L.dmxo_vga_global.argtypes = [vp, dbl, i32, i64, i64, i32, vp, vp]
         _lib = L
@@ -138,4 +140,11 @@ class OracleMap:
         sel = np.ascontiguousarray(sel_cells, dtype=np.int32)
         out = np.full(self.num_nodes, -1.0, dtype=np.float32)
         lib().dmxo_visual_stepdepth(self.h, _p(sel), len(sel), _p(out))
+        return out
+
+    def vga_local(self, gates_only=False, node_begin=0, node_end=-1, threads=1):
+        """VGAVisualLocal::run: [N][3] Visual Clustering Coefficient, Visual Control, Visual
+        Controllability (-1: skipped source or neighbourhood of <= 1 cell)."""
+        out = np.full((self.num_nodes, 3), -1.0, dtype=np.float32)
+        lib().dmxo_vga_local(self.h, int(gates_only), node_begin, node_end, threads, _p(out))
         return out

@@ -73,7 +73,7 @@ static void dumpVga(PointMap& pm, const std::string& path) {
 int main(int argc, char** argv) {
     std::string linesCsv, graphIn, outDir = ".", writeGraph;
     double spacing = -1, maxdist = -1, radius = -1;
-    bool boundary = false, vga = false, roundtrip = false;
+    bool boundary = false, vga = false, roundtrip = false, vlocal = false;
     long sources = 0;
     std::vector<Point2f> fills, stepPoints;
     for (int i = 1; i < argc; i++) {
@@ -88,6 +88,7 @@ int main(int argc, char** argv) {
         else if (a == "--boundary") boundary = true;
         else if (a == "--vga") vga = true;
         else if (a == "--roundtrip") roundtrip = true;
+        else if (a == "--vlocal") vlocal = true;
         else if (a == "--out") outDir = next();
         else if (a == "--write-graph") writeGraph = next();
         else if (a == "--sources") sources = atol(next().c_str());
@@ -287,14 +288,35 @@ int main(int argc, char** argv) {
         if (writeGraph.empty()) remove(g.c_str());
     }
 
+    // VGA visual local (-vl: mgraph.cpp:349-353 -> VGAVisualLocal::run), last so that its columns do
+    // not travel through the round trip above
+    double tvl = 0;
+    if (vlocal) {
+        Options opt;
+        opt.output_type = Options::OUTPUT_VISUAL;
+        opt.local = 1;
+        opt.global = 0;
+        opt.radius = -1;
+        auto a = std::chrono::steady_clock::now();
+        mg.analyseGraph(nullptr, opt, false);
+        auto b = std::chrono::steady_clock::now();
+        tvl = std::chrono::duration<double>(b - a).count();
+        AttributeTable& at = pm.getAttributeTable();
+        const char* names[3] = {"Visual Clustering Coefficient", "Visual Control", "Visual Controllability"};
+        std::vector<float> out;
+        for (auto it = at.begin(); it != at.end(); ++it)
+            for (auto n : names) out.push_back(it->getRow().getValue((int)at.getColumnIndex(n)));
+        dump(outDir + "/vlocal.bin", out);
+    }
+
     FILE* f = fopen((outDir + "/grid.txt").c_str(), "w");
     fprintf(f, "spacing %.17g\ncols %zu\nrows %zu\n", pm.m_spacing, cols, rows);
     fprintf(f, "bottom_left %.17g %.17g\n", pm.m_bottom_left.x, pm.m_bottom_left.y);
     fprintf(f, "region %.17g %.17g %.17g %.17g\n", reg.bottom_left.x, reg.bottom_left.y, reg.top_right.x,
             reg.top_right.y);
     fprintf(f, "filled %d\nnodes %ld\nruns %zu\n", pm.m_filled_point_count, nodes, runs.size() / 4);
-    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\nt_stepdepth %.6f\nt_vstepdepth %.6f\n",
-            std::chrono::duration<double>(t1 - t0).count(), tv, tvrt, tsd, tvsd);
+    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\nt_stepdepth %.6f\nt_vstepdepth %.6f\nt_vlocal %.6f\n",
+            std::chrono::duration<double>(t1 - t0).count(), tv, tvrt, tsd, tvsd, tvl);
     fclose(f);
     printf("ok nodes %ld runs %zu t_makegraph %.3f t_vga %.3f\n", nodes, runs.size() / 4,
            std::chrono::duration<double>(t1 - t0).count(), tv);

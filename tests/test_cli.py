@@ -128,3 +128,40 @@ def test_cli_pipeline_matches_reference(tmp_path):
     cols4 = {c[0]: c[1] for c in graphio.read_chunk(chunk(g4))["columns"]}
     want = om.visual_stepdepth(np.array([17 * rows + 17], np.int32))
     np.testing.assert_array_equal(cols4["Visual Step Depth"], want)
+
+
+@pytest.mark.gpu
+def test_cli_vga_local_and_global(tmp_path):
+    """VGA -vm visibility -vl -vg -vr n: the local columns come first (VGAVisualLocal runs before
+    VGAVisualGlobal, mgraph.cpp:349-356) and equal the C restatement on the re-read graph; the
+    global columns equal the reference CLI's."""
+    from depthmapx_amd import VGA_COLUMNS, VGA_LOCAL_COLUMNS, graphio
+    from golden_io import load_case
+    from pyoracle import OracleMap
+    meta, A = load_case("syn32")
+    src = os.path.join(GOLDEN, "inputs", "syn32.csv")
+    g1, g2 = str(tmp_path / "a.dmxg"), str(tmp_path / "b.dmxg")
+    rc, out = run("-m", "VISPREP", "-f", src, "-o", g1, "-pg", "1", "-pp", "0.5,0.5", "-pm")
+    assert rc == 0, out
+    rc, out = run("-m", "VGA", "-f", g1, "-o", g2, "-vm", "visibility", "-vl", "-vg", "-vr", "n")
+    assert rc == 0, out
+
+    def chunk(path):
+        b = open(path, "rb").read()
+        nl = int(np.frombuffer(b[40:48], np.int64)[0])
+        o = 48 + nl * 32 + 1
+        n = int(np.frombuffer(b[o:o + 8], np.int64)[0])
+        return b[o + 8:o + 8 + n]
+    doc = graphio.read_chunk(chunk(g2))
+    names = [c[0] for c in doc["columns"]]
+    assert names == ["Connectivity", "Point First Moment", "Point Second Moment"] + VGA_LOCAL_COLUMNS + VGA_COLUMNS
+    om = OracleMap(meta["region"], meta["spacing"], np.load(os.path.join(GOLDEN, meta["lines_npy"])))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph()
+    om.set_graph(doc["bins"], doc["runs"])
+    want = om.vga_local(threads=8)
+    got = np.stack([c[1] for c in doc["columns"][3:6]], axis=1)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    glob = np.stack([c[1] for c in doc["columns"][6:]], axis=1)
+    assert (np.abs(glob.astype(np.float64) - A["vga_rt"]) <= 1e-6 * np.maximum(1.0, np.abs(A["vga_rt"]))).all()

@@ -448,3 +448,36 @@ def test_vga_prep_shard_two_ranks_threads(ctx, name):
     for r in range(2):
         got[lists[r]] = outs[r].cpu().numpy()[lists[r]]
     np.testing.assert_array_equal(got.view(np.uint32), full.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery"])
+def test_vga_local_matches_reference_and_oracle(ctx, name):
+    """VGA -vl on the GPU: bit-exact against the reference's columns where a fixture exists
+    (make_golden_vlocal.py) and against the C restatement (itself pinned on those fixtures)."""
+    import os
+    from golden_io import GOLDEN
+    from pyoracle import OracleMap
+    meta, A = load_case(name)
+    pm = _map(meta)
+    got = pm.make_graph(ctx).vga_visual_local()
+    path = os.path.join(GOLDEN, name + "_vlocal.npy")
+    if os.path.exists(path):
+        np.testing.assert_array_equal(got.view(np.uint32), np.load(path).view(np.uint32))
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph(threads=8)
+    np.testing.assert_array_equal(got.view(np.uint32), om.vga_local(threads=8).view(np.uint32))
+
+
+def test_vga_local_ranges_and_gates_only(ctx):
+    """Source ranges leave other rows untouched; gates_only skips every source (-1)."""
+    meta, A = load_case("syn32")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    full = g.vga_visual_local()
+    n = full.shape[0]
+    part = g.vga_visual_local(src_begin=100, src_end=300)
+    np.testing.assert_array_equal(part[100:300].view(np.uint32), full[100:300].view(np.uint32))
+    assert (part[:100] == -1).all() and (part[300:] == -1).all()
+    assert (g.vga_visual_local(gates_only=True) == -1).all()

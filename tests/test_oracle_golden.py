@@ -149,3 +149,21 @@ def test_visual_stepdepth_matches_reference_bitexact(name):
     got = om.visual_stepdepth(cells)
     np.testing.assert_array_equal(got.view(np.uint32), A["vstepdepth"].view(np.uint32))
     assert (A["vstepdepth"] >= 1).sum() > 0
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery"])
+def test_vga_local_matches_reference_bitexact(name):
+    """VGAVisualLocal::run restatement vs the reference's -vl columns (ref_probe --vlocal,
+    tests/golden/make_golden_vlocal.py): clustering coefficient, control, controllability."""
+    import os
+    from golden_io import GOLDEN
+    path = os.path.join(GOLDEN, name + "_vlocal.npy")
+    if not os.path.exists(path):
+        pytest.skip("no -vl fixture for this case (the reference takes hours on it)")
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    want = np.load(path)
+    got = om.vga_local(threads=8)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert (want[:, 0] >= 0).sum() > 0
