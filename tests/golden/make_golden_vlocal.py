@@ -3,7 +3,8 @@ VGAVisualLocal::run on salalib compiled from /root/reference) and saves the [N][
 tests/golden/<case>_vlocal.npy (Visual Clustering Coefficient, Visual Control, Visual
 Controllability, node order).  The reference's per-source cost grows with k * sum |V(n)| * |total|
 (std::find over vectors), so only cases it finishes in reasonable time are generated: kat, syn16,
-syn32 take < 70 s; syn64 and gallery take hours and are generated only when asked by name.
+syn32 take < 75 s (the default set); gallery takes ~130 s and syn64 about an hour, generated when
+asked by name (gallery is committed).
 
 Usage: python tests/golden/make_golden_vlocal.py [case ...]"""
 import os
