@@ -471,6 +471,55 @@ struct Vga : Mode {
             if (radius.empty()) throw CommandLineException("Metric vga requires a radius, use -vr <radius>");
         }
     }
+    // runVga METRIC branch (runmethods.cpp:245-248, RadiusConverter::ConvertForMetric
+    // radiusconverter.cpp:39-60) -> VGAMetric::run (vgametric.cpp:26-136)
+    void run_metric(const Args& a, Perf& perf, Document& d, Context& C, LoadedMap& m) {
+        double r = -1.0;
+        if (radius != "n") {
+            char* end = nullptr;
+            r = std::strtod(radius.c_str(), &end);
+            if (r <= 0)
+                throw RuntimeException(std::string("Radius for metric vga must be n for the whole range or a positive "
+                                                   "number. Got ") + radius);
+            if (std::isnan(r)) throw RuntimeException("Radius NaN?! Really?");
+            if (std::isinf(r)) throw RuntimeException("Radius inf?! Who are you kidding?");
+        }
+        std::cout << " ok\nAnalysing graph..." << std::flush;
+        std::vector<float> out((size_t)m.nnodes * 4, -1.0f);
+        timed(perf, "Run VGA", [&] { check(dmx_vga_metric(C.ctx, m.g, r, 0, 0, -1, out.data())); });
+        std::cout << " ok\nWriting out result..." << std::flush;
+        timed(perf, "Writing graph", [&] {
+            // radius suffix (vgametric.cpp:34-43) from the PointMap region (pointdata.cpp:151-154)
+            std::string suffix;
+            if (r != -1.0) {
+                int32_t cols_ = 0, rows_ = 0;
+                double blx = 0, bly = 0;
+                check(dmx_pointmap_info(m.pm, &cols_, &rows_, &blx, &bly, nullptr));
+                double sp = 0;
+                check(dmx_chunk_info(m.chunk, nullptr, nullptr, &sp, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
+                const double width = (blx + double(cols_ - 1) * sp + sp / 2.0) - (blx - sp / 2.0);
+                char buf[64];
+                snprintf(buf, sizeof(buf), r > 100.0 ? "%.f" : (width < 1.0 ? "%.4f" : "%.2f"), r);
+                suffix = std::string(" R") + buf;
+            }
+            const char* names[4] = {"Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance",
+                                    "Metric Mean Straight-Line Distance", "Metric Node Count"};
+            int displayed = -1;
+            for (int j = 0; j < 4; j++) {
+                Column c;
+                c.name = std::string(names[j]) + suffix;
+                c.values.resize((size_t)m.nnodes);
+                c.set.assign((size_t)m.nnodes, 1);
+                for (int64_t i = 0; i < m.nnodes; i++) c.values[i] = out[i * 4 + j];
+                if (j == 1) displayed = (int)m.columns.size();   // setDisplayedAttribute(mspl_col)
+                m.columns.push_back(c);
+            }
+            d.chunk = write_chunk(m.pm, m.nnodes, m.bins.data(), m.runs.data(), m.nruns, m.gridconn.data(), m.columns,
+                                  displayed);
+            write_document(a.out, d);
+        });
+        std::cout << " ok" << std::endl;
+    }
     void run(const Args& a, Perf& perf) override {
         Document d;
         timed(perf, "Load graph file", [&] { d = read_document(a.file); });
@@ -478,7 +527,11 @@ struct Vga : Mode {
         LoadedMap m;
         load_map(C, d, m);
         std::cout << "Getting options..." << std::flush;
-        if (mode != VISIBILITY) throw RuntimeException("Only -vm visibility is part of the accelerated path");
+        if (mode == METRIC) {
+            run_metric(a, perf, d, C, m);
+            return;
+        }
+        if (mode != VISIBILITY) throw RuntimeException("Only -vm visibility and -vm metric are part of the accelerated path");
         double r = -1.0;
         if (global) {
             if (radius != "n") {

@@ -1399,6 +1399,89 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
     return vga_tile_impl(ctx, g, radius, gates_only, 0, n, out_device, true, nullptr, tw, th, nullptr, 0, nullptr, d_list.p);
 }
 
+// ---------------------------------------------------------------- VGA metric (all sources)
+int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");
+    if (g->node_begin != 0 || g->node_end != g->nnodes)
+        return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
+    HIPCHK(hipSetDevice(ctx->device));
+    PointMapHost& h = *g->pm->host;
+    const int cols = h.cols(), rows = h.rows();
+    const int64_t C = (int64_t)cols * rows, N = g->nnodes;
+    if (se < 0 || se > N) se = N;
+    if (sb < 0 || sb > se) return fail(DMX_ERR_ARG, "source range out of bounds");
+    const auto& st = h.state();
+    // expanders: BLOCKED or next to a BLOCKED cell (ngraph.cpp:67-76, pointdata.cpp:1016-1068); the
+    // source expands at distance 0 whatever its flags
+    std::vector<uint8_t> flags((size_t)C, 0);
+    int64_t nexp = 0;
+    for (int x = 0; x < cols; x++)
+        for (int y = 0; y < rows; y++) {
+            const int64_t c = h.index(x, y);
+            if (!(st[c] & CELL_FILLED)) continue;
+            uint8_t f = SDF_FILLED;
+            bool ex = (st[c] & CELL_BLOCKED) != 0;
+            for (int dx = -1; dx <= 1 && !ex; dx++)
+                for (int dy = -1; dy <= 1 && !ex; dy++)
+                    if ((dx || dy) && h.includes(x + dx, y + dy) && (st[h.index(x + dx, y + dy)] & CELL_BLOCKED)) ex = true;
+            if (ex) { f |= SDF_EXPAND; nexp++; }
+            flags[c] = f;
+        }
+    hipStream_t s = ctx->stream;
+    int occ = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_metric_kernel, SD_THREADS, 0));
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(se - sb, (int64_t)ctx->num_cu * std::max(occ, 1)));
+    DevBuf<uint8_t> d_flags;
+    DevBuf<unsigned long long> d_key, d_over, d_comp, d_srt;
+    DevBuf<float> d_mdist, d_cum, d_out;
+    DevBuf<int32_t> d_last;
+    HIPCHK(d_flags.alloc(C));
+    HIPCHK(d_key.alloc((size_t)nb * C));
+    HIPCHK(d_mdist.alloc((size_t)nb * C));
+    HIPCHK(d_cum.alloc((size_t)nb * C));
+    HIPCHK(d_last.alloc((size_t)nb * C));
+    HIPCHK(d_comp.alloc((size_t)nb * std::max<int64_t>(N, 1)));
+    HIPCHK(d_srt.alloc((size_t)nb * std::max<int64_t>(N, 1)));
+    HIPCHK(d_out.alloc((size_t)std::max<int64_t>(N, 1) * 4));
+    HIPCHK(hipMemcpyAsync(d_flags.p, flags.data(), C, hipMemcpyHostToDevice, s));
+    int64_t cap = 8 * (nexp + 1) + SD_WIN + 1024;
+    for (int attempt = 0; attempt < 4; attempt++) {
+        HIPCHK(d_over.alloc((size_t)nb * cap));
+        HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), s));
+        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), s));
+        StepDepthParams P;
+        P.cols = cols; P.rows = rows; P.flags = d_flags.p; P.cell_node = g->pm->d_cell_node.p;
+        P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
+        P.key = d_key.p; P.mdist = d_mdist.p; P.cum = d_cum.p; P.lastpix = d_last.p;
+        P.over = d_over.p; P.over_cap = cap; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
+        HIPCHK(hipEventRecord(ctx->ev0, s));
+        if (se > sb) {
+            hipLaunchKernelGGL(vga_metric_kernel, dim3((unsigned)nb), dim3(SD_THREADS), 0, s, P, C, g->pm->d_node_cell.p,
+                               sb, se, gates_only, h.spacing(), radius < 0 ? -1.0 : radius, d_comp.p, d_srt.p,
+                               std::max<int64_t>(N, 1), d_out.p);
+            HIPCHK(hipGetLastError());
+        }
+        HIPCHK(hipEventRecord(ctx->ev1, s));
+        HIPCHK(hipStreamSynchronize(s));
+        int hc[2];
+        HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+        if (hc[1] & KERR_FRONTIER) { cap *= 4; continue; }
+        if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA metric: a distance bucket exceeded the sort window");
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+        ctx->last_vga_s = ms * 1e-3;
+        if (se > sb)
+            HIPCHK(hipMemcpy(out + sb * 4, d_out.p + sb * 4, (size_t)(se - sb) * 16, hipMemcpyDeviceToHost));
+        unsigned long long stv[3];
+        HIPCHK(hipMemcpy(stv, ctx->stats.p, sizeof(stv), hipMemcpyDeviceToHost));
+        ctx->last_sd_stats[0] = (long long)stv[0];
+        ctx->last_sd_stats[1] = (long long)stv[1];
+        ctx->last_stats[7] = se - sb;
+        return DMX_OK;
+    }
+    return fail(DMX_ERR_CAPACITY, "VGA metric: queue overflow after retries");
+}
+
 // ---------------------------------------------------------------- VGA visual local
 int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t sb, int64_t se, float* out) {
     if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");

@@ -18,6 +18,8 @@
 //     (tens of thousands of cells) is spread over its 1024 threads in <=128-cell chunks;
 //   * the queue is an unsorted LDS window (parallel min per pop) refilled from an HBM overflow
 //     list by distance windows.
+#include <cstddef>
+
 #include "common.hpp"
 
 namespace dmx {
@@ -61,6 +63,8 @@ struct SdShared {
     int nwin, nchunk, cut_ok, pad;
     unsigned long long cur;         // key being popped
     float cut_w;                    // refill window width (distance units)
+    unsigned long long keep;
+    int idx, cnt;
 };
 
 __device__ __forceinline__ void sd_push(SdShared& S, const StepDepthParams& P, unsigned long long k) {
@@ -109,13 +113,15 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
     }
 }
 
-__global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P, const int32_t* sel, int nsel) {
-    __shared__ SdShared S;
-    __shared__ unsigned long long s_keep;
-    __shared__ int s_idx, s_cnt;
+// The search of one workgroup from the nsel selected cells (all at distance 0).  rlim >= 0 stops it
+// at the first pop with dist * spacing > rlim (VGAMetric's radius, vgametric.cpp:86-88): later
+// pops can only resolve cells beyond the radius.
+__device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel, int nsel, double spacing,
+                       double rlim, unsigned long long& popped, unsigned long long& refills, unsigned& relaxed) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    unsigned long long popped = 0, refills = 0;
-    unsigned relaxed = 0;
+    unsigned long long& s_keep = S.keep;
+    int& s_idx = S.idx;
+    int& s_cnt = S.cnt;
     if (tid == 0) {
         S.nwin = 0; S.nchunk = 0; S.gmin = SD_INF; S.nover = 0; S.cut_w = 4.0f;
     }
@@ -219,8 +225,9 @@ __global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P
         const int ux = (int)((ku >> 16) & 0xffff), uy = (int)(ku & 0xffff);
         const int64_t uc = (int64_t)ux * P.rows + uy;
         if (P.key[uc] != ku) continue;    // stale: the cell was queued again with a smaller key
-        popped++;
         const float du = __uint_as_float((unsigned)(ku >> 32));
+        if (rlim >= 0.0 && (double)du * spacing > rlim) break;   // uniform: every thread read S.cur
+        popped++;
         const float cumu = P.cum[uc];
         const int lastu = P.lastpix[uc];
         const int node = P.cell_node[uc];
@@ -257,10 +264,181 @@ __global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P
         }
         __syncthreads();
     }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P, const int32_t* sel, int nsel) {
+    __shared__ SdShared S;
+    const int tid = threadIdx.x, lane = tid & 63;
+    unsigned long long popped = 0, refills = 0;
+    unsigned relaxed = 0;
+    sd_run(S, P, sel, nsel, 1.0, -1.0, popped, refills, relaxed);
     unsigned long long rl = relaxed;
     for (int off = 32; off >= 1; off >>= 1) rl += __shfl_xor(rl, off);
     if (lane == 0) atomicAdd(&P.stats[1], rl);
     if (tid == 0) { P.stats[0] = popped; P.stats[2] = refills; }
+}
+
+// ---------------------------------------------------------------- VGA metric (all sources)
+// VGAMetric::run (salalib/vgamodules/vgametric.cpp:26-136): the search above from every source,
+// one source per workgroup at a time (per-workgroup key / dist / angle arrays in HBM), followed by
+// the reference's float totals, which are accumulated in pop order = ascending key order:
+//   total_depth += float(dist * spacing), total_angle += cumangle,
+//   euclid_depth += float(spacing * dist(cell, source)), total_nodes++.
+// Ordering: the reached keys are bucketed by distance (VM_BUCKETS, counting sort through HBM), a
+// window of whole buckets (<= VM_CAP keys) is bitonic-sorted in the LDS the search no longer needs,
+// and wave 0 adds the terms lane by lane (readlane) -- the reference's sequential float chains.
+constexpr int VM_BUCKETS = 1024;
+constexpr int VM_CAP = 2 * SD_WIN;     // keys sorted at once: the search's window + chunk queue LDS
+constexpr int KERR_VM_BUCKET = 128;    // one distance bucket held more than VM_CAP keys
+
+__global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams P0, int64_t C, const int32_t* node_cell,
+                                                                int64_t sb, int64_t se, int gates_only, double spacing,
+                                                                double radius, unsigned long long* comp_all,
+                                                                unsigned long long* srt_all, int64_t nstride,
+                                                                float* out) {
+    __shared__ SdShared S;
+    __shared__ int hoff[VM_BUCKETS + 1];
+    __shared__ int cur[VM_BUCKETS];
+    __shared__ int s_src, s_n, s_pos, s_wend;
+    __shared__ unsigned s_maxd;
+    static_assert(offsetof(SdShared, chunk) == SD_WIN * sizeof(unsigned long long), "window + chunk queue contiguous");
+    unsigned long long* sk = S.win;   // VM_CAP keys (spans win and chunk)
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t b = blockIdx.x;
+    StepDepthParams P = P0;
+    P.key = P0.key + b * C;
+    P.mdist = P0.mdist + b * C;
+    P.cum = P0.cum + b * C;
+    P.lastpix = P0.lastpix + b * C;
+    P.over = P0.over + b * P0.over_cap;
+    unsigned long long* comp = comp_all + b * nstride;
+    unsigned long long* srt = srt_all + b * nstride;
+    unsigned long long popped = 0, refills = 0;
+    unsigned relaxed = 0;
+    for (int64_t src = sb + blockIdx.x; src < se; src += gridDim.x) {
+        float* o = out + src * 4;
+        if (gates_only) {
+            if (tid < 4) o[tid] = -1.0f;
+            continue;
+        }
+        for (int64_t c = tid; c < C; c += SD_THREADS) {
+            P.key[c] = SD_INF;
+            P.mdist[c] = -1.0f;
+            P.cum[c] = 0.0f;
+            P.lastpix[c] = -1;
+        }
+        if (tid == 0) { s_src = node_cell[src]; s_n = 0; s_pos = 0; s_maxd = 0u; }
+        __syncthreads();
+        sd_run(S, P, &s_src, 1, spacing, radius, popped, refills, relaxed);
+        const int sx = s_src / P.rows, sy = s_src % P.rows;
+        // reached cells within the radius: count and largest distance
+        int n = 0;
+        unsigned md = 0u;
+        for (int64_t c = tid; c < C; c += SD_THREADS) {
+            const unsigned long long k = P.key[c];
+            if (k == SD_INF) continue;
+            const float d = __uint_as_float((unsigned)(k >> 32));
+            if (radius >= 0.0 && (double)d * spacing > radius) continue;
+            n++;
+            md = max(md, (unsigned)(k >> 32));   // non-negative floats order like their bits
+        }
+        for (int off = 32; off >= 1; off >>= 1) {
+            n += __shfl_xor(n, off);
+            md = max(md, (unsigned)__shfl_xor((int)md, off));
+        }
+        for (int i = tid; i < VM_BUCKETS; i += SD_THREADS) cur[i] = 0;
+        if (lane == 0) { atomicAdd(&s_n, n); atomicMax(&s_maxd, md); }
+        __syncthreads();
+        const int nt = s_n;
+        const float inv = (float)VM_BUCKETS / fmaxf(__uint_as_float(s_maxd), 1e-30f);
+        // histogram + compaction (any order)
+        for (int64_t c = tid; c < C; c += SD_THREADS) {
+            const unsigned long long k = P.key[c];
+            if (k == SD_INF) continue;
+            const float d = __uint_as_float((unsigned)(k >> 32));
+            if (radius >= 0.0 && (double)d * spacing > radius) continue;
+            const int bk = min(VM_BUCKETS - 1, (int)(d * inv));
+            atomicAdd(&cur[bk], 1);
+            comp[atomicAdd(&s_pos, 1)] = k;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int acc = 0;
+            for (int i = 0; i < VM_BUCKETS; i++) { hoff[i] = acc; acc += cur[i]; cur[i] = hoff[i]; }
+            hoff[VM_BUCKETS] = acc;
+        }
+        __syncthreads();
+        for (int i = tid; i < nt; i += SD_THREADS) {
+            const unsigned long long k = comp[i];
+            const int bk = min(VM_BUCKETS - 1, (int)(__uint_as_float((unsigned)(k >> 32)) * inv));
+            srt[atomicAdd(&cur[bk], 1)] = k;
+        }
+        __syncthreads();
+        // windows of whole buckets, sorted in LDS, summed in order by wave 0
+        float td = 0.0f, ta = 0.0f, te = 0.0f;
+        int bs = 0;
+        while (bs < VM_BUCKETS) {
+            if (tid == 0) {
+                int be = bs + 1;
+                while (be < VM_BUCKETS && hoff[be + 1] - hoff[bs] <= VM_CAP) be++;
+                if (hoff[be] - hoff[bs] > VM_CAP) { atomicOr(P.error, KERR_VM_BUCKET); be = VM_BUCKETS; }
+                s_wend = be;
+            }
+            __syncthreads();
+            const int be = s_wend;
+            const int w0 = hoff[bs], m = min(hoff[be] - w0, VM_CAP);
+            int p2 = 1;
+            while (p2 < m) p2 <<= 1;
+            for (int i = tid; i < p2; i += SD_THREADS) sk[i] = i < m ? srt[w0 + i] : SD_INF;
+            __syncthreads();
+            for (int k = 2; k <= p2; k <<= 1)
+                for (int j = k >> 1; j > 0; j >>= 1) {
+                    for (int i = tid; i < p2; i += SD_THREADS) {
+                        const int ixj = i ^ j;
+                        if (ixj > i) {
+                            const unsigned long long a = sk[i], c2 = sk[ixj];
+                            if ((a > c2) == ((i & k) == 0)) { sk[i] = c2; sk[ixj] = a; }
+                        }
+                    }
+                    __syncthreads();
+                }
+            if (wave == 0) {
+                for (int i0 = 0; i0 < m; i0 += 64) {
+                    const int i = i0 + lane;
+                    float t0 = 0.0f, t1 = 0.0f, t2 = 0.0f;
+                    if (i < m) {
+                        const unsigned long long k = sk[i];
+                        const int x = (int)((k >> 16) & 0xffff), y = (int)(k & 0xffff);
+                        const float d = __uint_as_float((unsigned)(k >> 32));
+                        const int dx = x - sx, dy = y - sy;
+                        t0 = (float)((double)d * spacing);
+                        t1 = P.cum[(int64_t)x * P.rows + y];
+                        t2 = (float)(spacing * sqrt((double)(dx * dx + dy * dy)));
+                    }
+                    const int cnt = min(64, m - i0);
+                    for (int l = 0; l < cnt; l++) {
+                        td += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t0), l));
+                        ta += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t1), l));
+                        te += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t2), l));
+                    }
+                }
+            }
+            __syncthreads();
+            bs = be;
+        }
+        if (tid == 0) {
+            o[0] = (float)((double)ta / (double)nt);
+            o[1] = (float)((double)td / (double)nt);
+            o[2] = (float)((double)te / (double)nt);
+            o[3] = (float)nt;
+        }
+        __syncthreads();
+    }
+    unsigned long long rl = relaxed;
+    for (int off = 32; off >= 1; off >>= 1) rl += __shfl_xor(rl, off);
+    if (lane == 0) atomicAdd(&P0.stats[1], rl);
+    if (tid == 0) { atomicAdd(&P0.stats[0], popped); atomicAdd(&P0.stats[2], refills); }
 }
 
 // Attribute rows (vgametricdepth.cpp:54-61): float(spacing * dist), cumulative angle and, for a

@@ -19,6 +19,9 @@ STEPDEPTH_COLUMNS = ["Metric Step Shortest-Path Angle", "Metric Step Shortest-Pa
                      "Metric Straight-Line Distance"]
 # VGAVisualLocal column insertion order (vgavisuallocal.cpp:31-35), also alphabetical
 VGA_LOCAL_COLUMNS = ["Visual Clustering Coefficient", "Visual Control", "Visual Controllability"]
+# VGAMetric columns (vgametric.cpp:45-54, inserted in this alphabetical order; " R<r>" suffix)
+VGA_METRIC_COLUMNS = ["Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance",
+                      "Metric Mean Straight-Line Distance", "Metric Node Count"]
 VGA_COLUMNS = ["Visual Entropy", "Visual Integration [HH]", "Visual Integration [P-value]",
                "Visual Integration [Tekl]", "Visual Mean Depth", "Visual Node Count",
                "Visual Relativised Entropy"]
@@ -203,6 +206,15 @@ class Graph:
         N.check(N.lib().dmx_vga_global(self.ctx.h, self.h, float(radius), int(bool(gates_only)), int(src_begin),
                                        int(src_end), N.ptr(out), N.ptr(lv)))
         return (out, lv) if levels else out
+
+    def vga_metric(self, radius=-1.0, gates_only=False, src_begin=0, src_end=-1):
+        """VGA -vm metric -vr <radius|n> (VGAMetric::run, vgamodules/vgametric.cpp:26-136) on the GPU:
+        [N][4] float32 in VGA_METRIC_COLUMNS order (radius < 0: n)."""
+        n = self.info()["nnodes"]
+        out = np.full((n, 4), -1.0, dtype=np.float32)
+        N.check(N.lib().dmx_vga_metric(self.ctx.h, self.h, float(radius), int(bool(gates_only)), int(src_begin),
+                                       int(src_end), N.ptr(out)))
+        return out
 
     def vga_visual_local(self, gates_only=False, src_begin=0, src_end=-1):
         """VGA -vm visibility -vl (VGAVisualLocal::run, vgamodules/vgavisuallocal.cpp:23-117) on the

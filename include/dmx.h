@@ -128,6 +128,15 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
  * nodes in out_device are left untouched.  Used to interleave multi-GPU shards over the grid. */
 int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
                                int64_t n, float* out_device);
+/* ---- VGA metric (GPU) ----------------------------------------------------------------------- */
+/* MetaGraph::analyseGraph(OUTPUT_METRIC) -> VGAMetric(radius, gates_only).run (salalib/mgraph.cpp:
+ * 359-361, vgamodules/vgametric.cpp:26-136) for source nodes [src_begin, src_end) (src_end < 0:
+ * all); radius < 0 for "n" (otherwise in drawing units, compared with dist * spacing).  out: host
+ * [N][4] in node order, rows outside the range untouched: Metric Mean Shortest-Path Angle, Metric
+ * Mean Shortest-Path Distance, Metric Mean Straight-Line Distance, Metric Node Count (-1 rows with
+ * gates_only). */
+int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin, int64_t src_end,
+                   float* out);
 /* ---- VGA visual local (GPU) ----------------------------------------------------------------- */
 /* MetaGraph::analyseGraph(OUTPUT_VISUAL, local) -> VGAVisualLocal(gates_only).run
  * (salalib/mgraph.cpp:349-353, vgamodules/vgavisuallocal.cpp:23-117) for source nodes

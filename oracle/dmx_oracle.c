@@ -1030,22 +1030,20 @@ static int blocked_adjacent(const dmxo_map* m, int x, int y) {
     return 0;
 }
 
-int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out) {
-    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
-    for (int64_t i = 0; i < 3 * N; i++) out[i] = -1.0f;
-    if (nsel <= 0) return -1;
-    float* mdist = (float*)malloc(C * sizeof(float));
-    float* cum = (float*)calloc(C, sizeof(float));
-    int32_t* misc = (int32_t*)calloc(C, sizeof(int32_t));
-    Vec* ins = (Vec*)calloc(C, sizeof(Vec)); /* dists inserted per cell (std::set key dedupe) */
-    for (int64_t c = 0; c < C; c++) mdist[c] = -1.0f;
+/* The std::set<MetricTriple> search shared by VGAMetricDepth::run (vgametricdepth.cpp:45-84) and
+ * VGAMetric::run (vgametric.cpp:82-112): every selected cell enters at dist 0; popped triples of
+ * FILLED, not yet visited cells expand through Node::extractMetric when they are the search roots,
+ * BLOCKED or blocked-adjacent; `visit` sees every resolved cell in pop order.  radius >= 0 stops the
+ * search at the first popped triple with dist * spacing > radius (vgametric.cpp:86-88). */
+typedef void (*metric_visit_fn)(void* ctx, const dmxo_map* m, int64_t cell, float dist, float cum);
+static void metric_search(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, double radius, metric_visit_fn visit,
+                          void* vctx, float* mdist, float* cum, int32_t* misc, Vec* ins) {
+    const int64_t C = (int64_t)m->cols * m->rows;
+    for (int64_t c = 0; c < C; c++) { mdist[c] = -1.0f; cum[c] = 0.0f; misc[c] = 0; ins[c].n = 0; }
     MHeap h = {0, 0, 0};
-    /* std::set<int> getSelSet() order; every selected cell enters at dist 0 (vgametricdepth.cpp:45-47) */
-    int32_t sx0 = 0, sy0 = 0;
     for (int64_t i = 0; i < nsel; i++) {
         int32_t c = sel_cells[i];
         int x = c / m->rows, y = c % m->rows;
-        if (i == 0) { sx0 = x; sy0 = y; }
         MTrip t = {0.0f, pix_int(x, y), -1};
         float* d = (float*)vec_push(&ins[c], sizeof(float));
         *d = 0.0f;
@@ -1053,6 +1051,7 @@ int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
     }
     while (h.n) {
         MTrip here = mh_pop(&h);
+        if (radius >= 0.0 && ((double)here.dist * m->spacing) > radius) break;
         int hx = here.pix >> 16, hy = here.pix & 0xffff;
         int64_t hc = cidx(m, hx, hy);
         if (!(m->state[hc] & ST_FILLED) || misc[hc] == ~0) continue;
@@ -1099,13 +1098,83 @@ int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
             }
         }
         misc[hc] = ~0;
-        float* o = out + 3 * m->node_of_cell[hc];
-        o[0] = cum[hc];
-        o[1] = (float)(m->spacing * here.dist);
-        if (nsel == 1) o[2] = (float)(m->spacing * pix_dist(hx, hy, sx0, sy0));
+        visit(vctx, m, hc, here.dist, cum[hc]);
     }
+    free(h.a);
+}
+
+typedef struct { float* out; int64_t nsel; int sx0, sy0; } StepVisit;
+static void stepdepth_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
+    StepVisit* v = (StepVisit*)vctx;
+    float* o = v->out + 3 * m->node_of_cell[hc];
+    o[0] = cumv;
+    o[1] = (float)(m->spacing * dist);
+    if (v->nsel == 1) o[2] = (float)(m->spacing * pix_dist((int)(hc / m->rows), (int)(hc % m->rows), v->sx0, v->sy0));
+}
+
+int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out) {
+    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
+    for (int64_t i = 0; i < 3 * N; i++) out[i] = -1.0f;
+    if (nsel <= 0) return -1;
+    float* mdist = (float*)malloc(C * sizeof(float));
+    float* cum = (float*)malloc(C * sizeof(float));
+    int32_t* misc = (int32_t*)malloc(C * sizeof(int32_t));
+    Vec* ins = (Vec*)calloc(C, sizeof(Vec)); /* dists inserted per cell (std::set key dedupe) */
+    /* std::set<int> getSelSet() order; every selected cell enters at dist 0 (vgametricdepth.cpp:45-47) */
+    StepVisit v = {out, nsel, sel_cells[0] / m->rows, sel_cells[0] % m->rows};
+    metric_search(m, sel_cells, nsel, -1.0, stepdepth_visit, &v, mdist, cum, misc, ins);
     for (int64_t c = 0; c < C; c++) free(ins[c].p);
-    free(ins); free(h.a); free(mdist); free(cum); free(misc);
+    free(ins); free(mdist); free(cum); free(misc);
+    return 0;
+}
+
+/* VGAMetric::run (vgametric.cpp:26-136): per FILLED source, the metric search from it alone, with
+ * float totals accumulated in pop order: total_depth += float(dist * spacing), total_angle +=
+ * cumangle, euclid_depth += float(spacing * dist(pixel, source)), total_nodes++.  out [N][4]:
+ * Metric Mean Shortest-Path Angle, Mean Shortest-Path Distance, Mean Straight-Line Distance,
+ * Node Count (-1 for every source when gates_only). */
+typedef struct { float ftd, fta, fte; int64_t tn; int sx, sy; } MetricVisit;
+static void metric_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
+    MetricVisit* v = (MetricVisit*)vctx;
+    v->ftd += (float)(dist * m->spacing);
+    v->fta += cumv;
+    v->fte += (float)(m->spacing * pix_dist((int)(hc / m->rows), (int)(hc % m->rows), v->sx, v->sy));
+    v->tn += 1;
+}
+
+int dmxo_vga_metric(dmxo_map* m, double radius, int gates_only, int64_t nb, int64_t ne, int nthreads, float* out) {
+    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
+    if (ne < 0 || ne > N) ne = N;
+    if (nb < 0) nb = 0;
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        float* mdist = (float*)malloc(C * sizeof(float));
+        float* cum = (float*)malloc(C * sizeof(float));
+        int32_t* misc = (int32_t*)malloc(C * sizeof(int32_t));
+        Vec* ins = (Vec*)calloc(C, sizeof(Vec));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t k = nb; k < ne; k++) {
+            float* o = out + 4 * k;
+            for (int i = 0; i < 4; i++) o[i] = -1.0f;
+            if (gates_only) continue;
+            const int32_t c = m->node_cell[k];
+            MetricVisit v;
+            memset(&v, 0, sizeof(v));
+            v.sx = c / m->rows; v.sy = c % m->rows;
+            metric_search(m, &c, 1, radius, metric_visit, &v, mdist, cum, misc, ins);
+            o[0] = (float)((double)v.fta / (double)v.tn);
+            o[1] = (float)((double)v.ftd / (double)v.tn);
+            o[2] = (float)((double)v.fte / (double)v.tn);
+            o[3] = (float)v.tn;
+        }
+        for (int64_t c = 0; c < C; c++) free(ins[c].p);
+        free(ins); free(mdist); free(cum); free(misc);
+    }
     return 0;
 }
 

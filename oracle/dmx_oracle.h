@@ -59,6 +59,11 @@ int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t node_beg
  * Angle, Metric Step Shortest-Path Length, Metric Straight-Line Distance (single selection only;
  * otherwise -1); unreached cells keep -1.  Returns -1 for an empty selection. */
 int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
+/* VGAMetric::run (vgamodules/vgametric.cpp:26-136) for source nodes [node_begin, node_end),
+ * radius < 0 for "n".  out [N][4]: Metric Mean Shortest-Path Angle, Metric Mean Shortest-Path
+ * Distance, Metric Mean Straight-Line Distance, Metric Node Count (-1 rows with gates_only). */
+int dmxo_vga_metric(dmxo_map* m, double radius, int gates_only, int64_t node_begin, int64_t node_end, int nthreads,
+                    float* out);
 /* VGAVisualGlobalDepth::run (vgamodules/vgavisualglobaldepth.cpp:23-77): out [N], -1 unreached. */
 int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
 /* VGAVisualLocal::run (vgamodules/vgavisuallocal.cpp:23-117) for source nodes [node_begin,

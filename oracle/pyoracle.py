@@ -48,6 +48,8 @@ def lib():
         L.dmxo_metric_stepdepth.argtypes = [vp, vp, i64, vp]
         L.dmxo_visual_stepdepth.restype = i32
         L.dmxo_visual_stepdepth.argtypes = [vp, vp, i64, vp]
+        L.dmxo_vga_metric.restype = i32
+        L.dmxo_vga_metric.argtypes = [vp, dbl, i32, i64, i64, i32, vp]
         L.dmxo_vga_local.restype = i32
         L.dmxo_vga_local.argtypes = [vp, i32, i64, i64, i32, vp]
         L.dmxo_vga_global.restype = i32
@@ -147,4 +149,11 @@ class OracleMap:
         Controllability (-1: skipped source or neighbourhood of <= 1 cell)."""
         out = np.full((self.num_nodes, 3), -1.0, dtype=np.float32)
         lib().dmxo_vga_local(self.h, int(gates_only), node_begin, node_end, threads, _p(out))
+        return out
+
+    def vga_metric(self, radius=-1.0, gates_only=False, node_begin=0, node_end=-1, threads=1):
+        """VGAMetric::run: [N][4] Metric Mean Shortest-Path Angle, Mean Shortest-Path Distance, Mean
+        Straight-Line Distance, Node Count."""
+        out = np.full((self.num_nodes, 4), -1.0, dtype=np.float32)
+        lib().dmxo_vga_metric(self.h, float(radius), int(gates_only), node_begin, node_end, threads, _p(out))
         return out

@@ -73,7 +73,8 @@ static void dumpVga(PointMap& pm, const std::string& path) {
 int main(int argc, char** argv) {
     std::string linesCsv, graphIn, outDir = ".", writeGraph;
     double spacing = -1, maxdist = -1, radius = -1;
-    bool boundary = false, vga = false, roundtrip = false, vlocal = false;
+    bool boundary = false, vga = false, roundtrip = false, vlocal = false, vmetric = false;
+    double mradius = -1;
     long sources = 0;
     std::vector<Point2f> fills, stepPoints;
     for (int i = 1; i < argc; i++) {
@@ -89,6 +90,7 @@ int main(int argc, char** argv) {
         else if (a == "--vga") vga = true;
         else if (a == "--roundtrip") roundtrip = true;
         else if (a == "--vlocal") vlocal = true;
+        else if (a == "--vmetric") { vmetric = true; mradius = atof(next().c_str()); }
         else if (a == "--out") outDir = next();
         else if (a == "--write-graph") writeGraph = next();
         else if (a == "--sources") sources = atol(next().c_str());
@@ -309,14 +311,37 @@ int main(int argc, char** argv) {
         dump(outDir + "/vlocal.bin", out);
     }
 
+    // VGA metric (-vm metric -vr r: mgraph.cpp:359-361 -> VGAMetric::run), after everything else
+    double tvm = 0;
+    if (vmetric) {
+        Options opt;
+        opt.output_type = Options::OUTPUT_METRIC;
+        opt.radius = mradius;
+        auto a = std::chrono::steady_clock::now();
+        mg.analyseGraph(nullptr, opt, false);
+        auto b = std::chrono::steady_clock::now();
+        tvm = std::chrono::duration<double>(b - a).count();
+        AttributeTable& at = pm.getAttributeTable();
+        std::vector<int> mc;
+        for (size_t i = 0; i < at.getNumColumns(); i++)
+            if (at.getColumnName(i).rfind("Metric ", 0) == 0) mc.push_back((int)i);   // the 4 VGAMetric columns
+        std::vector<float> out;
+        for (auto it = at.begin(); it != at.end(); ++it)
+            for (int c : mc) out.push_back(it->getRow().getValue(c));
+        dump(outDir + "/vmetric.bin", out);
+        FILE* fn = fopen((outDir + "/vmetric_cols.txt").c_str(), "w");
+        for (int c : mc) fprintf(fn, "%s\n", at.getColumnName(c).c_str());
+        fclose(fn);
+    }
+
     FILE* f = fopen((outDir + "/grid.txt").c_str(), "w");
     fprintf(f, "spacing %.17g\ncols %zu\nrows %zu\n", pm.m_spacing, cols, rows);
     fprintf(f, "bottom_left %.17g %.17g\n", pm.m_bottom_left.x, pm.m_bottom_left.y);
     fprintf(f, "region %.17g %.17g %.17g %.17g\n", reg.bottom_left.x, reg.bottom_left.y, reg.top_right.x,
             reg.top_right.y);
     fprintf(f, "filled %d\nnodes %ld\nruns %zu\n", pm.m_filled_point_count, nodes, runs.size() / 4);
-    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\nt_stepdepth %.6f\nt_vstepdepth %.6f\nt_vlocal %.6f\n",
-            std::chrono::duration<double>(t1 - t0).count(), tv, tvrt, tsd, tvsd, tvl);
+    fprintf(f, "t_makegraph %.6f\nt_vga %.6f\nt_vga_rt %.6f\nt_stepdepth %.6f\nt_vstepdepth %.6f\nt_vlocal %.6f\nt_vmetric %.6f\n",
+            std::chrono::duration<double>(t1 - t0).count(), tv, tvrt, tsd, tvsd, tvl, tvm);
     fclose(f);
     printf("ok nodes %ld runs %zu t_makegraph %.3f t_vga %.3f\n", nodes, runs.size() / 4,
            std::chrono::duration<double>(t1 - t0).count(), tv);

@@ -165,3 +165,49 @@ def test_cli_vga_local_and_global(tmp_path):
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
     glob = np.stack([c[1] for c in doc["columns"][6:]], axis=1)
     assert (np.abs(glob.astype(np.float64) - A["vga_rt"]) <= 1e-6 * np.maximum(1.0, np.abs(A["vga_rt"]))).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("radius", ["n", "10"])
+def test_cli_vga_metric(tmp_path, radius):
+    """VGA -vm metric -vr <n|r> (runVga METRIC branch -> VGAMetric::run): four columns with the
+    reference's radius suffix, equal to the C restatement on the re-read graph."""
+    from depthmapx_amd import VGA_METRIC_COLUMNS, graphio
+    from golden_io import load_case
+    from pyoracle import OracleMap
+    meta, A = load_case("syn32")
+    src = os.path.join(GOLDEN, "inputs", "syn32.csv")
+    g1, g2 = str(tmp_path / "a.dmxg"), str(tmp_path / "b.dmxg")
+    rc, out = run("-m", "VISPREP", "-f", src, "-o", g1, "-pg", "1", "-pp", "0.5,0.5", "-pm")
+    assert rc == 0, out
+    rc, out = run("-m", "VGA", "-f", g1, "-o", g2, "-vm", "metric", "-vr", radius)
+    assert rc == 0, out
+
+    def chunk(path):
+        b = open(path, "rb").read()
+        nl = int(np.frombuffer(b[40:48], np.int64)[0])
+        o = 48 + nl * 32 + 1
+        n = int(np.frombuffer(b[o:o + 8], np.int64)[0])
+        return b[o + 8:o + 8 + n]
+    doc = graphio.read_chunk(chunk(g2))
+    suffix = "" if radius == "n" else " R10.00"
+    names = [c[0] for c in doc["columns"]]
+    assert names == ["Connectivity", "Point First Moment", "Point Second Moment"] + [n + suffix for n in VGA_METRIC_COLUMNS]
+    om = OracleMap(meta["region"], meta["spacing"], np.load(os.path.join(GOLDEN, meta["lines_npy"])))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph()
+    om.set_graph(doc["bins"], doc["runs"])
+    want = om.vga_metric(radius=-1.0 if radius == "n" else float(radius), threads=8)
+    got = np.stack([c[1] for c in doc["columns"][3:]], axis=1)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_cli_vga_metric_radius_errors(tmp_path):
+    src = os.path.join(GOLDEN, "inputs", "syn16.csv")
+    g1 = str(tmp_path / "a.dmxg")
+    rc, out = run("-m", "VISPREP", "-f", src, "-o", g1, "-pg", "1", "-pp", "0.5,0.5", "-pm")
+    assert rc == 0, out
+    rc, out = run("-m", "VGA", "-f", g1, "-o", str(tmp_path / "b.dmxg"), "-vm", "metric", "-vr", "-3")
+    assert rc == 255 and "Radius for metric vga must be n for the whole range or a positive number. Got -3" in out

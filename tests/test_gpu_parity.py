@@ -453,7 +453,7 @@ def test_vga_prep_shard_two_ranks_threads(ctx, name):
 @pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery"])
 def test_vga_local_matches_reference_and_oracle(ctx, name):
     """VGA -vl on the GPU: bit-exact against the reference's columns where a fixture exists
-    (make_golden_vlocal.py) and against the C restatement (itself pinned on those fixtures)."""
+    (make_golden_vga_modes.py) and against the C restatement (itself pinned on those fixtures)."""
     import os
     from golden_io import GOLDEN
     from pyoracle import OracleMap
@@ -481,3 +481,53 @@ def test_vga_local_ranges_and_gates_only(ctx):
     np.testing.assert_array_equal(part[100:300].view(np.uint32), full[100:300].view(np.uint32))
     assert (part[:100] == -1).all() and (part[300:] == -1).all()
     assert (g.vga_visual_local(gates_only=True) == -1).all()
+
+
+@pytest.mark.parametrize("name,radius", [("kat", -1.0), ("syn16", -1.0), ("syn32", -1.0), ("syn32", 10.0),
+                                         ("gallery", -1.0), ("syn64", -1.0), ("syn64", 7.5)])
+def test_vga_metric_matches_reference_and_oracle(ctx, name, radius):
+    """VGA -vm metric on the GPU (all sources, ordered float totals): bit-exact against the
+    reference's columns where a fixture exists and against the C restatement."""
+    import os
+    from golden_io import GOLDEN
+    from pyoracle import OracleMap
+    meta, A = load_case(name)
+    pm = _map(meta)
+    got = pm.make_graph(ctx).vga_metric(radius=radius)
+    path = os.path.join(GOLDEN, name + "_vmetric" + ("" if radius < 0 else "_r%g" % radius) + ".npy")
+    if os.path.exists(path):
+        np.testing.assert_array_equal(got.view(np.uint32), np.load(path).view(np.uint32))
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph(threads=8)
+    np.testing.assert_array_equal(got.view(np.uint32), om.vga_metric(radius=radius, threads=8).view(np.uint32))
+
+
+def test_vga_metric_ranges_and_gates_only(ctx):
+    meta, A = load_case("syn32")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    full = g.vga_metric()
+    part = g.vga_metric(src_begin=200, src_end=500)
+    np.testing.assert_array_equal(part[200:500].view(np.uint32), full[200:500].view(np.uint32))
+    assert (part[:200] == -1).all() and (part[500:] == -1).all()
+    assert (g.vga_metric(gates_only=True) == -1).all()
+
+
+def test_vga_metric_syn128_sources_match_oracle(ctx):
+    """A block of sources in the middle of the 128^2 synthetic plan (16k nodes, long float chains
+    and NaN angles from acos of a rounded-up cosine, as in the reference) against the oracle."""
+    from pyoracle import OracleMap
+    meta, A = load_case("syn128sd")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    n = g.info()["nnodes"]
+    b, e = n // 2 - 48, n // 2 + 48
+    got = g.vga_metric(src_begin=b, src_end=e)
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph(threads=8)
+    want = om.vga_metric(node_begin=b, node_end=e, threads=8)
+    np.testing.assert_array_equal(got[b:e].view(np.uint32), want[b:e].view(np.uint32))

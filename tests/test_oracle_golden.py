@@ -154,7 +154,7 @@ def test_visual_stepdepth_matches_reference_bitexact(name):
 @pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery"])
 def test_vga_local_matches_reference_bitexact(name):
     """VGAVisualLocal::run restatement vs the reference's -vl columns (ref_probe --vlocal,
-    tests/golden/make_golden_vlocal.py): clustering coefficient, control, controllability."""
+    tests/golden/make_golden_vga_modes.py): clustering coefficient, control, controllability."""
     import os
     from golden_io import GOLDEN
     path = os.path.join(GOLDEN, name + "_vlocal.npy")
@@ -167,3 +167,25 @@ def test_vga_local_matches_reference_bitexact(name):
     got = om.vga_local(threads=8)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
     assert (want[:, 0] >= 0).sum() > 0
+
+
+VMETRIC_CASES = [("kat", -1.0), ("syn16", -1.0), ("syn32", -1.0), ("syn32", 10.0), ("gallery", -1.0)]
+
+
+def _vmetric_fixture(name, radius):
+    import os
+    from golden_io import GOLDEN
+    return os.path.join(GOLDEN, name + "_vmetric" + ("" if radius < 0 else "_r%g" % radius) + ".npy")
+
+
+@pytest.mark.parametrize("name,radius", VMETRIC_CASES)
+def test_vga_metric_matches_reference_bitexact(name, radius):
+    """VGAMetric::run restatement vs the reference's -vm metric columns (ref_probe --vmetric,
+    tests/golden/make_golden_vga_modes.py): mean angle, mean path distance, mean straight-line
+    distance, node count -- float totals accumulated in the reference's pop order."""
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    want = np.load(_vmetric_fixture(name, radius))
+    got = om.vga_metric(radius=radius, threads=8)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
