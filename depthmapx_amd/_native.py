@@ -43,6 +43,8 @@ SIGNATURES = {
     "dmx_graph_set_prep_shard": (_i32, [_vp, _i64, _i64, _vp, _vp]),
     "dmx_vga_local": (_i32, [_vp, _vp, _i32, _i64, _i64, _vp]),
     "dmx_vga_metric": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp]),
+    "dmx_vga_angular": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp]),
+    "dmx_angular_stepdepth": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "dmx_release_cached_memory": (_i32, []),
     "dmx_ctx_last_stepdepth": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_ctx_last_phase_cycles": (_i32, [_vp, _vp]),

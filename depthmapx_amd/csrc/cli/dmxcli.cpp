@@ -473,9 +473,12 @@ struct Vga : Mode {
     }
     // runVga METRIC branch (runmethods.cpp:245-248, RadiusConverter::ConvertForMetric
     // radiusconverter.cpp:39-60) -> VGAMetric::run (vgametric.cpp:26-136)
+    // runVga ANGULAR branch (runmethods.cpp:249-251: no radius option, so -1) -> VGAAngular::run
+    // (vgaangular.cpp:26-133) shares the writer below.
     void run_metric(const Args& a, Perf& perf, Document& d, Context& C, LoadedMap& m) {
+        const bool ang = mode == ANGULAR;
         double r = -1.0;
-        if (radius != "n") {
+        if (!ang && radius != "n") {
             char* end = nullptr;
             r = std::strtod(radius.c_str(), &end);
             if (r <= 0)
@@ -485,8 +488,12 @@ struct Vga : Mode {
             if (std::isinf(r)) throw RuntimeException("Radius inf?! Who are you kidding?");
         }
         std::cout << " ok\nAnalysing graph..." << std::flush;
-        std::vector<float> out((size_t)m.nnodes * 4, -1.0f);
-        timed(perf, "Run VGA", [&] { check(dmx_vga_metric(C.ctx, m.g, r, 0, 0, -1, out.data())); });
+        const int nc = ang ? 3 : 4;
+        std::vector<float> out((size_t)m.nnodes * nc, -1.0f);
+        timed(perf, "Run VGA", [&] {
+            check(ang ? dmx_vga_angular(C.ctx, m.g, r, 0, 0, -1, out.data())
+                      : dmx_vga_metric(C.ctx, m.g, r, 0, 0, -1, out.data()));
+        });
         std::cout << " ok\nWriting out result..." << std::flush;
         timed(perf, "Writing graph", [&] {
             // radius suffix (vgametric.cpp:34-43) from the PointMap region (pointdata.cpp:151-154)
@@ -502,16 +509,19 @@ struct Vga : Mode {
                 snprintf(buf, sizeof(buf), r > 100.0 ? "%.f" : (width < 1.0 ? "%.4f" : "%.2f"), r);
                 suffix = std::string(" R") + buf;
             }
-            const char* names[4] = {"Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance",
-                                    "Metric Mean Straight-Line Distance", "Metric Node Count"};
+            const char* mnames[4] = {"Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance",
+                                     "Metric Mean Straight-Line Distance", "Metric Node Count"};
+            // VGAAngular inserts Mean Depth, Total Depth, Node Count (vgaangular.cpp:43-48)
+            const char* anames[3] = {"Angular Mean Depth", "Angular Total Depth", "Angular Node Count"};
             int displayed = -1;
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < nc; j++) {
                 Column c;
-                c.name = std::string(names[j]) + suffix;
+                c.name = std::string(ang ? anames[j] : mnames[j]) + suffix;
                 c.values.resize((size_t)m.nnodes);
                 c.set.assign((size_t)m.nnodes, 1);
-                for (int64_t i = 0; i < m.nnodes; i++) c.values[i] = out[i * 4 + j];
-                if (j == 1) displayed = (int)m.columns.size();   // setDisplayedAttribute(mspl_col)
+                for (int64_t i = 0; i < m.nnodes; i++) c.values[i] = out[i * nc + j];
+                // setDisplayedAttribute(mspl_col) / (mean_depth_col)
+                if (j == (ang ? 0 : 1)) displayed = (int)m.columns.size();
                 m.columns.push_back(c);
             }
             d.chunk = write_chunk(m.pm, m.nnodes, m.bins.data(), m.runs.data(), m.nruns, m.gridconn.data(), m.columns,
@@ -527,11 +537,12 @@ struct Vga : Mode {
         LoadedMap m;
         load_map(C, d, m);
         std::cout << "Getting options..." << std::flush;
-        if (mode == METRIC) {
+        if (mode == METRIC || mode == ANGULAR) {
             run_metric(a, perf, d, C, m);
             return;
         }
-        if (mode != VISIBILITY) throw RuntimeException("Only -vm visibility and -vm metric are part of the accelerated path");
+        if (mode != VISIBILITY)
+            throw RuntimeException("Only -vm visibility, metric and angular are part of the accelerated path");
         double r = -1.0;
         if (global) {
             if (radius != "n") {
@@ -673,22 +684,22 @@ struct StepDepth : Mode {
             sel.push_back(x * rows + y);
         }
         std::cout << "ok\nCalculating step-depth... " << std::flush;
-        if (type == ANGULAR) throw RuntimeException("Only -sdt metric and -sdt visual are part of the accelerated path");
         std::vector<float> out((size_t)m.nnodes * 3, -1.0f);
         int rc = DMX_OK;
         timed(perf, "Calculating step-depth", [&] {
-            rc = type == METRIC ? dmx_metric_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data())
-                                : dmx_visual_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data());
+            rc = type == METRIC   ? dmx_metric_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data())
+                 : type == ANGULAR ? dmx_angular_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data())
+                                   : dmx_visual_stepdepth(C.ctx, m.g, sel.data(), (int64_t)sel.size(), out.data());
         });
         if (rc != DMX_OK && rc != DMX_ERR_STATE) check(rc);   // no selection: analyseGraph returns false
         std::cout << " ok\nWriting out result..." << std::flush;
         timed(perf, "Writing graph", [&] {
             int displayed = -1;
-            if (rc == DMX_OK && type == VISUAL) {
-                // VGAVisualGlobalDepth::run: one column, reset to -1, set on every reached cell
-                // (vgavisualglobaldepth.cpp:28, :49)
+            if (rc == DMX_OK && (type == VISUAL || type == ANGULAR)) {
+                // VGAVisualGlobalDepth::run / VGAAngularDepth::run: one column, reset to -1, set on every
+                // reached cell (vgavisualglobaldepth.cpp:28, :49; vgaangulardepth.cpp:27, :53-55)
                 Column c;
-                c.name = "Visual Step Depth";
+                c.name = type == VISUAL ? "Visual Step Depth" : "Angular Step Depth";
                 c.values.assign(out.begin(), out.begin() + m.nnodes);
                 c.set.resize((size_t)m.nnodes);
                 for (int64_t k = 0; k < m.nnodes; k++) c.set[k] = out[k] >= 0.0f ? 1 : 0;
@@ -733,8 +744,8 @@ void print_help() {
     std::cout << "Usage: dmxcli -m <mode> -f <filename> -o <output file> [-t <times.csv>] [-s] [-p] [mode options]\n"
                  "Modes (the accelerated depthmapXcli path):\n"
                  "  VISPREP   -pg <grid spacing> -pp <x,y> | -pf <points file> [-pr <max visibility>] [-pb] [-pm]\n"
-                 "  VGA       -vm visibility -vg -vr <radius|n>\n"
-                 "  STEPDEPTH -sdt metric|visual -sdp <x,y> | -sdf <points file>\n"
+                 "  VGA       -vm visibility [-vl] [-vg -vr <radius|n>] | -vm metric -vr <radius|n> | -vm angular\n"
+                 "  STEPDEPTH -sdt metric|visual|angular -sdp <x,y> | -sdf <points file>\n"
                  "Input: a CSV drawing (x1,y1,x2,y2) or a .dmxg written by this tool; output: .dmxg\n";
 }
 

@@ -1400,7 +1400,10 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
 }
 
 // ---------------------------------------------------------------- VGA metric (all sources)
-int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+// VGAMetric::run / VGAAngular::run for every source: one search per workgroup (stepdepth.hip).
+extern "C++" template <bool ANG>
+static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    constexpr int NO = ANG ? 3 : 4;
     if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
@@ -1429,7 +1432,7 @@ int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
         }
     hipStream_t s = ctx->stream;
     int occ = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_metric_kernel, SD_THREADS, 0));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_metric_kernel<ANG>, SD_THREADS, 0));
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(se - sb, (int64_t)ctx->num_cu * std::max(occ, 1)));
     DevBuf<uint8_t> d_flags;
     DevBuf<unsigned long long> d_key, d_over, d_comp, d_srt;
@@ -1440,11 +1443,12 @@ int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
     HIPCHK(d_mdist.alloc((size_t)nb * C));
     HIPCHK(d_cum.alloc((size_t)nb * C));
     HIPCHK(d_last.alloc((size_t)nb * C));
-    HIPCHK(d_comp.alloc((size_t)nb * std::max<int64_t>(N, 1)));
+    HIPCHK(d_comp.alloc((size_t)nb * 2 * std::max<int64_t>(N, 1)));
     HIPCHK(d_srt.alloc((size_t)nb * std::max<int64_t>(N, 1)));
-    HIPCHK(d_out.alloc((size_t)std::max<int64_t>(N, 1) * 4));
+    HIPCHK(d_out.alloc((size_t)std::max<int64_t>(N, 1) * NO));
     HIPCHK(hipMemcpyAsync(d_flags.p, flags.data(), C, hipMemcpyHostToDevice, s));
     int64_t cap = 8 * (nexp + 1) + SD_WIN + 1024;
+    if (ANG) cap += 32 * N;   // cells reached at angle 0 are queued too (and re-queued on improvement)
     for (int attempt = 0; attempt < 4; attempt++) {
         HIPCHK(d_over.alloc((size_t)nb * cap));
         HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), s));
@@ -1456,7 +1460,7 @@ int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
         P.over = d_over.p; P.over_cap = cap; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
         HIPCHK(hipEventRecord(ctx->ev0, s));
         if (se > sb) {
-            hipLaunchKernelGGL(vga_metric_kernel, dim3((unsigned)nb), dim3(SD_THREADS), 0, s, P, C, g->pm->d_node_cell.p,
+            hipLaunchKernelGGL(vga_metric_kernel<ANG>, dim3((unsigned)nb), dim3(SD_THREADS), 0, s, P, C, g->pm->d_node_cell.p,
                                sb, se, gates_only, h.spacing(), radius < 0 ? -1.0 : radius, d_comp.p, d_srt.p,
                                std::max<int64_t>(N, 1), d_out.p);
             HIPCHK(hipGetLastError());
@@ -1466,12 +1470,12 @@ int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
         int hc[2];
         HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
         if (hc[1] & KERR_FRONTIER) { cap *= 4; continue; }
-        if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA metric: a distance bucket exceeded the sort window");
+        if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA metric/angular search failed");
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
         ctx->last_vga_s = ms * 1e-3;
         if (se > sb)
-            HIPCHK(hipMemcpy(out + sb * 4, d_out.p + sb * 4, (size_t)(se - sb) * 16, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(out + sb * NO, d_out.p + sb * NO, (size_t)(se - sb) * NO * 4, hipMemcpyDeviceToHost));
         unsigned long long stv[3];
         HIPCHK(hipMemcpy(stv, ctx->stats.p, sizeof(stv), hipMemcpyDeviceToHost));
         ctx->last_sd_stats[0] = (long long)stv[0];
@@ -1480,6 +1484,14 @@ int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
         return DMX_OK;
     }
     return fail(DMX_ERR_CAPACITY, "VGA metric: queue overflow after retries");
+}
+
+int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    return vga_search_all<false>(ctx, g, radius, gates_only, sb, se, out);
+}
+
+int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    return vga_search_all<true>(ctx, g, radius, gates_only, sb, se, out);
 }
 
 // ---------------------------------------------------------------- VGA visual local
@@ -1544,7 +1556,10 @@ int dmx_graph_set_prep_shard(dmx_graph* g, int64_t node_begin, int64_t node_end,
 }
 
 // ---------------------------------------------------------------- metric step depth
-int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+// STEPDEPTH -sdt metric (VGAMetricDepth) or, with ANG, -sdt angular (VGAAngularDepth): one search
+// from the selection; out [N][3] (metric) or [N] (angular).
+extern "C++" template <bool ANG>
+static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
@@ -1595,13 +1610,14 @@ int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
     HIPCHK(d_out.alloc(std::max<int64_t>(N, 1) * 3));
     HIPCHK(hipMemcpyAsync(d_flags.p, flags.data(), C, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, s));
-    int64_t cap = 8 * (nexp + (int64_t)sel.size()) + SD_WIN + 1024;
+    int64_t cap = 8 * (nexp + (int64_t)sel.size()) + SD_WIN + 1024 + (ANG ? 8 * N : 0);
     for (int attempt = 0; attempt < 4; attempt++) {
         HIPCHK(d_over.alloc(cap));
         HIPCHK(hipMemsetAsync(d_key.p, 0xFF, C * 8, s));
         std::vector<float> m1((size_t)C, -1.0f);
         HIPCHK(hipMemcpyAsync(d_mdist.p, m1.data(), C * 4, hipMemcpyHostToDevice, s));
-        HIPCHK(hipMemsetAsync(d_cum.p, 0, C * 4, s));
+        if (ANG) HIPCHK(hipMemcpyAsync(d_cum.p, m1.data(), C * 4, hipMemcpyHostToDevice, s));
+        else HIPCHK(hipMemsetAsync(d_cum.p, 0, C * 4, s));
         HIPCHK(hipMemsetAsync(d_last.p, 0xFF, C * 4, s));
         HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), s));
         HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), s));
@@ -1611,12 +1627,15 @@ int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
         P.key = d_key.p; P.mdist = d_mdist.p; P.cum = d_cum.p; P.lastpix = d_last.p;
         P.over = d_over.p; P.over_cap = cap; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
         HIPCHK(hipEventRecord(ctx->ev0, s));
-        hipLaunchKernelGGL(stepdepth_kernel, dim3(1), dim3(SD_THREADS), 0, s, P, d_sel.p, (int)sel.size());
+        hipLaunchKernelGGL(stepdepth_kernel<ANG>, dim3(1), dim3(SD_THREADS), 0, s, P, d_sel.p, (int)sel.size());
         HIPCHK(hipGetLastError());
         const int single = sel.size() == 1 ? 1 : 0;
-        hipLaunchKernelGGL(stepdepth_out_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rows, h.spacing(),
-                           g->pm->d_node_cell.p, N, d_key.p, d_cum.p, single, sel[0] / rows, sel[0] % rows, d_out.p);
-        HIPCHK(hipGetLastError());
+        if (!ANG) {
+            hipLaunchKernelGGL(stepdepth_out_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rows,
+                               h.spacing(), g->pm->d_node_cell.p, N, d_key.p, d_cum.p, single, sel[0] / rows,
+                               sel[0] % rows, d_out.p);
+            HIPCHK(hipGetLastError());
+        }
         HIPCHK(hipEventRecord(ctx->ev1, s));
         HIPCHK(hipStreamSynchronize(s));
         int hc[2];
@@ -1628,10 +1647,30 @@ int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
         unsigned long long st3[3];
         HIPCHK(hipMemcpy(st3, ctx->stats.p, sizeof(st3), hipMemcpyDeviceToHost));
         for (int i = 0; i < 3; i++) ctx->last_sd_stats[i] = (long long)st3[i];
-        if (N) HIPCHK(hipMemcpy(out, d_out.p, N * 3 * 4, hipMemcpyDeviceToHost));
+        if (ANG) {
+            // "Angular Step Depth" = m_cumangle of every cell the search resolved (vgaangulardepth.cpp:53-55)
+            std::vector<unsigned long long> kh((size_t)C);
+            std::vector<float> ch((size_t)C);
+            HIPCHK(hipMemcpy(kh.data(), d_key.p, C * 8, hipMemcpyDeviceToHost));
+            HIPCHK(hipMemcpy(ch.data(), d_cum.p, C * 4, hipMemcpyDeviceToHost));
+            for (int64_t k = 0; k < N; k++) {
+                const int c = g->pm->node_cell[k];
+                out[k] = kh[c] != SD_INF ? ch[c] : -1.0f;
+            }
+        } else if (N) {
+            HIPCHK(hipMemcpy(out, d_out.p, N * 3 * 4, hipMemcpyDeviceToHost));
+        }
         return DMX_OK;
     }
     return fail(DMX_ERR_CAPACITY, "step depth queue overflow after retries");
+}
+
+int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    return stepdepth_impl<false>(ctx, g, sel_cells, nsel, out);
+}
+
+int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    return stepdepth_impl<true>(ctx, g, sel_cells, nsel, out);
 }
 
 int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {

@@ -80,7 +80,21 @@ __device__ __forceinline__ void sd_push(SdShared& S, const StepDepthParams& P, u
     atomicMin(&S.gmin, k);
 }
 
-// Relax cell (x, y) from expander u (Bin::extractMetric, ngraph.cpp:330-345).
+// PixelRef angle(a, b, c) / (pi/2) (pixelref.h:121-131) with a = (x, y), b = u, c = last.
+__device__ __forceinline__ float sd_turn(int dx, int dy, int ux, int uy, int lastu) {
+    if (lastu == -1) return 0.0f;
+    const int lx = lastu >> 16, ly = lastu & 0xffff;
+    const int ex = ux - lx, ey = uy - ly;
+    return (float)(acos((double)(dx * ex + dy * ey) /
+                        (sqrt((double)(dx * dx + dy * dy)) * sqrt((double)(ex * ex + ey * ey)) + 1e-12)) /
+                   (3.14159265358979323846 * 0.5));
+}
+
+// Relax cell (x, y) from expander u: Bin::extractMetric (ngraph.cpp:330-345), or with ANG
+// Bin::extractAngular (ngraph.cpp:348-366): the key is the cumulative angle, the update test
+// here.angle + ang < cumangle (floats), and a cell reached with angle 0 expands too
+// (Node::extractAngular expands when curs.angle == 0, ngraph.cpp:78-85).
+template <bool ANG>
 __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, int x, int y, int ux, int uy, float du,
                                          float cumu, int lastu, unsigned long long ku, unsigned& relaxed) {
     const int64_t c = (int64_t)x * P.rows + y;
@@ -89,21 +103,29 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
     const unsigned long long kv = P.key[c];
     if (kv < ku) return;                  // already popped: m_misc == ~0
     relaxed++;
+    if (ANG) {
+        const float cv = P.cum[c];
+        if (cv != -1.0f && !(du < cv)) return;   // ang >= 0 (or NaN): du + ang < cv cannot hold
+        const float ang = sd_turn(x - ux, y - uy, ux, uy, lastu);
+        if (cv == -1.0f || du + ang < cv) {
+            const float nv = cumu + ang;
+            P.cum[c] = nv;
+            const unsigned long long nk = sd_key(nv, pix_of(x, y));
+            if (nk < kv) {
+                P.key[c] = nk;
+                P.lastpix[c] = pix_of(ux, uy);
+                if ((f & SDF_EXPAND) || nv == 0.0f) sd_push(S, P, nk);
+            }
+        }
+        return;
+    }
     const int dx = x - ux, dy = y - uy;
     const double dd = sqrt((double)(dx * dx + dy * dy));
     const float md = P.mdist[c];
     if (md == -1.0f || (double)du + dd < (double)md) {
         const float nd = du + (float)dd;
         P.mdist[c] = nd;
-        float a = 0.0f;
-        if (lastu != -1) {   // PixelRef angle (pixelref.h:121-131)
-            const int lx = lastu >> 16, ly = lastu & 0xffff;
-            const int ex = ux - lx, ey = uy - ly;
-            a = (float)(acos((double)(dx * ex + dy * ey) /
-                             (sqrt((double)(dx * dx + dy * dy)) * sqrt((double)(ex * ex + ey * ey)) + 1e-12)) /
-                        (3.14159265358979323846 * 0.5));
-        }
-        P.cum[c] = cumu + a;
+        P.cum[c] = cumu + sd_turn(dx, dy, ux, uy, lastu);
         const unsigned long long nk = sd_key(nd, pix_of(x, y));
         if (nk < kv) {                    // a new smallest entry: it carries this lastpixel
             P.key[c] = nk;
@@ -116,6 +138,7 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
 // The search of one workgroup from the nsel selected cells (all at distance 0).  rlim >= 0 stops it
 // at the first pop with dist * spacing > rlim (VGAMetric's radius, vgametric.cpp:86-88): later
 // pops can only resolve cells beyond the radius.
+template <bool ANG>
 __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel, int nsel, double spacing,
                        double rlim, unsigned long long& popped, unsigned long long& refills, unsigned& relaxed) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -131,6 +154,7 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
         const int c = sel[i];
         const unsigned long long k = sd_key(0.0f, pix_of(c / P.rows, c % P.rows));
         P.key[c] = k;
+        if (ANG) P.cum[c] = 0.0f;         // m_cumangle of the selected cells (vgaangulardepth.cpp:39-42)
         sd_push(S, P, k);
     }
     __syncthreads();
@@ -226,7 +250,7 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
         const int64_t uc = (int64_t)ux * P.rows + uy;
         if (P.key[uc] != ku) continue;    // stale: the cell was queued again with a smaller key
         const float du = __uint_as_float((unsigned)(ku >> 32));
-        if (rlim >= 0.0 && (double)du * spacing > rlim) break;   // uniform: every thread read S.cur
+        if (rlim >= 0.0 && (ANG ? (double)du : (double)du * spacing) > rlim) break;   // uniform (S.cur)
         popped++;
         const float cumu = P.cum[uc];
         const int lastu = P.lastpix[uc];
@@ -240,14 +264,14 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
             const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
             const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
             const int own = min(len, SD_CHUNK);
-            for (int i = 0; i < own; i++) sd_relax(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+            for (int i = 0; i < own; i++) sd_relax<ANG>(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
             for (int o = SD_CHUNK; o < len; o += SD_CHUNK) {
                 const int q = atomicAdd(&S.nchunk, 1);
                 if (q < SD_CHUNKQ) {
                     S.chunk[q] = make_int2(r, o);
                 } else {
                     const int e = min(len, o + SD_CHUNK);
-                    for (int i = o; i < e; i++) sd_relax(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+                    for (int i = o; i < e; i++) sd_relax<ANG>(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
                 }
             }
         }
@@ -260,19 +284,20 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
             const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
             const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
             const int e = min(len, ch.y + SD_CHUNK);
-            for (int i = ch.y; i < e; i++) sd_relax(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+            for (int i = ch.y; i < e; i++) sd_relax<ANG>(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
         }
         __syncthreads();
     }
     __syncthreads();
 }
 
+template <bool ANG>
 __global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P, const int32_t* sel, int nsel) {
     __shared__ SdShared S;
     const int tid = threadIdx.x, lane = tid & 63;
     unsigned long long popped = 0, refills = 0;
     unsigned relaxed = 0;
-    sd_run(S, P, sel, nsel, 1.0, -1.0, popped, refills, relaxed);
+    sd_run<ANG>(S, P, sel, nsel, 1.0, -1.0, popped, refills, relaxed);
     unsigned long long rl = relaxed;
     for (int off = 32; off >= 1; off >>= 1) rl += __shfl_xor(rl, off);
     if (lane == 0) atomicAdd(&P.stats[1], rl);
@@ -290,8 +315,8 @@ __global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P
 // and wave 0 adds the terms lane by lane (readlane) -- the reference's sequential float chains.
 constexpr int VM_BUCKETS = 1024;
 constexpr int VM_CAP = 2 * SD_WIN;     // keys sorted at once: the search's window + chunk queue LDS
-constexpr int KERR_VM_BUCKET = 128;    // one distance bucket held more than VM_CAP keys
 
+template <bool ANG>
 __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams P0, int64_t C, const int32_t* node_cell,
                                                                 int64_t sb, int64_t se, int gates_only, double spacing,
                                                                 double radius, unsigned long long* comp_all,
@@ -312,25 +337,26 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
     P.cum = P0.cum + b * C;
     P.lastpix = P0.lastpix + b * C;
     P.over = P0.over + b * P0.over_cap;
-    unsigned long long* comp = comp_all + b * nstride;
+    unsigned long long* comp = comp_all + b * 2 * nstride;   // [2N]: compaction, then the sort of an oversize bucket
     unsigned long long* srt = srt_all + b * nstride;
     unsigned long long popped = 0, refills = 0;
     unsigned relaxed = 0;
     for (int64_t src = sb + blockIdx.x; src < se; src += gridDim.x) {
-        float* o = out + src * 4;
+        constexpr int NO = ANG ? 3 : 4;
+        float* o = out + src * NO;
         if (gates_only) {
-            if (tid < 4) o[tid] = -1.0f;
+            if (tid < NO) o[tid] = -1.0f;
             continue;
         }
         for (int64_t c = tid; c < C; c += SD_THREADS) {
             P.key[c] = SD_INF;
             P.mdist[c] = -1.0f;
-            P.cum[c] = 0.0f;
+            P.cum[c] = ANG ? -1.0f : 0.0f;
             P.lastpix[c] = -1;
         }
         if (tid == 0) { s_src = node_cell[src]; s_n = 0; s_pos = 0; s_maxd = 0u; }
         __syncthreads();
-        sd_run(S, P, &s_src, 1, spacing, radius, popped, refills, relaxed);
+        sd_run<ANG>(S, P, &s_src, 1, spacing, radius, popped, refills, relaxed);
         const int sx = s_src / P.rows, sy = s_src % P.rows;
         // reached cells within the radius: count and largest distance
         int n = 0;
@@ -339,7 +365,7 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
             const unsigned long long k = P.key[c];
             if (k == SD_INF) continue;
             const float d = __uint_as_float((unsigned)(k >> 32));
-            if (radius >= 0.0 && (double)d * spacing > radius) continue;
+            if (radius >= 0.0 && (ANG ? (double)d : (double)d * spacing) > radius) continue;
             n++;
             md = max(md, (unsigned)(k >> 32));   // non-negative floats order like their bits
         }
@@ -357,7 +383,7 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
             const unsigned long long k = P.key[c];
             if (k == SD_INF) continue;
             const float d = __uint_as_float((unsigned)(k >> 32));
-            if (radius >= 0.0 && (double)d * spacing > radius) continue;
+            if (radius >= 0.0 && (ANG ? (double)d : (double)d * spacing) > radius) continue;
             const int bk = min(VM_BUCKETS - 1, (int)(d * inv));
             atomicAdd(&cur[bk], 1);
             comp[atomicAdd(&s_pos, 1)] = k;
@@ -382,23 +408,25 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
             if (tid == 0) {
                 int be = bs + 1;
                 while (be < VM_BUCKETS && hoff[be + 1] - hoff[bs] <= VM_CAP) be++;
-                if (hoff[be] - hoff[bs] > VM_CAP) { atomicOr(P.error, KERR_VM_BUCKET); be = VM_BUCKETS; }
                 s_wend = be;
             }
             __syncthreads();
             const int be = s_wend;
-            const int w0 = hoff[bs], m = min(hoff[be] - w0, VM_CAP);
+            const int w0 = hoff[bs], m = hoff[be] - w0;
+            // a window is whole buckets of <= VM_CAP keys, sorted in LDS; a single bucket above that
+            // (e.g. every cell seen straight from the source sits at angle 0) is sorted in HBM scratch
+            unsigned long long* arr = m > VM_CAP ? comp : sk;
             int p2 = 1;
             while (p2 < m) p2 <<= 1;
-            for (int i = tid; i < p2; i += SD_THREADS) sk[i] = i < m ? srt[w0 + i] : SD_INF;
+            for (int i = tid; i < p2; i += SD_THREADS) arr[i] = i < m ? srt[w0 + i] : SD_INF;
             __syncthreads();
             for (int k = 2; k <= p2; k <<= 1)
                 for (int j = k >> 1; j > 0; j >>= 1) {
                     for (int i = tid; i < p2; i += SD_THREADS) {
                         const int ixj = i ^ j;
                         if (ixj > i) {
-                            const unsigned long long a = sk[i], c2 = sk[ixj];
-                            if ((a > c2) == ((i & k) == 0)) { sk[i] = c2; sk[ixj] = a; }
+                            const unsigned long long a = arr[i], c2 = arr[ixj];
+                            if ((a > c2) == ((i & k) == 0)) { arr[i] = c2; arr[ixj] = a; }
                         }
                     }
                     __syncthreads();
@@ -408,7 +436,7 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
                     const int i = i0 + lane;
                     float t0 = 0.0f, t1 = 0.0f, t2 = 0.0f;
                     if (i < m) {
-                        const unsigned long long k = sk[i];
+                        const unsigned long long k = arr[i];
                         const int x = (int)((k >> 16) & 0xffff), y = (int)(k & 0xffff);
                         const float d = __uint_as_float((unsigned)(k >> 32));
                         const int dx = x - sx, dy = y - sy;
@@ -428,10 +456,16 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
             bs = be;
         }
         if (tid == 0) {
-            o[0] = (float)((double)ta / (double)nt);
-            o[1] = (float)((double)td / (double)nt);
-            o[2] = (float)((double)te / (double)nt);
-            o[3] = (float)nt;
+            if (ANG) {   // vgaangular.cpp:113-118 (nt >= 1: the source itself)
+                o[0] = (float)((double)ta / (double)nt);
+                o[1] = ta;
+                o[2] = (float)nt;
+            } else {
+                o[0] = (float)((double)ta / (double)nt);
+                o[1] = (float)((double)td / (double)nt);
+                o[2] = (float)((double)te / (double)nt);
+                o[3] = (float)nt;
+            }
         }
         __syncthreads();
     }

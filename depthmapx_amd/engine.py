@@ -22,6 +22,8 @@ VGA_LOCAL_COLUMNS = ["Visual Clustering Coefficient", "Visual Control", "Visual 
 # VGAMetric columns (vgametric.cpp:45-54, inserted in this alphabetical order; " R<r>" suffix)
 VGA_METRIC_COLUMNS = ["Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance",
                       "Metric Mean Straight-Line Distance", "Metric Node Count"]
+# VGAAngular columns (vgaangular.cpp:43-48; " R<r>" suffix)
+VGA_ANGULAR_COLUMNS = ["Angular Mean Depth", "Angular Total Depth", "Angular Node Count"]
 VGA_COLUMNS = ["Visual Entropy", "Visual Integration [HH]", "Visual Integration [P-value]",
                "Visual Integration [Tekl]", "Visual Mean Depth", "Visual Node Count",
                "Visual Relativised Entropy"]
@@ -214,6 +216,27 @@ class Graph:
         out = np.full((n, 4), -1.0, dtype=np.float32)
         N.check(N.lib().dmx_vga_metric(self.ctx.h, self.h, float(radius), int(bool(gates_only)), int(src_begin),
                                        int(src_end), N.ptr(out)))
+        return out
+
+    def vga_angular(self, radius=-1.0, gates_only=False, src_begin=0, src_end=-1):
+        """VGA -vm angular (VGAAngular::run, vgamodules/vgaangular.cpp:26-133) on the GPU: [N][3]
+        float32 in VGA_ANGULAR_COLUMNS order (radius < 0: n)."""
+        n = self.info()["nnodes"]
+        out = np.full((n, 3), -1.0, dtype=np.float32)
+        N.check(N.lib().dmx_vga_angular(self.ctx.h, self.h, float(radius), int(bool(gates_only)), int(src_begin),
+                                        int(src_end), N.ptr(out)))
+        return out
+
+    def angular_step_depth(self, points=None, cells=None):
+        """STEPDEPTH -sdt angular (VGAAngularDepth::run): [N] Angular Step Depth (-1: not reached)."""
+        sel = [] if cells is None else [int(c) for c in cells]
+        for (x, y) in (points or []):
+            if not self.pm.region_contains(x, y):
+                raise N.DmxError(-6, "Point outside of target region")
+            sel.append(self.pm.pixelate(x, y))
+        arr = np.ascontiguousarray(sel, dtype=np.int32)
+        out = np.full(self.info()["nnodes"], -1.0, dtype=np.float32)
+        N.check(N.lib().dmx_angular_stepdepth(self.ctx.h, self.h, N.ptr(arr), len(arr), N.ptr(out)))
         return out
 
     def vga_visual_local(self, gates_only=False, src_begin=0, src_end=-1):

@@ -137,6 +137,13 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
  * gates_only). */
 int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin, int64_t src_end,
                    float* out);
+/* ---- VGA angular (GPU) ---------------------------------------------------------------------- */
+/* MetaGraph::analyseGraph(OUTPUT_ANGULAR) -> VGAAngular(radius, gates_only).run (salalib/mgraph.cpp:
+ * 362-364, vgamodules/vgaangular.cpp:26-133) for source nodes [src_begin, src_end); radius < 0 for
+ * "n" (otherwise compared with the cumulative angle).  out: host [N][3] in node order: Angular Mean
+ * Depth, Angular Total Depth, Angular Node Count (-1 rows with gates_only). */
+int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin, int64_t src_end,
+                    float* out);
 /* ---- VGA visual local (GPU) ----------------------------------------------------------------- */
 /* MetaGraph::analyseGraph(OUTPUT_VISUAL, local) -> VGAVisualLocal(gates_only).run
  * (salalib/mgraph.cpp:349-353, vgamodules/vgavisuallocal.cpp:23-117) for source nodes
@@ -165,6 +172,13 @@ int dmx_graph_set_prep_shard(dmx_graph* g, int64_t node_begin, int64_t node_end,
  * Metric Straight-Line Distance (single selected cell only, else -1); unreached cells -1.
  * DMX_ERR_STATE if no filled cell is selected (the reference then skips the analysis). */
 int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out);
+/* ---- VGA angular step depth (GPU) ---------------------------------------------------------- */
+/* dm_runmethods::runStepDepth with -sdt angular -> MetaGraph::analyseGraph(point_depth_selection=3)
+ * -> VGAAngularDepth::run (depthmapXcli/runmethods.cpp:770-772, salalib/mgraph.cpp:334-336,
+ * vgamodules/vgaangulardepth.cpp:23-75).  sel_cells as for dmx_metric_stepdepth.  out: host [N]
+ * "Angular Step Depth" in node order (unreached cells -1).  DMX_ERR_STATE if no filled cell is
+ * selected. */
+int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out);
 /* ---- VGA visual step depth (GPU) ----------------------------------------------------------- */
 /* dm_runmethods::runStepDepth with -sdt visual -> MetaGraph::analyseGraph(point_depth_selection=1)
  * -> VGAVisualGlobalDepth::run (depthmapXcli/runmethods.cpp:767-769, salalib/mgraph.cpp:312-314,

@@ -1178,6 +1178,143 @@ int dmxo_vga_metric(dmxo_map* m, double radius, int gates_only, int64_t nb, int6
     return 0;
 }
 
+/* The std::set<AngularTriple> search shared by VGAAngularDepth::run (vgaangulardepth.cpp:23-75) and
+ * VGAAngular::run (vgaangular.cpp:26-133): selected cells enter with cumangle 0; a popped FILLED,
+ * unvisited cell expands through Node::extractAngular (ngraph.cpp:78-85) when its angle is 0 or it is
+ * BLOCKED / blocked-adjacent; Bin::extractAngular (ngraph.cpp:348-366) relaxes every unvisited cell
+ * of its runs (no FILLED test) with ang = angle(pix, here, last)/(pi/2) when cumangle == -1 or
+ * here.angle + ang < cumangle.  cum[] starts at -1 for every cell (VGAAngular resets all points;
+ * VGAAngularDepth only the filled ones, but unfilled cells are never counted nor expanded).
+ * radius >= 0 stops at the first popped triple with angle > radius (vgaangular.cpp:86-88). */
+static void angular_search(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, double radius, metric_visit_fn visit,
+                           void* vctx, float* cum, int32_t* misc, Vec* ins) {
+    const int64_t C = (int64_t)m->cols * m->rows;
+    for (int64_t c = 0; c < C; c++) { cum[c] = -1.0f; misc[c] = 0; ins[c].n = 0; }
+    MHeap h = {0, 0, 0};
+    for (int64_t i = 0; i < nsel; i++) {
+        int32_t c = sel_cells[i];
+        int x = c / m->rows, y = c % m->rows;
+        MTrip t = {0.0f, pix_int(x, y), -1};
+        int dup = 0;
+        for (int64_t q = 0; q < ins[c].n; q++)
+            if (((float*)ins[c].p)[q] == 0.0f) dup = 1;
+        if (!dup) {
+            float* d = (float*)vec_push(&ins[c], sizeof(float));
+            *d = 0.0f;
+            mh_push(&h, t);
+        }
+        cum[c] = 0.0f;
+    }
+    while (h.n) {
+        MTrip here = mh_pop(&h);
+        if (radius >= 0.0 && (double)here.dist > radius) break;
+        int hx = here.pix >> 16, hy = here.pix & 0xffff;
+        int64_t hc = cidx(m, hx, hy);
+        if (!(m->state[hc] & ST_FILLED) || misc[hc] == ~0) continue;
+        if (here.dist == 0.0f || (m->state[hc] & ST_BLOCKED) || blocked_adjacent(m, hx, hy)) {
+            const NodeG* nd = &m->nodes[m->node_of_cell[hc]];
+            const Run* r = nd->runs;
+            int lx = here.last >> 16, ly = here.last & 0xffff;
+            for (int b = 0; b < 32; b++) {
+                char dir = nd->dir[b];
+                for (int k = 0; k < nd->nruns[b]; k++, r++) {
+                    int px = r->x0, py = r->y0;
+                    int endc = (dir & D_V) ? r->y1 : r->x1;
+                    for (;;) {
+                        int col = (dir & D_V) ? py : px;
+                        if (col > endc) break;
+                        int64_t pc = cidx(m, px, py);
+                        if (misc[pc] == 0) {
+                            float ang = here.last == -1 ? 0.0f : (float)(pix_angle(px, py, hx, hy, lx, ly) / (M_PI_ * 0.5));
+                            if (cum[pc] == -1.0 || here.dist + ang < cum[pc]) {
+                                cum[pc] = cum[hc] + ang;
+                                int dup = 0;
+                                for (int64_t q = 0; q < ins[pc].n; q++)
+                                    if (((float*)ins[pc].p)[q] == cum[pc]) { dup = 1; break; }
+                                if (!dup) {
+                                    float* d = (float*)vec_push(&ins[pc], sizeof(float));
+                                    *d = cum[pc];
+                                    MTrip t = {cum[pc], pix_int(px, py), here.pix};
+                                    mh_push(&h, t);
+                                }
+                            }
+                        }
+                        switch (dir) {
+                        case D_PD: px++; py++; break;
+                        case D_ND: px++; py--; break;
+                        case D_H: px++; break;
+                        case D_V: py++; break;
+                        }
+                    }
+                }
+            }
+        }
+        misc[hc] = ~0;
+        visit(vctx, m, hc, here.dist, cum[hc]);
+    }
+    free(h.a);
+}
+
+static void angular_step_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
+    (void)dist;
+    ((float*)vctx)[m->node_of_cell[hc]] = cumv;
+}
+
+int dmxo_angular_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out) {
+    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
+    for (int64_t i = 0; i < N; i++) out[i] = -1.0f;
+    if (nsel <= 0) return -1;
+    float* cum = (float*)malloc(C * sizeof(float));
+    int32_t* misc = (int32_t*)malloc(C * sizeof(int32_t));
+    Vec* ins = (Vec*)calloc(C, sizeof(Vec));
+    angular_search(m, sel_cells, nsel, -1.0, angular_step_visit, out, cum, misc, ins);
+    for (int64_t c = 0; c < C; c++) free(ins[c].p);
+    free(ins); free(cum); free(misc);
+    return 0;
+}
+
+typedef struct { float total; int64_t n; } AngularVisit;
+static void angular_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
+    (void)m; (void)hc; (void)dist;
+    AngularVisit* v = (AngularVisit*)vctx;
+    v->total += cumv;
+    v->n += 1;
+}
+
+/* VGAAngular::run (vgaangular.cpp:26-133): out [N][3] Angular Mean Depth, Angular Total Depth,
+ * Angular Node Count (-1 rows with gates_only). */
+int dmxo_vga_angular(dmxo_map* m, double radius, int gates_only, int64_t nb, int64_t ne, int nthreads, float* out) {
+    const int64_t N = m->nnodes, C = (int64_t)m->cols * m->rows;
+    if (ne < 0 || ne > N) ne = N;
+    if (nb < 0) nb = 0;
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        float* cum = (float*)malloc(C * sizeof(float));
+        int32_t* misc = (int32_t*)malloc(C * sizeof(int32_t));
+        Vec* ins = (Vec*)calloc(C, sizeof(Vec));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t k = nb; k < ne; k++) {
+            float* o = out + 3 * k;
+            for (int i = 0; i < 3; i++) o[i] = -1.0f;
+            if (gates_only) continue;
+            const int32_t c = m->node_cell[k];
+            AngularVisit v = {0.0f, 0};
+            angular_search(m, &c, 1, radius, angular_visit, &v, cum, misc, ins);
+            if (v.n > 0) o[0] = (float)((double)v.total / (double)v.n);
+            o[1] = v.total;
+            o[2] = (float)v.n;
+        }
+        for (int64_t c = 0; c < C; c++) free(ins[c].p);
+        free(ins); free(cum); free(misc);
+    }
+    return 0;
+}
+
 /* VGAVisualGlobalDepth::run (salalib/vgamodules/vgavisualglobaldepth.cpp:23-77) with
  * Node::extractUnseen -> Bin::extractUnseen (ngraph.cpp:60-65, :308-326): one search tree from the
  * whole selection (std::set<int> PixelRef order), each level walked in reverse; Point::m_misc and

@@ -64,6 +64,13 @@ int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
  * Distance, Metric Mean Straight-Line Distance, Metric Node Count (-1 rows with gates_only). */
 int dmxo_vga_metric(dmxo_map* m, double radius, int gates_only, int64_t node_begin, int64_t node_end, int nthreads,
                     float* out);
+/* VGAAngularDepth::run (vgamodules/vgaangulardepth.cpp:23-75): out [N] Angular Step Depth, -1
+ * unreached.  Returns -1 for an empty selection. */
+int dmxo_angular_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
+/* VGAAngular::run (vgamodules/vgaangular.cpp:26-133), radius < 0 for "n".  out [N][3]: Angular Mean
+ * Depth, Angular Total Depth, Angular Node Count (-1 rows with gates_only). */
+int dmxo_vga_angular(dmxo_map* m, double radius, int gates_only, int64_t node_begin, int64_t node_end, int nthreads,
+                     float* out);
 /* VGAVisualGlobalDepth::run (vgamodules/vgavisualglobaldepth.cpp:23-77): out [N], -1 unreached. */
 int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, float* out);
 /* VGAVisualLocal::run (vgamodules/vgavisuallocal.cpp:23-117) for source nodes [node_begin,

@@ -50,6 +50,10 @@ def lib():
         L.dmxo_visual_stepdepth.argtypes = [vp, vp, i64, vp]
         L.dmxo_vga_metric.restype = i32
         L.dmxo_vga_metric.argtypes = [vp, dbl, i32, i64, i64, i32, vp]
+        L.dmxo_vga_angular.restype = i32
+        L.dmxo_vga_angular.argtypes = [vp, dbl, i32, i64, i64, i32, vp]
+        L.dmxo_angular_stepdepth.restype = i32
+        L.dmxo_angular_stepdepth.argtypes = [vp, vp, i64, vp]
         L.dmxo_vga_local.restype = i32
         L.dmxo_vga_local.argtypes = [vp, i32, i64, i64, i32, vp]
         L.dmxo_vga_global.restype = i32
@@ -156,4 +160,18 @@ class OracleMap:
         Straight-Line Distance, Node Count."""
         out = np.full((self.num_nodes, 4), -1.0, dtype=np.float32)
         lib().dmxo_vga_metric(self.h, float(radius), int(gates_only), node_begin, node_end, threads, _p(out))
+        return out
+
+    def vga_angular(self, radius=-1.0, gates_only=False, node_begin=0, node_end=-1, threads=1):
+        """VGAAngular::run: [N][3] Angular Mean Depth, Angular Total Depth, Angular Node Count."""
+        out = np.full((self.num_nodes, 3), -1.0, dtype=np.float32)
+        lib().dmxo_vga_angular(self.h, float(radius), int(gates_only), node_begin, node_end, threads, _p(out))
+        return out
+
+    def angular_stepdepth(self, sel_cells):
+        """VGAAngularDepth::run from x-major cell indices (std::set<int> PixelRef order): [N] Angular
+        Step Depth, -1 where not reached."""
+        sel = np.ascontiguousarray(sel_cells, dtype=np.int32)
+        out = np.full(self.num_nodes, -1.0, dtype=np.float32)
+        lib().dmxo_angular_stepdepth(self.h, _p(sel), len(sel), _p(out))
         return out

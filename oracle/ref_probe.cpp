@@ -73,7 +73,7 @@ static void dumpVga(PointMap& pm, const std::string& path) {
 int main(int argc, char** argv) {
     std::string linesCsv, graphIn, outDir = ".", writeGraph;
     double spacing = -1, maxdist = -1, radius = -1;
-    bool boundary = false, vga = false, roundtrip = false, vlocal = false, vmetric = false;
+    bool boundary = false, vga = false, roundtrip = false, vlocal = false, vmetric = false, vangular = false;
     double mradius = -1;
     long sources = 0;
     std::vector<Point2f> fills, stepPoints;
@@ -91,6 +91,7 @@ int main(int argc, char** argv) {
         else if (a == "--roundtrip") roundtrip = true;
         else if (a == "--vlocal") vlocal = true;
         else if (a == "--vmetric") { vmetric = true; mradius = atof(next().c_str()); }
+        else if (a == "--vangular") { vangular = true; mradius = atof(next().c_str()); }
         else if (a == "--out") outDir = next();
         else if (a == "--write-graph") writeGraph = next();
         else if (a == "--sources") sources = atol(next().c_str());
@@ -253,6 +254,15 @@ int main(int argc, char** argv) {
         const int vcol = vdone && at.hasColumn("Visual Step Depth") ? (int)at.getColumnIndex("Visual Step Depth") : -1;
         for (auto it = at.begin(); it != at.end(); ++it) vsd.push_back(vcol >= 0 ? it->getRow().getValue(vcol) : -1.0f);
         dump(outDir + "/vstepdepth.bin", vsd);
+        // and -sdt angular (runmethods.cpp:770-772 -> VGAAngularDepth::run, mgraph.cpp:334-336)
+        Options aopt;
+        aopt.global = 0;
+        aopt.point_depth_selection = 3;
+        bool adone = mg.analyseGraph(nullptr, aopt, false);
+        std::vector<float> asd;
+        const int acol = adone && at.hasColumn("Angular Step Depth") ? (int)at.getColumnIndex("Angular Step Depth") : -1;
+        for (auto it = at.begin(); it != at.end(); ++it) asd.push_back(acol >= 0 ? it->getRow().getValue(acol) : -1.0f);
+        dump(outDir + "/astepdepth.bin", asd);
         pm.clearSel();
     }
 
@@ -313,9 +323,9 @@ int main(int argc, char** argv) {
 
     // VGA metric (-vm metric -vr r: mgraph.cpp:359-361 -> VGAMetric::run), after everything else
     double tvm = 0;
-    if (vmetric) {
+    if (vmetric || vangular) {
         Options opt;
-        opt.output_type = Options::OUTPUT_METRIC;
+        opt.output_type = vmetric ? Options::OUTPUT_METRIC : Options::OUTPUT_ANGULAR;
         opt.radius = mradius;
         auto a = std::chrono::steady_clock::now();
         mg.analyseGraph(nullptr, opt, false);
@@ -324,12 +334,12 @@ int main(int argc, char** argv) {
         AttributeTable& at = pm.getAttributeTable();
         std::vector<int> mc;
         for (size_t i = 0; i < at.getNumColumns(); i++)
-            if (at.getColumnName(i).rfind("Metric ", 0) == 0) mc.push_back((int)i);   // the 4 VGAMetric columns
+            if (at.getColumnName(i).rfind(vmetric ? "Metric " : "Angular ", 0) == 0) mc.push_back((int)i);
         std::vector<float> out;
         for (auto it = at.begin(); it != at.end(); ++it)
             for (int c : mc) out.push_back(it->getRow().getValue(c));
-        dump(outDir + "/vmetric.bin", out);
-        FILE* fn = fopen((outDir + "/vmetric_cols.txt").c_str(), "w");
+        dump(outDir + (vmetric ? "/vmetric.bin" : "/vangular.bin"), out);
+        FILE* fn = fopen((outDir + (vmetric ? "/vmetric_cols.txt" : "/vangular_cols.txt")).c_str(), "w");
         for (int c : mc) fprintf(fn, "%s\n", at.getColumnName(c).c_str());
         fclose(fn);
     }

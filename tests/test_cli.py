@@ -211,3 +211,40 @@ def test_cli_vga_metric_radius_errors(tmp_path):
     assert rc == 0, out
     rc, out = run("-m", "VGA", "-f", g1, "-o", str(tmp_path / "b.dmxg"), "-vm", "metric", "-vr", "-3")
     assert rc == 255 and "Radius for metric vga must be n for the whole range or a positive number. Got -3" in out
+
+
+@pytest.mark.gpu
+def test_cli_vga_angular_and_angular_stepdepth(tmp_path):
+    """VGA -vm angular (VGAAngular::run) and STEPDEPTH -sdt angular (VGAAngularDepth::run) through
+    the CLI, against the C restatement on the re-read graph."""
+    from depthmapx_amd import VGA_ANGULAR_COLUMNS, graphio
+    from golden_io import load_case
+    from pyoracle import OracleMap
+    meta, A = load_case("syn32")
+    src = os.path.join(GOLDEN, "inputs", "syn32.csv")
+    g1, g2, g3 = (str(tmp_path / n) for n in ("a.dmxg", "b.dmxg", "c.dmxg"))
+    rc, out = run("-m", "VISPREP", "-f", src, "-o", g1, "-pg", "1", "-pp", "0.5,0.5", "-pm")
+    assert rc == 0, out
+    rc, out = run("-m", "VGA", "-f", g1, "-o", g2, "-vm", "angular")
+    assert rc == 0, out
+    rc, out = run("-m", "STEPDEPTH", "-f", g1, "-o", g3, "-sdt", "angular", "-sdp", "16.5,16.5")
+    assert rc == 0, out
+
+    def chunk(path):
+        b = open(path, "rb").read()
+        nl = int(np.frombuffer(b[40:48], np.int64)[0])
+        o = 48 + nl * 32 + 1
+        n = int(np.frombuffer(b[o:o + 8], np.int64)[0])
+        return b[o + 8:o + 8 + n]
+    doc = graphio.read_chunk(chunk(g2))
+    assert [c[0] for c in doc["columns"]][3:] == VGA_ANGULAR_COLUMNS
+    om = OracleMap(meta["region"], meta["spacing"], np.load(os.path.join(GOLDEN, meta["lines_npy"])))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph()
+    om.set_graph(doc["bins"], doc["runs"])
+    got = np.stack([c[1] for c in doc["columns"][3:]], axis=1)
+    np.testing.assert_array_equal(got.view(np.uint32), om.vga_angular(threads=8).view(np.uint32))
+    cols3 = {c[0]: c[1] for c in graphio.read_chunk(chunk(g3))["columns"]}
+    want = om.angular_stepdepth(np.array([17 * meta["rows"] + 17], np.int32))
+    np.testing.assert_array_equal(cols3["Angular Step Depth"], want)

@@ -531,3 +531,68 @@ def test_vga_metric_syn128_sources_match_oracle(ctx):
     om.make_graph(threads=8)
     want = om.vga_metric(node_begin=b, node_end=e, threads=8)
     np.testing.assert_array_equal(got[b:e].view(np.uint32), want[b:e].view(np.uint32))
+
+
+@pytest.mark.parametrize("name,radius", [("kat", -1.0), ("syn16", -1.0), ("syn32", -1.0), ("syn32", 1.5),
+                                         ("gallery", -1.0), ("syn64", -1.0), ("syn64", 0.5)])
+def test_vga_angular_matches_reference_and_oracle(ctx, name, radius):
+    """VGA -vm angular on the GPU (all sources; cells reached at angle 0 expand too): bit-exact
+    against the reference's columns where a fixture exists and against the C restatement."""
+    import os
+    from golden_io import GOLDEN
+    from pyoracle import OracleMap
+    meta, A = load_case(name)
+    pm = _map(meta)
+    got = pm.make_graph(ctx).vga_angular(radius=radius)
+    path = os.path.join(GOLDEN, name + "_vangular" + ("" if radius < 0 else "_r%g" % radius) + ".npy")
+    if os.path.exists(path):
+        np.testing.assert_array_equal(got.view(np.uint32), np.load(path).view(np.uint32))
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph(threads=8)
+    np.testing.assert_array_equal(got.view(np.uint32), om.vga_angular(radius=radius, threads=8).view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery", "barnsbury", "syn128sd"])
+def test_angular_stepdepth_matches_reference(ctx, name):
+    """STEPDEPTH -sdt angular on the GPU: the reference's column (fixtures) / the oracle (syn128sd)."""
+    import os
+    from golden_io import GOLDEN
+    from pyoracle import OracleMap
+    meta, A = load_case(name)
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    sel = A["stepdepth_sel"]
+    cells = (sel >> 16) * meta["rows"] + (sel & 0xFFFF)
+    got = g.angular_step_depth(cells=cells)
+    path = os.path.join(GOLDEN, name + "_astepdepth.npy")
+    if os.path.exists(path):
+        want = np.load(path)
+    else:
+        om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+        for f in meta["fills"]:
+            om.fill(*f)
+        om.make_graph(threads=8)
+        want = om.angular_stepdepth(cells)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert (got >= 0).sum() > 0
+
+
+def test_vga_angular_syn128_sources_match_oracle(ctx):
+    """A block of sources of the 128^2 plan against the oracle: thousands of cells sit at angle 0
+    (seen straight from the source), more than one LDS sort window -- the HBM sort path."""
+    from pyoracle import OracleMap
+    meta, A = load_case("syn128sd")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    n = g.info()["nnodes"]
+    b, e = n // 2 - 48, n // 2 + 48
+    got = g.vga_angular(src_begin=b, src_end=e)
+    om = OracleMap(meta["region"], meta["spacing"], case_input_lines(meta))
+    for f in meta["fills"]:
+        om.fill(*f)
+    om.make_graph(threads=8)
+    want = om.vga_angular(node_begin=b, node_end=e, threads=8)
+    np.testing.assert_array_equal(got[b:e].view(np.uint32), want[b:e].view(np.uint32))
+    assert (got[b:e, 2] > 8192).any()

@@ -189,3 +189,32 @@ def test_vga_metric_matches_reference_bitexact(name, radius):
     want = np.load(_vmetric_fixture(name, radius))
     got = om.vga_metric(radius=radius, threads=8)
     np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("name,radius", [("kat", -1.0), ("syn16", -1.0), ("syn32", -1.0), ("syn32", 1.5),
+                                         ("gallery", -1.0)])
+def test_vga_angular_matches_reference_bitexact(name, radius):
+    """VGAAngular::run restatement vs the reference's -vm angular columns (ref_probe --vangular)."""
+    import os
+    from golden_io import GOLDEN
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    want = np.load(os.path.join(GOLDEN, name + "_vangular" + ("" if radius < 0 else "_r%g" % radius) + ".npy"))
+    got = om.vga_angular(radius=radius, threads=8)
+    np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "syn64", "gallery", "barnsbury"])
+def test_angular_stepdepth_matches_reference_bitexact(name):
+    """VGAAngularDepth::run restatement vs the reference's STEPDEPTH -sdt angular column on the
+    same selection as the metric / visual step depth fixtures."""
+    import os
+    from golden_io import GOLDEN
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    sel = A["stepdepth_sel"]
+    cells = (sel >> 16) * meta["rows"] + (sel & 0xFFFF)
+    want = np.load(os.path.join(GOLDEN, name + "_astepdepth.npy"))
+    np.testing.assert_array_equal(om.angular_stepdepth(cells).view(np.uint32), want.view(np.uint32))
