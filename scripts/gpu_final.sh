@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/final_${TAG:-r1}
 mkdir -p $OUT
 BA="--steps 1 --warmup 0 --no-cpu-baseline"
-timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 200 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
+timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
 timeout -k 10 600 python bench.py > $OUT/bench.log 2>&1 && \
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- python3 bench.py $BA > $OUT/kt.log 2>&1 && \
