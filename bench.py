@@ -34,14 +34,38 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
-def load_lines(W, occluders):
+def load_lines(W, occluders, lmin=0.02, lmax=0.10):
     p = os.path.join(REPO, "tests", "golden", "inputs", "syn%d.csv" % W)
     if occluders == 50 and os.path.exists(p):
         from tests.golden_io import read_csv_lines
         return read_csv_lines(p)
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
     from gen_synthetic import make_lines
-    return np.array(make_lines(W, occluders, seed=1), dtype=np.float64)
+    return np.array(make_lines(W, occluders, seed=1, lmin=lmin, lmax=lmax), dtype=np.float64)
+
+
+def nearest_filled(pm, x, y):
+    """STEPDEPTH -sdp x,y on the synthetic config-5 grid: the cell under (x, y), moved to the nearest
+    FILLED cell when an occluder blocks it."""
+    i = pm.info()
+    rows, cols = i["rows"], i["cols"]
+    st = pm.state()
+    c0 = pm.pixelate(x, y)
+    x0, y0 = c0 // rows, c0 % rows
+    for r in range(max(rows, cols)):
+        best = None
+        for dx in range(-r, r + 1):
+            for dy in range(-r, r + 1):
+                if max(abs(dx), abs(dy)) != r:
+                    continue
+                xx, yy = x0 + dx, y0 + dy
+                if 0 <= xx < cols and 0 <= yy < rows and (st[xx * rows + yy] & 2):
+                    d = dx * dx + dy * dy
+                    if best is None or d < best[0]:
+                        best = (d, xx * rows + yy)
+        if best is not None:
+            return best[1]
+    raise RuntimeError("no filled cell")
 
 
 def load_traffic(workload):
@@ -93,12 +117,38 @@ def cpu_baseline(region, lines, spacing, fill, g, budget_s):
             "makegraph_s_per_source": mk_per_src, "vga_s_per_source": vga_per_src}
 
 
+def cpu_baseline_mk(region, lines, spacing, fill, N, budget_s):
+    """Config 5: the C restatement's makeGraph timed single-threaded on a contiguous source block.
+    The step-depth leg is not sampled (it needs the whole ~94 GB graph on the host), so the CPU
+    figure omits it and overstates the CPU rate."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from pyoracle import OracleMap
+    om = OracleMap(region, spacing, lines)
+    om.fill(*fill)
+    mid, k = N // 2, 4
+    while True:
+        t0 = time.perf_counter()
+        om.make_graph(node_begin=mid, node_end=min(N, mid + k), threads=1)
+        t_mk = time.perf_counter() - t0
+        if t_mk > 0.5 * budget_s or mid + k >= N:
+            break
+        k = min(N - mid, max(k * 2, int(k * 0.5 * budget_s / max(t_mk, 1e-3))))
+    k = min(k, N - mid)
+    return {"value": k / t_mk, "unit": "cells/s", "cores": 1, "kind": "port",
+            "sample": "oracle/dmx_oracle.c single thread: makeGraph on %d sources (%.2f s) from node %d; "
+                      "step depth not sampled (CPU rate overstated)" % (k, t_mk, mid),
+            "makegraph_s_per_source": t_mk / k}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--grid", type=int, default=1000, help="W: region [0,W]^2 at spacing 1 -> (W+1)^2 cells")
+    ap.add_argument("--config", type=int, choices=[1, 2, 5], default=2,
+                    help="BASELINE.json configs[i]: 2 = 1000^2 makeGraph + VGA global (default), 1 = 256^2, "
+                         "5 = 2000^2/5000 occluders makeGraph + metric step depth")
+    ap.add_argument("--grid", type=int, default=None, help="W: region [0,W]^2 at spacing 1 -> (W+1)^2 cells")
     ap.add_argument("--occluders", type=int, default=50)
     ap.add_argument("--mk-mode", choices=["auto", "shard", "replicate"], default="auto")
     ap.add_argument("--prep-mode", choices=["shard", "replicate"], default="shard",
@@ -128,11 +178,15 @@ def main():
     from depthmapx_amd.sharded import (allgather_blobs, allgather_rows_chunked, prep_allreduce, shard_range,
                                        vga_nodes)
 
-    W = args.grid
+    stepdepth = args.config == 5
+    if stepdepth:
+        W, args.occluders, lmin, lmax = 1999, 5000, 0.0025, 0.01
+    else:
+        W, lmin, lmax = args.grid or (256 if args.config == 1 else 1000), 0.02, 0.10
     mk_mode = args.mk_mode
     if mk_mode == "auto":
         mk_mode = "shard"
-    lines = load_lines(W, args.occluders)
+    lines = load_lines(W, args.occluders, lmin, lmax)
     region = [0.0, 0.0, float(W), float(W)]
     fill = (0.5, 0.5)
     ctx = dmx.Context(local)
@@ -144,8 +198,14 @@ def main():
     vnodes = vga_nodes(N, rank, world) if world > 1 else None   # VGA sources of this rank
     workload = "synthetic-%d/%d-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + VGA -vm visibility -vg -vr n" % (
         W, args.occluders)
+    sd_cell = None
+    if stepdepth:
+        sd_cell = nearest_filled(pm, W / 2 + 0.5, W / 2 + 0.5)
+        workload = ("synthetic-%d/%d-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + STEPDEPTH -sdt metric -sdp "
+                    "%g,%g (cell %d)" % (W, args.occluders, W / 2 + 0.5, W / 2 + 0.5, sd_cell))
 
-    out_full = torch.full((N, 7), -1.0, dtype=torch.float32, device=dev)
+    out_full = None if stepdepth else torch.full((N, 7), -1.0, dtype=torch.float32, device=dev)
+    sd_out = [None]
     kt = {"makegraph_s": 0.0, "vga_s": 0.0, "n": 0}
     stats = {}
 
@@ -167,6 +227,18 @@ def main():
             del flat, blob, shard
         else:
             g = shard
+        if stepdepth:
+            # 3'. metric step depth from one cell: a single-source Dijkstra, replicas only (every rank
+            #     holds the whole graph and runs the same selection)
+            sd_out[0] = g.metric_step_depth(cells=[sd_cell])
+            t_sd = ctx.last_stepdepth()["seconds"]
+            if record:
+                kt["makegraph_s"] += t_mk
+                kt["vga_s"] += t_sd
+                kt["n"] += 1
+                st.update({"sd_" + k: v for k, v in ctx.last_stepdepth().items()})
+                stats.update(st)
+            return g
         # 3. VGA global for this rank's sources (node chunks dealt round-robin: balanced BFS cost);
         #    the O(runs) pre-passes are split by contiguous node range, partials all-reduced
         if world > 1:
@@ -221,7 +293,15 @@ def main():
         tvw = th * ((tw + 63) // 64)
         vga_bytes = (8 * stats.get("vga_runs_expanded", 0) + 16 * tw * th * nsrc + 32 * tw * th * levels +
                      2 * stats.get("vga_tvis_bytes", 0) + 8 * tvw * stats.get("vga_b_tiles", 0))
-        dominant = "vga_tile_kernel" if vga_s >= mk_s else "makegraph_kernel"
+        second = "vga_tile_kernel"
+        if stepdepth:
+            # expanders' run records (average runs per node: the per-expander counts are not exported)
+            # + one 8 B relaxation record per relaxed cell
+            runs_per_node = g.info()["nruns"] / max(N, 1)
+            vga_bytes = int(8 * runs_per_node * stats.get("sd_expanders_popped", 0) +
+                            8 * stats.get("sd_cells_relaxed", 0))
+            second = "stepdepth_kernel"
+        dominant = second if vga_s >= mk_s else "makegraph_kernel"
         dom_bytes, dom_s = (vga_bytes, vga_s) if vga_s >= mk_s else (mk_bytes, mk_s)
         achieved = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
         traffic = load_traffic(workload)
@@ -258,11 +338,23 @@ def main():
             "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": tr},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if stepdepth:
+            rec["metric"] = "grid cells/sec for VISPREP makeGraph + metric step depth on N×N grid"
+            kk = rec["kernels"]
+            for k in [k for k in kk if k.startswith("vga")]:
+                del kk[k]
+            kk.update({"stepdepth_s": vga_s, "stepdepth_expanders_popped": stats.get("sd_expanders_popped"),
+                       "stepdepth_cells_relaxed": stats.get("sd_cells_relaxed"),
+                       "stepdepth_algorithmic_bytes": vga_bytes,
+                       "stepdepth_reached_cells": int((sd_out[0][:, 0] >= 0).sum())})
+        if not args.no_cpu_baseline and world == 1 and stepdepth:
+            rec["cpu_baseline"] = cpu_baseline_mk(region, lines, 1.0, fill, N, args.cpu_budget)
+            rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
+        elif not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, g, args.cpu_budget)
             rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
         print(json.dumps(rec), flush=True)
-        if args.dump_out:
+        if args.dump_out and out_full is not None:
             np.save(args.dump_out, out_full.cpu().numpy())
     if world > 1:
         dist.destroy_process_group()

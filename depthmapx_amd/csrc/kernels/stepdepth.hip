@@ -27,7 +27,8 @@ namespace dmx {
 constexpr int SD_THREADS = 1024;
 constexpr int SD_WIN = 4096;       // LDS queue window (u64 keys)
 constexpr int SD_CHUNKQ = 4096;    // LDS queue of long-run chunks
-constexpr int SD_CHUNK = 128;      // cells per chunk
+constexpr int SD_CHUNK = 32;       // cells per chunk
+constexpr int SD_BATCH = 8;        // cells whose state one lane loads at once
 constexpr unsigned long long SD_INF = ~0ull;
 
 enum : uint8_t { SDF_FILLED = 1, SDF_EXPAND = 2 };
@@ -95,16 +96,14 @@ __device__ __forceinline__ float sd_turn(int dx, int dy, int ux, int uy, int las
 // here.angle + ang < cumangle (floats), and a cell reached with angle 0 expands too
 // (Node::extractAngular expands when curs.angle == 0, ngraph.cpp:78-85).
 template <bool ANG>
-__device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, int x, int y, int ux, int uy, float du,
-                                         float cumu, int lastu, unsigned long long ku, unsigned& relaxed) {
-    const int64_t c = (int64_t)x * P.rows + y;
-    const uint8_t f = P.flags[c];
+__device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, int64_t c, int x, int y, uint8_t f,
+                                         unsigned long long kv, float mv, int ux, int uy, float du, float cumu,
+                                         int lastu, unsigned long long ku, unsigned& relaxed) {
     if (!(f & SDF_FILLED)) return;        // diagonal-gap cells never resolve (p.filled() check)
-    const unsigned long long kv = P.key[c];
     if (kv < ku) return;                  // already popped: m_misc == ~0
     relaxed++;
     if (ANG) {
-        const float cv = P.cum[c];
+        const float cv = mv;              // P.cum[c]
         if (cv != -1.0f && !(du < cv)) return;   // ang >= 0 (or NaN): du + ang < cv cannot hold
         const float ang = sd_turn(x - ux, y - uy, ux, uy, lastu);
         if (cv == -1.0f || du + ang < cv) {
@@ -121,7 +120,7 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
     }
     const int dx = x - ux, dy = y - uy;
     const double dd = sqrt((double)(dx * dx + dy * dy));
-    const float md = P.mdist[c];
+    const float md = mv;                  // P.mdist[c]
     if (md == -1.0f || (double)du + dd < (double)md) {
         const float nd = du + (float)dd;
         P.mdist[c] = nd;
@@ -131,6 +130,42 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
             P.key[c] = nk;
             P.lastpix[c] = pix_of(ux, uy);
             if (f & SDF_EXPAND) sd_push(S, P, nk);
+        }
+    }
+}
+
+// Cells [i0, i1) of run ru relaxed from expander u.  The cells of one expander's runs are distinct
+// (every visible cell sits in one bin; diagonal gap cells lie on that bin's own diagonal), so the
+// per-cell state of a batch of SD_BATCH cells is loaded up front -- up to 3*SD_BATCH independent
+// loads in flight per lane instead of three dependent round trips per cell.
+template <bool ANG>
+__device__ __forceinline__ void sd_relax_span(SdShared& S, const StepDepthParams& P, const Run& ru, int i0, int i1,
+                                              int ux, int uy, float du, float cumu, int lastu,
+                                              unsigned long long ku, unsigned& relaxed) {
+    const int dxs = (ru.x1 > ru.x0) ? 1 : 0;
+    const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
+    const float* mvp = ANG ? P.cum : P.mdist;
+    for (int b = i0; b < i1; b += SD_BATCH) {
+        const int n = min(SD_BATCH, i1 - b);
+        uint8_t f[SD_BATCH];
+        unsigned long long kv[SD_BATCH];
+        float mv[SD_BATCH];
+#pragma unroll
+        for (int j = 0; j < SD_BATCH; j++) {
+            if (j < n) {
+                const int64_t c = (int64_t)(ru.x0 + (b + j) * dxs) * P.rows + (ru.y0 + (b + j) * dys);
+                f[j] = P.flags[c];
+                kv[j] = P.key[c];
+                mv[j] = mvp[c];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < SD_BATCH; j++) {
+            if (j < n) {
+                const int x = ru.x0 + (b + j) * dxs, y = ru.y0 + (b + j) * dys;
+                sd_relax<ANG>(S, P, (int64_t)x * P.rows + y, x, y, f[j], kv[j], mv[j], ux, uy, du, cumu, lastu, ku,
+                              relaxed);
+            }
         }
     }
 }
@@ -260,19 +295,12 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
         // ---- relax: runs up to SD_CHUNK cells by their thread, longer tails through the chunk queue
         for (int r = tid; r < nr; r += SD_THREADS) {
             const Run ru = P.pool[rs + r];
-            const int dxs = (ru.x1 > ru.x0) ? 1 : 0;
-            const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
             const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
-            const int own = min(len, SD_CHUNK);
-            for (int i = 0; i < own; i++) sd_relax<ANG>(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+            sd_relax_span<ANG>(S, P, ru, 0, min(len, SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
             for (int o = SD_CHUNK; o < len; o += SD_CHUNK) {
                 const int q = atomicAdd(&S.nchunk, 1);
-                if (q < SD_CHUNKQ) {
-                    S.chunk[q] = make_int2(r, o);
-                } else {
-                    const int e = min(len, o + SD_CHUNK);
-                    for (int i = o; i < e; i++) sd_relax<ANG>(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
-                }
+                if (q < SD_CHUNKQ) S.chunk[q] = make_int2(r, o);
+                else sd_relax_span<ANG>(S, P, ru, o, min(len, o + SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
             }
         }
         __syncthreads();
@@ -280,11 +308,8 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
         for (int j = tid; j < nch; j += SD_THREADS) {
             const int2 ch = S.chunk[j];
             const Run ru = P.pool[rs + ch.x];
-            const int dxs = (ru.x1 > ru.x0) ? 1 : 0;
-            const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
             const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
-            const int e = min(len, ch.y + SD_CHUNK);
-            for (int i = ch.y; i < e; i++) sd_relax<ANG>(S, P, ru.x0 + i * dxs, ru.y0 + i * dys, ux, uy, du, cumu, lastu, ku, relaxed);
+            sd_relax_span<ANG>(S, P, ru, ch.y, min(len, ch.y + SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
         }
         __syncthreads();
     }
