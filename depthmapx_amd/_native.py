@@ -47,6 +47,7 @@ SIGNATURES = {
     "dmx_angular_stepdepth": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "dmx_release_cached_memory": (_i32, []),
     "dmx_ctx_last_stepdepth": (_i32, [_vp, _vp, _vp, _vp]),
+    "dmx_ctx_last_stepdepth_detail": (_i32, [_vp, _vp]),
     "dmx_ctx_last_phase_cycles": (_i32, [_vp, _vp]),
     "dmx_chunk_write": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "dmx_pointmap_set_state": (_i32, [_vp, _vp]),

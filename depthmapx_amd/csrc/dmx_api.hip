@@ -146,7 +146,9 @@ struct dmx_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int num_cu = 0;
     double last_mk_s = 0, last_vga_s = 0, last_sd_s = 0;
-    long long last_sd_stats[3] = {0, 0, 0};
+    long long last_sd_stats[3] = {0, 0, 0};   // expanders popped, cells relaxed, batches (serial: refills)
+    long long last_sd_extra[2] = {0, 0};      // batched: improved cells, ambiguous cells
+    int last_sd_mode = 0;                     // 0 serial, 1 batched, 2 batched overflow -> serial
     long long phase_cycles[5] = {0, 0, 0, 0, 0};   // tile BFS: level 1, A, B, C, bookkeeping (sum over workgroups)
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
@@ -1556,6 +1558,114 @@ int dmx_graph_set_prep_shard(dmx_graph* g, int64_t node_begin, int64_t node_end,
 }
 
 // ---------------------------------------------------------------- metric step depth
+// Batched metric search (stepdepth.hip): key/mdist/cum/lastpix are left in the VGAMetricDepth end
+// state.  Returns DMX_OK, a negative status on a HIP error, or 1 when a batch capacity overflowed
+// (the caller then re-runs the selection with the serial kernel).
+static int stepdepth_batched(dmx_ctx* ctx, dmx_graph* g, const std::vector<uint8_t>& flags,
+                             const std::vector<int32_t>& sel, const uint8_t* d_flags, const int32_t* d_sel,
+                             unsigned long long* d_key, float* d_mdist, float* d_cum, int32_t* d_last) {
+    PointMapHost& h = *g->pm->host;
+    const int rows = h.rows();
+    const int64_t C = (int64_t)h.cols() * rows;
+    hipStream_t s = ctx->stream;
+    std::vector<int32_t> ex;
+    for (int64_t c = 0; c < C; c++)
+        if (flags[(size_t)c] & SDF_EXPAND) ex.push_back((int32_t)c);
+    const int64_t E = (int64_t)ex.size();
+    // work units: ceil(runs / SDB_UNIT) per expander
+    std::vector<int32_t> nr((size_t)g->nnodes);
+    HIPCHK(hipStreamSynchronize(s));
+    if (g->nnodes) HIPCHK(hipMemcpy(nr.data(), g->node_nruns.p, g->nnodes * 4, hipMemcpyDeviceToHost));
+    int64_t units = 0;
+    const auto& nc = g->pm->node_cell;   // ascending cell index = node order
+    for (int32_t c : ex) {
+        const size_t node = (size_t)(std::lower_bound(nc.begin(), nc.end(), c) - nc.begin());
+        units += (nr[node] + SDB_UNIT - 1) / SDB_UNIT;
+    }
+    const unsigned amb_cap = 1u << 16, ent_cap = 1u << 22;
+    DevBuf<int32_t> d_ex, d_uown, d_win, d_ambid, d_touch, d_amb;
+    DevBuf<uint8_t> d_done;
+    DevBuf<SdbExp> d_bq;
+    DevBuf<unsigned long long> d_best;
+    DevBuf<unsigned> d_nnear;
+    DevBuf<int2> d_ent;
+    DevBuf<SdbCtl> d_ctl;
+    HIPCHK(d_ex.alloc(std::max<int64_t>(E, 1)));
+    HIPCHK(d_done.alloc(std::max<int64_t>(E, 1)));
+    HIPCHK(d_bq.alloc(std::max<int64_t>(E, 1)));
+    HIPCHK(d_uown.alloc(std::max<int64_t>(units, 1)));
+    HIPCHK(d_best.alloc(C));
+    HIPCHK(d_nnear.alloc(C));
+    HIPCHK(d_win.alloc(C));
+    HIPCHK(d_ambid.alloc(C));
+    HIPCHK(d_touch.alloc(C));
+    HIPCHK(d_amb.alloc(amb_cap));
+    HIPCHK(d_ent.alloc(ent_cap));
+    HIPCHK(d_ctl.alloc(1));
+    if (E) HIPCHK(hipMemcpyAsync(d_ex.p, ex.data(), E * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_done.p, 0, std::max<int64_t>(E, 1), s));
+    HIPCHK(hipMemsetAsync(d_best.p, 0xFF, C * 8, s));
+    HIPCHK(hipMemsetAsync(d_nnear.p, 0, C * 4, s));
+    HIPCHK(hipMemsetAsync(d_ambid.p, 0xFF, C * 4, s));
+    HIPCHK(hipMemsetAsync(d_key, 0xFF, C * 8, s));
+    std::vector<float> m1((size_t)C, -1.0f);
+    HIPCHK(hipMemcpyAsync(d_mdist, m1.data(), C * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(d_cum, 0, C * 4, s));
+    HIPCHK(hipMemsetAsync(d_last, 0xFF, C * 4, s));
+    SdbCtl c0;
+    memset(&c0, 0, sizeof(c0));
+    c0.gcur = 0ull;            // the selected cells' distance 0
+    c0.gnext = SD_INF;
+    HIPCHK(hipMemcpyAsync(d_ctl.p, &c0, sizeof(c0), hipMemcpyHostToDevice, s));
+    SdbParams P;
+    P.rows = rows; P.E = E; P.flags = d_flags; P.cell_node = g->pm->d_cell_node.p;
+    P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
+    P.key = d_key; P.mdist = d_mdist; P.cum = d_cum; P.lastpix = d_last;
+    P.ex_cells = d_ex.p; P.ex_done = d_done.p; P.bq = d_bq.p; P.uown = d_uown.p;
+    P.best = d_best.p; P.nnear = d_nnear.p; P.win = d_win.p; P.ambid = d_ambid.p; P.touch = d_touch.p;
+    P.amb = d_amb.p; P.ent = d_ent.p; P.ent_cap = ent_cap; P.amb_cap = amb_cap; P.ctl = d_ctl.p;
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipEventRecord(ctx->ev0, s));
+    hipLaunchKernelGGL(sdb_init_kernel, dim3((unsigned)((sel.size() + 255) / 256)), dim3(256), 0, s, P, d_sel,
+                       (int)sel.size());
+    HIPCHK(hipGetLastError());
+    const unsigned gs = (unsigned)std::max<int64_t>(1, (E + 255) / 256);
+    const unsigned gr = (unsigned)std::max(64, ctx->num_cu * 4);
+    SdbCtl hc;
+    // Batches advance the smallest live distance by >= 1 - 2^-18; the number of batches is bounded
+    // by the longest path length, itself < C grid units.
+    const int64_t max_it = 2 * C + 64;
+    int64_t it = 0;
+    for (;;) {
+        for (int k = 0; k < 32; k++, it++) {
+            hipLaunchKernelGGL(sdb_select_kernel, dim3(gs), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(sdb_relax_kernel<1>, dim3(gr), dim3(SDB_THREADS), 0, s, P);
+            hipLaunchKernelGGL(sdb_relax_kernel<2>, dim3(gr), dim3(SDB_THREADS), 0, s, P);
+            hipLaunchKernelGGL(sdb_apply_kernel, dim3(gr), dim3(256), 0, s, P);
+            hipLaunchKernelGGL(sdb_relax_kernel<3>, dim3(gr), dim3(SDB_THREADS), 0, s, P);
+            hipLaunchKernelGGL(sdb_fold_kernel, dim3(256), dim3(SDB_THREADS), 0, s, P);
+            hipLaunchKernelGGL(sdb_finish_kernel, dim3(1), dim3(1), 0, s, P);
+        }
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(&hc, d_ctl.p, sizeof(hc), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (hc.done) break;
+        if (it > max_it) return fail(DMX_ERR_STATE, "batched step depth did not terminate");
+    }
+    HIPCHK(hipEventRecord(ctx->ev1, s));
+    HIPCHK(hipEventSynchronize(ctx->ev1));
+    if (hc.error) return 1;
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_sd_s = ms * 1e-3;
+    ctx->last_sd_stats[0] = (long long)hc.popped;
+    ctx->last_sd_stats[1] = (long long)hc.relaxed;
+    ctx->last_sd_stats[2] = (long long)hc.batches;
+    ctx->last_sd_extra[0] = (long long)hc.improved;
+    ctx->last_sd_extra[1] = (long long)hc.ambiguous;
+    return DMX_OK;
+}
+
 // STEPDEPTH -sdt metric (VGAMetricDepth) or, with ANG, -sdt angular (VGAAngularDepth): one search
 // from the selection; out [N][3] (metric) or [N] (angular).
 extern "C++" template <bool ANG>
@@ -1611,6 +1721,30 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
     HIPCHK(hipMemcpyAsync(d_flags.p, flags.data(), C, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(d_sel.p, sel.data(), sel.size() * 4, hipMemcpyHostToDevice, s));
     int64_t cap = 8 * (nexp + (int64_t)sel.size()) + SD_WIN + 1024 + (ANG ? 8 * N : 0);
+    // metric: the batched search over the whole GPU (stepdepth.hip, "batched metric step depth");
+    // DMX_SD_KERNEL=serial forces the one-workgroup kernel, which is also the fallback
+    bool batched = !ANG;
+    if (const char* e = getenv("DMX_SD_KERNEL")) batched = batched && strcmp(e, "serial") != 0;
+    ctx->last_sd_mode = 0;
+    if (batched) {
+        int rc = stepdepth_batched(ctx, g, flags, sel, d_flags.p, d_sel.p, d_key.p, d_mdist.p, d_cum.p, d_last.p);
+        if (rc < 0) return rc;
+        if (rc == DMX_OK) {
+            const int single = sel.size() == 1 ? 1 : 0;
+            if (N) {
+                hipLaunchKernelGGL(stepdepth_out_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rows,
+                                   h.spacing(), g->pm->d_node_cell.p, N, d_key.p, d_cum.p, single, sel[0] / rows,
+                                   sel[0] % rows, d_out.p);
+                HIPCHK(hipGetLastError());
+                HIPCHK(hipMemcpyAsync(out, d_out.p, N * 3 * 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
+            ctx->last_sd_mode = 1;
+            return DMX_OK;
+        }
+        // rc > 0: a batch capacity overflowed; the serial search below redoes the whole selection
+        ctx->last_sd_mode = 2;
+    }
     for (int attempt = 0; attempt < 4; attempt++) {
         HIPCHK(d_over.alloc(cap));
         HIPCHK(hipMemsetAsync(d_key.p, 0xFF, C * 8, s));
@@ -1744,6 +1878,15 @@ int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_pop
     if (seconds) *seconds = ctx->last_sd_s;
     if (expanders_popped) *expanders_popped = ctx->last_sd_stats[0];
     if (cells_relaxed) *cells_relaxed = ctx->last_sd_stats[1];
+    return DMX_OK;
+}
+
+int dmx_ctx_last_stepdepth_detail(dmx_ctx* ctx, int64_t* out4) {
+    if (!ctx || !out4) return fail(DMX_ERR_ARG, "bad arguments");
+    out4[0] = ctx->last_sd_mode;
+    out4[1] = ctx->last_sd_stats[2];
+    out4[2] = ctx->last_sd_extra[0];
+    out4[3] = ctx->last_sd_extra[1];
     return DMX_OK;
 }
 

@@ -329,6 +329,313 @@ __global__ void __launch_bounds__(SD_THREADS) stepdepth_kernel(StepDepthParams P
     if (tid == 0) { P.stats[0] = popped; P.stats[2] = refills; }
 }
 
+// ---------------------------------------------------------------- batched metric step depth
+// The serial loop above pops one expander at a time.  Every relaxation adds dist(u, v) >= 1 grid
+// unit, so no expander whose key lies below dmin + 1 (dmin = the smallest live key) can still be
+// improved by any other live expander: all of them are final, and they form one batch whose
+// relaxations run over the whole GPU.  What the batch must still reproduce is the reference's
+// order-dependent fold of the batch's relaxations of one cell v (Bin::extractMetric,
+// ngraph.cpp:330-345, applied in pop order):
+//     if (md == -1 || du + dd < md) { md = du + float(dd); cum = cum_u + turn; set entry (md, v, u) }
+// Let s = du + dd (double) and f = du + float(dd) (float): |f - s| <= 2^-23 s.  If the smallest
+// candidate s_m has no rival within W = 2^-20 s_m, the fold's outcome is exactly "apply m's update
+// to the pre-batch state": an earlier success j leaves md = f_j > s_m, so m still succeeds, and after
+// m every later candidate has s > f_m.  Candidates with s > md0 (1 + 2^-20) can then never succeed
+// and are skipped.  Cells with a near rival ("ambiguous": exact ties on the grid are common) are
+// folded sequentially in pop order from the list of all their batch relaxers.  A batch is the
+// contiguous key range below the threshold, so batches run in the reference's pop order.
+// Kernels per batch: select -> relax<1> (min s) -> relax<2> (rivals) -> apply -> relax<3> (ambiguous
+// relaxer lists) -> fold -> finish.  Any capacity overflow raises ctl.error and the host re-runs the
+// search with the serial kernel.
+constexpr int SDB_THREADS = 256;
+constexpr int SDB_UNIT = 256;          // runs of one expander per work unit (one workgroup)
+constexpr int SDB_FOLD_CAP = 2048;     // relaxers of one ambiguous cell in one batch
+
+struct SdbExp {
+    int64_t rs;                 // first run of the expander's node in the pool
+    unsigned long long ku;      // the expander's key (pop order)
+    float du, cumu;
+    int ux, uy, lastu, nr, ubase, pad;
+};
+
+struct SdbCtl {
+    unsigned long long gcur, gnext;   // smallest live expander key: this batch / the next one
+    unsigned nb, nunits, ntouch, namb, nent, done, error, batches;
+    unsigned long long relaxed, improved, ambiguous, popped;
+};
+
+struct SdbParams {
+    int rows;
+    int64_t E;
+    const uint8_t* flags;
+    const int32_t* cell_node;
+    const int64_t* node_run_start;
+    const int32_t* node_nruns;
+    const Run* pool;
+    unsigned long long* key;
+    float* mdist;
+    float* cum;
+    int32_t* lastpix;
+    const int32_t* ex_cells;      // [E] expander cells (BLOCKED, blocked-adjacent, selected)
+    uint8_t* ex_done;             // [E] popped
+    SdbExp* bq;                   // [E] batch
+    int32_t* uown;                // [units] batch index of each work unit
+    unsigned long long* best;     // [C] smallest candidate s of the batch (double bits), ~0 = none
+    unsigned* nnear;              // [C] candidates within W of best
+    int32_t* win;                 // [C] batch index of the candidate at best
+    int32_t* ambid;               // [C] ambiguous-cell index, -1
+    int32_t* touch;               // [C] cells with a candidate this batch
+    int32_t* amb;                 // [amb_cap] ambiguous cells
+    int2* ent;                    // [ent_cap] (ambiguous index, batch index)
+    unsigned ent_cap, amb_cap;
+    SdbCtl* ctl;
+};
+
+__device__ __forceinline__ double sdb_w(double s) { return s * 0x1p-20; }
+
+// Append `want` lanes of the wave to a list: one atomic per wave.
+__device__ __forceinline__ unsigned sdb_wave_append(unsigned* counter, bool want) {
+    const unsigned long long m = __ballot(want);
+    if (!m) return 0;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(counter, (unsigned)__popcll(m));
+    base = __shfl(base, leader);
+    return base + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+}
+
+__global__ void sdb_select_kernel(SdbParams P) {
+    SdbCtl& C = *P.ctl;
+    const unsigned long long g = C.gcur;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g == SD_INF || C.error) return;
+    bool take = false;
+    int c = 0;
+    unsigned long long k = SD_INF;
+    if (e < P.E && !P.ex_done[e]) {
+        c = P.ex_cells[e];
+        k = P.key[c];
+        if (k != SD_INF) {
+            const double lim = (double)__uint_as_float((unsigned)(g >> 32)) + 1.0;
+            if ((double)__uint_as_float((unsigned)(k >> 32)) < lim - lim * 0x1p-18) take = true;
+            else atomicMin(&C.gnext, k);
+        }
+    }
+    const unsigned bi = sdb_wave_append(&C.nb, take);
+    if (!take) return;
+    P.ex_done[e] = 1;
+    const int node = P.cell_node[c];
+    SdbExp X;
+    X.rs = P.node_run_start[node];
+    X.nr = P.node_nruns[node];
+    X.ku = k;
+    X.du = __uint_as_float((unsigned)(k >> 32));
+    X.cumu = P.cum[c];
+    X.ux = c / P.rows;
+    X.uy = c % P.rows;
+    X.lastu = P.lastpix[c];
+    const int nu = (X.nr + SDB_UNIT - 1) / SDB_UNIT;
+    X.ubase = (int)atomicAdd(&C.nunits, (unsigned)nu);
+    X.pad = 0;
+    P.bq[bi] = X;
+    for (int j = 0; j < nu; j++) P.uown[X.ubase + j] = (int)bi;
+}
+
+// PH 1: candidate minimum per cell; PH 2: rivals within W of it; PH 3: relaxer lists of the
+// ambiguous cells.  One workgroup per (expander, <= SDB_UNIT runs); the unit's cells are spread over
+// the threads through an LDS prefix sum of the run lengths.
+template <int PH>
+__global__ void __launch_bounds__(SDB_THREADS) sdb_relax_kernel(SdbParams P) {
+    __shared__ Run runs[SDB_UNIT];
+    __shared__ int off[SDB_UNIT + 1];
+    __shared__ int wsum[SDB_THREADS / 64];
+    SdbCtl& C = *P.ctl;
+    if (C.error) return;
+    if (PH == 3 && C.namb == 0) return;
+    const unsigned nunits = C.nunits;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    unsigned long long relaxed = 0;
+    for (unsigned u = blockIdx.x; u < nunits; u += gridDim.x) {
+        const int b = P.uown[u];
+        const SdbExp X = P.bq[b];
+        const int r0 = ((int)u - X.ubase) * SDB_UNIT;
+        const int nr = min(SDB_UNIT, X.nr - r0);
+        int len = 0;
+        if (t < nr) {
+            const Run ru = P.pool[X.rs + r0 + t];
+            runs[t] = ru;
+            len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+        }
+        int inc = len;   // inclusive wave scan, then the wave totals
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(inc, o);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        int base = 0;
+        for (int w = 0; w < wave; w++) base += wsum[w];
+        off[t + 1] = base + inc;
+        if (t == 0) off[0] = 0;
+        __syncthreads();
+        const int T = off[nr];
+        for (int i = t; i < T; i += SDB_THREADS) {
+            int lo = 0, hi = nr - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (off[mid] <= i) lo = mid;
+                else hi = mid - 1;
+            }
+            const Run ru = runs[lo];
+            const int k = i - off[lo];
+            const int dxs = (ru.x1 > ru.x0) ? 1 : 0;
+            const int dys = (ru.y0 == ru.y1) ? 0 : ((ru.x0 == ru.x1) ? 1 : ((ru.y1 > ru.y0) ? 1 : -1));
+            const int x = ru.x0 + k * dxs, y = ru.y0 + k * dys;
+            const int64_t c = (int64_t)x * P.rows + y;
+            bool cand = false;
+            double s = 0.0;
+            if (P.flags[c] & SDF_FILLED) {
+                if (P.key[c] >= X.ku) {   // not popped before u (m_misc == 0)
+                    const int dx = x - X.ux, dy = y - X.uy;
+                    s = (double)X.du + sqrt((double)(dx * dx + dy * dy));
+                    if (PH == 3) {
+                        cand = P.ambid[c] >= 0;
+                    } else {
+                        const float md = P.mdist[c];
+                        cand = md == -1.0f || s <= (double)md + sdb_w((double)md);
+                    }
+                    if (PH == 1) relaxed++;
+                }
+            }
+            if (PH == 1) {
+                bool first = false;
+                if (cand) first = atomicMin(&P.best[c], (unsigned long long)__double_as_longlong(s)) == SD_INF;
+                const unsigned pos = sdb_wave_append(&C.ntouch, first);
+                if (first) P.touch[pos] = (int32_t)c;
+            } else if (PH == 2) {
+                if (cand) {
+                    const double bs = __longlong_as_double((long long)P.best[c]);
+                    if (s <= bs + sdb_w(bs)) {
+                        atomicAdd(&P.nnear[c], 1u);
+                        if (s == bs) P.win[c] = b;
+                    }
+                }
+            } else {
+                const unsigned pos = sdb_wave_append(&C.nent, cand);
+                if (cand) {
+                    if (pos < P.ent_cap) P.ent[pos] = make_int2(P.ambid[c], b);
+                    else C.error = 1;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (PH == 1) {
+        for (int o = 32; o >= 1; o >>= 1) relaxed += __shfl_xor(relaxed, o);
+        if (lane == 0 && relaxed) atomicAdd(&C.relaxed, relaxed);
+    }
+}
+
+// One relaxation of cell c = (x, y) from batch expander X, in the reference's sequential form
+// (sd_relax without the popped test, which the relax kernels already applied).
+__device__ __forceinline__ void sdb_update(const SdbParams& P, SdbCtl& C, int64_t c, int x, int y, uint8_t f,
+                                           const SdbExp& X) {
+    const int dx = x - X.ux, dy = y - X.uy;
+    const double dd = sqrt((double)(dx * dx + dy * dy));
+    const float md = P.mdist[c];
+    if (md == -1.0f || (double)X.du + dd < (double)md) {
+        const float nd = X.du + (float)dd;
+        P.mdist[c] = nd;
+        P.cum[c] = X.cumu + sd_turn(dx, dy, X.ux, X.uy, X.lastu);
+        const unsigned long long nk = sd_key(nd, pix_of(x, y));
+        if (nk < P.key[c]) {
+            P.key[c] = nk;
+            P.lastpix[c] = pix_of(X.ux, X.uy);
+            if (f & SDF_EXPAND) atomicMin(&C.gnext, nk);
+        }
+    }
+}
+
+__global__ void sdb_apply_kernel(SdbParams P) {
+    SdbCtl& C = *P.ctl;
+    if (C.error) return;
+    const unsigned n = C.ntouch;
+    for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const int c = P.touch[i];
+        const unsigned nn = P.nnear[c];
+        P.best[c] = SD_INF;
+        P.nnear[c] = 0u;
+        if (nn == 1u) {
+            const SdbExp X = P.bq[P.win[c]];
+            sdb_update(P, C, c, c / P.rows, c % P.rows, P.flags[c], X);
+        } else {
+            const unsigned a = atomicAdd(&C.namb, 1u);
+            if (a < P.amb_cap) {
+                P.amb[a] = c;
+                P.ambid[c] = (int)a;
+            } else {
+                C.error = 1;
+            }
+        }
+    }
+}
+
+// Sequential fold of each ambiguous cell over all its batch relaxers in pop (key) order.
+__global__ void __launch_bounds__(SDB_THREADS) sdb_fold_kernel(SdbParams P) {
+    __shared__ int lst[SDB_FOLD_CAP];
+    __shared__ int cnt;
+    SdbCtl& C = *P.ctl;
+    if (C.error) return;
+    const unsigned na = min(C.namb, P.amb_cap), ne = min(C.nent, P.ent_cap);
+    for (unsigned a = blockIdx.x; a < na; a += gridDim.x) {
+        if (threadIdx.x == 0) cnt = 0;
+        __syncthreads();
+        for (unsigned i = threadIdx.x; i < ne; i += SDB_THREADS) {
+            const int2 en = P.ent[i];
+            if (en.x == (int)a) {
+                const int p = atomicAdd(&cnt, 1);
+                if (p < SDB_FOLD_CAP) lst[p] = en.y;
+                else C.error = 1;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0 && cnt <= SDB_FOLD_CAP) {
+            const int c = P.amb[a];
+            const int n = cnt;
+            for (int i = 1; i < n; i++) {   // insertion sort by the relaxer's key (pop order)
+                const int v = lst[i];
+                const unsigned long long kv = P.bq[v].ku;
+                int j = i - 1;
+                while (j >= 0 && P.bq[lst[j]].ku > kv) { lst[j + 1] = lst[j]; j--; }
+                lst[j + 1] = v;
+            }
+            const uint8_t f = P.flags[c];
+            for (int i = 0; i < n; i++) sdb_update(P, C, c, c / P.rows, c % P.rows, f, P.bq[lst[i]]);
+            P.ambid[c] = -1;
+        }
+        __syncthreads();
+    }
+}
+
+// The selected cells enter at distance 0 (vgametricdepth.cpp:45-47).
+__global__ void sdb_init_kernel(SdbParams P, const int32_t* sel, int nsel) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nsel) P.key[sel[i]] = sd_key(0.0f, pix_of(sel[i] / P.rows, sel[i] % P.rows));
+}
+
+__global__ void sdb_finish_kernel(SdbParams P) {
+    SdbCtl& C = *P.ctl;
+    if (C.nb) C.batches++;
+    C.popped += C.nb;
+    C.improved += C.ntouch;
+    C.ambiguous += C.namb;
+    C.gcur = C.gnext;
+    C.gnext = SD_INF;
+    C.nb = 0; C.nunits = 0; C.ntouch = 0; C.namb = 0; C.nent = 0;
+    if (C.gcur == SD_INF || C.error) C.done = 1;
+}
+
 // ---------------------------------------------------------------- VGA metric (all sources)
 // VGAMetric::run (salalib/vgamodules/vgametric.cpp:26-136): the search above from every source,
 // one source per workgroup at a time (per-workgroup key / dist / angle arrays in HBM), followed by

@@ -53,7 +53,11 @@ class Context:
     def last_stepdepth(self):
         t, p, r = ctypes.c_double(), ctypes.c_int64(), ctypes.c_int64()
         N.check(N.lib().dmx_ctx_last_stepdepth(self.h, ctypes.byref(t), ctypes.byref(p), ctypes.byref(r)))
-        return dict(seconds=t.value, expanders_popped=p.value, cells_relaxed=r.value)
+        d = np.zeros(4, dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_stepdepth_detail(self.h, N.ptr(d)))
+        return dict(seconds=t.value, expanders_popped=p.value, cells_relaxed=r.value,
+                    mode=["serial", "batched", "batched-overflow-serial"][int(d[0])], batches=int(d[1]),
+                    improved=int(d[2]), ambiguous=int(d[3]))
 
     def last_phase_cycles(self):
         out = np.zeros(5, dtype=np.int64)

@@ -188,6 +188,10 @@ int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
 int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out);
 /* Kernel time of the last step-depth call, expanders popped, cells relaxed. */
 int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_popped, int64_t* cells_relaxed);
+/* How the last metric step depth ran: out4 = {mode (0 serial, 1 batched over the whole GPU, 2 a
+ * batch capacity overflowed and the serial kernel re-ran the search), batches (serial: queue
+ * refills), cells improved, ambiguous cells folded sequentially}. */
+int dmx_ctx_last_stepdepth_detail(dmx_ctx* ctx, int64_t* out4);
 
 /* ---- .graph PointMap chunk (host) ------------------------------------------------------------ */
 /* The bytes PointMap::write emits into a .graph file (salalib/pointdata.cpp:1158-1188, with

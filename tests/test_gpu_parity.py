@@ -280,6 +280,38 @@ def test_visual_stepdepth_random_matches_oracle(ctx, seed):
         assert got.max() >= 2
 
 
+def _dense_map(W, nocc, seed, lmin=0.0025, lmax=0.01):
+    from golden.gen_synthetic import make_lines
+    lines = np.array(make_lines(W, nocc, seed=seed, lmin=lmin, lmax=lmax), dtype=np.float64)
+    pm = dmx.PointMap([0.0, 0.0, float(W), float(W)], lines, 1.0)
+    assert pm.make_points(0.5, 0.5)
+    return pm
+
+
+@pytest.mark.parametrize("W,nocc,seed", [(48, 80, 3), (160, 400, 5), (300, 1500, 9)])
+def test_metric_stepdepth_batched_equals_serial(ctx, monkeypatch, W, nocc, seed):
+    """The whole-GPU batched search (distance windows of 1 grid unit, certified single winners,
+    sequential fold of ambiguous cells) reproduces the serial pop-order kernel bit-for-bit on all three
+    columns, for 1 and several selected cells (dense short occluders: many expanders)."""
+    pm = _dense_map(W, nocc, seed, lmin=0.01 if W < 100 else 0.0025, lmax=0.05 if W < 100 else 0.01)
+    g = pm.make_graph(ctx)
+    filled = np.nonzero(pm.state() & 2)[0]
+    rng = np.random.default_rng(seed)
+    for nsel in (1, 5):
+        cells = np.sort(rng.choice(filled, nsel, replace=False))
+        monkeypatch.delenv("DMX_SD_KERNEL", raising=False)
+        got = g.metric_step_depth(cells=cells)
+        sd = ctx.last_stepdepth()
+        assert sd["mode"] == "batched" and sd["batches"] > 1, sd
+        monkeypatch.setenv("DMX_SD_KERNEL", "serial")
+        want = g.metric_step_depth(cells=cells)
+        sd2 = ctx.last_stepdepth()
+        assert sd2["mode"] == "serial"
+        assert sd["expanders_popped"] == sd2["expanders_popped"]
+        assert sd["cells_relaxed"] == sd2["cells_relaxed"]
+        np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
+
+
 def test_metric_stepdepth_errors(ctx):
     meta, _ = load_case("syn32")
     pm = _map(meta)

@@ -218,3 +218,22 @@ def test_angular_stepdepth_matches_reference_bitexact(name):
     cells = (sel >> 16) * meta["rows"] + (sel & 0xFFFF)
     want = np.load(os.path.join(GOLDEN, name + "_astepdepth.npy"))
     np.testing.assert_array_equal(om.angular_stepdepth(cells).view(np.uint32), want.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["syn32", "gallery", "syn64"])
+def test_batched_stepdepth_schedule_matches_reference(name):
+    """The batched metric step-depth schedule (distance windows, certified single winners, ambiguous
+    cells folded in pop order), modelled in pure Python (tests/sd_batched_model.py), reproduces the
+    reference's VGAMetricDepth columns bit-for-bit.  Pins the schedule's mathematics on the CPU; the
+    GPU tests then pin the kernels to the serial pop-order kernel."""
+    from sd_batched_model import batched_metric_stepdepth
+    meta, A = load_case(name)
+    om = _oracle(meta)
+    om.make_graph(threads=8)
+    gr = om.graph()
+    sel = A["stepdepth_sel"]
+    cells = (sel >> 16) * meta["rows"] + (sel & 0xFFFF)
+    got, stats = batched_metric_stepdepth(om.state(), meta["rows"], meta["cols"], gr["bins"], gr["runs"], cells,
+                                          meta["spacing"])
+    assert stats["batches"] > 1
+    np.testing.assert_array_equal(got.view(np.uint32), A["stepdepth"].view(np.uint32))
