@@ -35,8 +35,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 
 
 def load_lines(W, occluders, lmin=0.02, lmax=0.10):
-    p = os.path.join(REPO, "tests", "golden", "inputs", "syn%d.csv" % W)
-    if occluders == 50 and os.path.exists(p):
+    p = os.path.join(REPO, "tests", "golden", "inputs", ("syn%d.csv" % W) if occluders == 50 else
+                     ("syn%d_%d.csv" % (W + 1, occluders)))
+    if os.path.exists(p):
         from tests.golden_io import read_csv_lines
         return read_csv_lines(p)
     sys.path.insert(0, os.path.join(REPO, "tests", "golden"))

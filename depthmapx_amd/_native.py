@@ -32,6 +32,7 @@ SIGNATURES = {
     "dmx_graph_free": (_i32, [_vp]),
     "dmx_graph_info": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_graph_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "dmx_graph_copy_range": (_i32, [_vp, _i64, _i64, _vp, _vp, _vp, _i64, _vp, _vp]),
     "dmx_graph_blob_size": (_i32, [_vp, _vp]),
     "dmx_graph_blob_write_device": (_i32, [_vp, _vp, _i64]),
     "dmx_graph_assemble_device": (_i32, [_vp, _vp, _vp, _vp, _i32, _vp]),

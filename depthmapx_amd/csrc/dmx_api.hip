@@ -43,6 +43,13 @@ bool verbose() {
     do {                                               \
         if (verbose()) fprintf(stderr, "[dmx] " __VA_ARGS__); \
     } while (0)
+// Every host<->device copy is ordered on the context's (non-blocking) stream: a plain hipMemcpy
+// runs on the null stream, which does not wait for the context stream's kernels.
+hipError_t copy_sync(hipStream_t s, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, s);
+    if (e != hipSuccess) return e;
+    return hipStreamSynchronize(s);
+}
 int fail(int code, const std::string& msg) {
     g_err = msg;
     return code;
@@ -538,7 +545,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
             kernel_s += ms * 1e-3;
             int hc[5] = {0, 0, 0, 0, 0};
-            HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+            HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
             const int err = hc[1], nfail = hc[4];
             VLOG("makegraph: attempt %d (%lld sources, gcap %d bcap %d spill %d capB %lld, occupancy %d): %.3f s, %d failed, "
                  "err %d\n", attempt, (long long)todo, gcap, bcap, spill_cap, (long long)capB, occ, ms * 1e-3, nfail, err);
@@ -575,11 +582,11 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
         kernel_s += ms * 1e-3;
         int hc[4] = {0, 0, 0, 0};
-        HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
         unsigned long long used = 0;
         std::memcpy(&used, &hc[2], 8);
         unsigned long long st[16];
-        HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
         if (verbose()) {
             double tot = 0;
             for (int i = 8; i < 16; i++) tot += (double)st[i];
@@ -615,20 +622,26 @@ int dmx_graph_info(const dmx_graph* g, int64_t* nnodes, int64_t* nb, int64_t* ne
     return DMX_OK;
 }
 
-int dmx_graph_copy(dmx_graph* g, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn) {
+int dmx_graph_copy_range(dmx_graph* g, int64_t kb, int64_t ke, float* attrs, int32_t* bins, int16_t* runs,
+                         int64_t runs_cap, int64_t* nruns_out, uint8_t* gridconn) {
     if (!g) return fail(DMX_ERR_ARG, "graph is NULL");
+    const int64_t nl = g->node_end - g->node_begin;
+    if (ke < 0) ke = nl;
+    if (kb < 0 || kb > ke || ke > nl) return fail(DMX_ERR_ARG, "node range outside the graph");
     HIPCHK(hipSetDevice(g->ctx->device));
-    const int64_t n = g->node_end - g->node_begin;
+    hipStream_t st = g->ctx->stream;
+    const int64_t n = ke - kb;
+    if (nruns_out) *nruns_out = 0;
     if (n == 0) return DMX_OK;
-    if (attrs) HIPCHK(hipMemcpy(attrs, g->attrs.p, n * 3 * 4, hipMemcpyDeviceToHost));
-    if (gridconn) HIPCHK(hipMemcpy(gridconn, g->gridconn.p, n, hipMemcpyDeviceToHost));
+    if (attrs) HIPCHK(copy_sync(st, attrs, g->attrs.p + kb * 3, n * 3 * 4, hipMemcpyDeviceToHost));
+    if (gridconn) HIPCHK(copy_sync(st, gridconn, g->gridconn.p + kb, n, hipMemcpyDeviceToHost));
     std::vector<int32_t> bn((size_t)n * 32);
-    HIPCHK(hipMemcpy(bn.data(), g->bin_nruns.p, n * 32 * 4, hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(st, bn.data(), g->bin_nruns.p + kb * 32, n * 32 * 4, hipMemcpyDeviceToHost));
     if (bins) {
         std::vector<uint16_t> bc((size_t)n * 32);
         std::vector<float> bd((size_t)n * 32);
-        HIPCHK(hipMemcpy(bc.data(), g->bin_count.p, n * 32 * 2, hipMemcpyDeviceToHost));
-        HIPCHK(hipMemcpy(bd.data(), g->bin_dist.p, n * 32 * 4, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(st, bc.data(), g->bin_count.p + kb * 32, n * 32 * 2, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(st, bd.data(), g->bin_dist.p + kb * 32, n * 32 * 4, hipMemcpyDeviceToHost));
         for (int64_t k = 0; k < n; k++)
             for (int b = 0; b < 32; b++) {
                 const int64_t i = k * 32 + b;
@@ -643,31 +656,33 @@ int dmx_graph_copy(dmx_graph* g, float* attrs, int32_t* bins, int16_t* runs, uin
                 bins[i * 4 + 3] = bn[i];
             }
     }
+    int64_t acc = 0;
+    std::vector<int64_t> dst((size_t)n);
+    for (int64_t k = 0; k < n; k++) {
+        int sum = 0;
+        for (int b = 0; b < 32; b++) sum += bn[k * 32 + b];
+        dst[k] = acc;
+        acc += sum;
+    }
+    if (nruns_out) *nruns_out = acc;
     if (runs) {
+        if (runs_cap >= 0 && acc > runs_cap) return fail(DMX_ERR_ARG, "runs buffer too small for the node range");
         // node-ordered copy (the pool is in completion order)
-        std::vector<int64_t> start((size_t)n), dst((size_t)n);
-        std::vector<int32_t> nr((size_t)n);
-        HIPCHK(hipMemcpy(start.data(), g->node_run_start.p, n * 8, hipMemcpyDeviceToHost));
-        int64_t acc = 0;
-        for (int64_t k = 0; k < n; k++) {
-            int s = 0;
-            for (int b = 0; b < 32; b++) s += bn[k * 32 + b];
-            nr[k] = s;
-            dst[k] = acc;
-            acc += s;
-        }
         DevBuf<int64_t> d_dst;
         DevBuf<Run> d_runs;
         HIPCHK(d_dst.alloc(n));
         HIPCHK(d_runs.alloc(std::max<int64_t>(acc, 1)));
-        HIPCHK(hipMemcpy(d_dst.p, dst.data(), n * 8, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(gather_runs_kernel, dim3((unsigned)n), dim3(256), 0, g->ctx->stream, g->pool.p,
-                           g->node_run_start.p, g->node_nruns.p, d_dst.p, n, d_runs.p);
+        HIPCHK(copy_sync(st, d_dst.p, dst.data(), n * 8, hipMemcpyHostToDevice));
+        hipLaunchKernelGGL(gather_runs_kernel, dim3((unsigned)n), dim3(256), 0, st, g->pool.p,
+                           g->node_run_start.p + kb, g->node_nruns.p + kb, d_dst.p, n, d_runs.p);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipStreamSynchronize(g->ctx->stream));
-        if (acc) HIPCHK(hipMemcpy(runs, d_runs.p, acc * sizeof(Run), hipMemcpyDeviceToHost));
+        if (acc) HIPCHK(copy_sync(st, runs, d_runs.p, acc * sizeof(Run), hipMemcpyDeviceToHost));
     }
     return DMX_OK;
+}
+
+int dmx_graph_copy(dmx_graph* g, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn) {
+    return dmx_graph_copy_range(g, 0, -1, attrs, bins, runs, -1, nullptr, gridconn);
 }
 
 // ---------------------------------------------------------------- shard blobs
@@ -738,7 +753,7 @@ int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const*
     std::vector<std::array<int64_t, 4>> hdr((size_t)nshards);
     int64_t total_runs = 0;
     for (int i = 0; i < nshards; i++) {
-        HIPCHK(hipMemcpy(hdr[i].data(), blobs[i], 32, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, hdr[i].data(), blobs[i], 32, hipMemcpyDeviceToHost));
         if (hdr[i][3] != kBlobMagic) return fail(DMX_ERR_ARG, "not a dmx graph blob");
         total_runs += hdr[i][2];
     }
@@ -925,7 +940,7 @@ static int prepare_symmetry(dmx_graph* g) {
     if (nspec == 0) { g->symmetric = 1; return DMX_OK; }
     if (nspec > kSpecLimit) { g->symmetric = 0; return DMX_OK; }
     std::vector<int32_t> specs((size_t)nspec);
-    HIPCHK(hipMemcpy(specs.data(), flist.p, nspec * 4, hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(g->ctx->stream, specs.data(), flist.p, nspec * 4, hipMemcpyDeviceToHost));
     std::sort(specs.begin(), specs.end());
     g->special_nodes = specs;
     std::vector<uint8_t> is_spec((size_t)N, 0);
@@ -938,8 +953,8 @@ static int prepare_symmetry(dmx_graph* g) {
     HIPCHK(d_specs.alloc(nspec));
     HIPCHK(d_out.alloc((size_t)nspec * nspec));
     HIPCHK(d_outn.alloc(nspec));
-    HIPCHK(hipMemcpy(d_is.p, is_spec.data(), N, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(d_specs.p, specs.data(), nspec * 4, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(g->ctx->stream, d_is.p, is_spec.data(), N, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(g->ctx->stream, d_specs.p, specs.data(), nspec * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemset(d_outn.p, 0, nspec * 4));
     hipLaunchKernelGGL(sym_special_out_kernel, dim3(nspec), dim3(256), 0, s, rows, d_specs.p, nspec,
                        g->pm->d_node_cell.p, g->pm->d_cell_node.p, d_is.p, g->node_run_start.p, g->node_nruns.p,
@@ -972,11 +987,11 @@ static int prepare_symmetry(dmx_graph* g) {
     HIPCHK(g->missing_off.alloc(moff.size()));
     HIPCHK(g->extra.alloc(std::max<size_t>(ev.size(), 1)));
     HIPCHK(g->missing.alloc(std::max<size_t>(mv.size(), 1)));
-    HIPCHK(hipMemcpy(g->spec_index.p, sidx.data(), N * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(g->extra_off.p, eoff.data(), eoff.size() * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(g->missing_off.p, moff.data(), moff.size() * 4, hipMemcpyHostToDevice));
-    if (!ev.empty()) HIPCHK(hipMemcpy(g->extra.p, ev.data(), ev.size() * 4, hipMemcpyHostToDevice));
-    if (!mv.empty()) HIPCHK(hipMemcpy(g->missing.p, mv.data(), mv.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(g->ctx->stream, g->spec_index.p, sidx.data(), N * 4, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(g->ctx->stream, g->extra_off.p, eoff.data(), eoff.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(copy_sync(g->ctx->stream, g->missing_off.p, moff.data(), moff.size() * 4, hipMemcpyHostToDevice));
+    if (!ev.empty()) HIPCHK(copy_sync(g->ctx->stream, g->extra.p, ev.data(), ev.size() * 4, hipMemcpyHostToDevice));
+    if (!mv.empty()) HIPCHK(copy_sync(g->ctx->stream, g->missing.p, mv.data(), mv.size() * 4, hipMemcpyHostToDevice));
     g->symmetric = 1;
     return DMX_OK;
 }
@@ -1042,7 +1057,7 @@ static int prepare_tiles(dmx_graph* g) {
         HIPCHK(hipMemcpyAsync(veto.p, &v, 8, hipMemcpyHostToDevice, s));
         if (int rc = prep_allreduce(g, veto.p, 1, DMX_I64)) return rc;
         int64_t vs = 0;
-        HIPCHK(hipMemcpy(&vs, veto.p, 8, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(g->ctx->stream, &vs, veto.p, 8, hipMemcpyDeviceToHost));
         tv_build = vs == 0;
     }
     if (tv_build) {
@@ -1208,10 +1223,10 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->last_vga_s = ms * 1e-3;
     int hc[2];
-    HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level capacity");
     unsigned long long st[32];
-    HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
     for (int i = 0; i < 5; i++) ctx->phase_cycles[i] = (long long)st[8 + i];
     ctx->last_stats[18] = (long long)st[16];                          // phase-C hits by a fully seen tile
     ctx->last_stats[19] = (long long)st[17];                          // clocks of top-down levels > 1
@@ -1241,9 +1256,9 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[17] = (long long)st[14];                          // phase-C cells (regular)
     if (nseeds > 0) return DMX_OK;
     if (!out_on_device && nsrc > 0)
-        HIPCHK(hipMemcpy(out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
     if (levels && nsrc > 0)
-        HIPCHK(hipMemcpy(levels + sb * 3, d_lv.p + sb * 3, nsrc * 3 * 8, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, levels + sb * 3, d_lv.p + sb * 3, nsrc * 3 * 8, hipMemcpyDeviceToHost));
     return DMX_OK;
 }
 
@@ -1343,10 +1358,10 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->last_vga_s = ms * 1e-3;
     int hc[2];
-    HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level/frontier capacity");
     unsigned long long st[8];
-    HIPCHK(hipMemcpy(st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
     ctx->last_stats[8] = (long long)st[5];   // bottom-up cells that scanned all their runs without a hit
     ctx->last_stats[9] = (long long)st[6];   // runs read by those
     ctx->last_stats[10] = gbm ? 1 : 0;
@@ -1357,9 +1372,9 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     ctx->last_stats[6] = (long long)st[2];
     ctx->last_stats[7] = nsrc;
     if (!out_on_device && nsrc > 0)
-        HIPCHK(hipMemcpy(out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
     if (levels && nsrc > 0)
-        HIPCHK(hipMemcpy(levels + sb * 3, d_lv.p + sb * 3, nsrc * 3 * 8, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, levels + sb * 3, d_lv.p + sb * 3, nsrc * 3 * 8, hipMemcpyDeviceToHost));
     return DMX_OK;
 }
 
@@ -1470,16 +1485,16 @@ static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
         HIPCHK(hipEventRecord(ctx->ev1, s));
         HIPCHK(hipStreamSynchronize(s));
         int hc[2];
-        HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
         if (hc[1] & KERR_FRONTIER) { cap *= 4; continue; }
         if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA metric/angular search failed");
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
         ctx->last_vga_s = ms * 1e-3;
         if (se > sb)
-            HIPCHK(hipMemcpy(out + sb * NO, d_out.p + sb * NO, (size_t)(se - sb) * NO * 4, hipMemcpyDeviceToHost));
+            HIPCHK(copy_sync(ctx->stream, out + sb * NO, d_out.p + sb * NO, (size_t)(se - sb) * NO * 4, hipMemcpyDeviceToHost));
         unsigned long long stv[3];
-        HIPCHK(hipMemcpy(stv, ctx->stats.p, sizeof(stv), hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, stv, ctx->stats.p, sizeof(stv), hipMemcpyDeviceToHost));
         ctx->last_sd_stats[0] = (long long)stv[0];
         ctx->last_sd_stats[1] = (long long)stv[1];
         ctx->last_stats[7] = se - sb;
@@ -1536,9 +1551,9 @@ int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t sb, int64_
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->last_vga_s = ms * 1e-3;
     if (se > sb)
-        HIPCHK(hipMemcpy(out + sb * 3, d_out.p + sb * 3, (size_t)(se - sb) * 3 * 4, hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, out + sb * 3, d_out.p + sb * 3, (size_t)(se - sb) * 3 * 4, hipMemcpyDeviceToHost));
     unsigned long long st0 = 0;
-    HIPCHK(hipMemcpy(&st0, ctx->stats.p, 8, hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(ctx->stream, &st0, ctx->stats.p, 8, hipMemcpyDeviceToHost));
     ctx->last_stats[4] = (long long)st0;   // neighbour runs walked
     ctx->last_stats[7] = se - sb;
     return DMX_OK;
@@ -1575,7 +1590,7 @@ static int stepdepth_batched(dmx_ctx* ctx, dmx_graph* g, const std::vector<uint8
     // work units: ceil(runs / SDB_UNIT) per expander
     std::vector<int32_t> nr((size_t)g->nnodes);
     HIPCHK(hipStreamSynchronize(s));
-    if (g->nnodes) HIPCHK(hipMemcpy(nr.data(), g->node_nruns.p, g->nnodes * 4, hipMemcpyDeviceToHost));
+    if (g->nnodes) HIPCHK(copy_sync(ctx->stream, nr.data(), g->node_nruns.p, g->nnodes * 4, hipMemcpyDeviceToHost));
     int64_t units = 0;
     const auto& nc = g->pm->node_cell;   // ascending cell index = node order
     for (int32_t c : ex) {
@@ -1773,26 +1788,26 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
         HIPCHK(hipEventRecord(ctx->ev1, s));
         HIPCHK(hipStreamSynchronize(s));
         int hc[2];
-        HIPCHK(hipMemcpy(hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
         if (hc[1] & KERR_FRONTIER) { cap *= 4; continue; }
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
         ctx->last_sd_s = ms * 1e-3;
         unsigned long long st3[3];
-        HIPCHK(hipMemcpy(st3, ctx->stats.p, sizeof(st3), hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, st3, ctx->stats.p, sizeof(st3), hipMemcpyDeviceToHost));
         for (int i = 0; i < 3; i++) ctx->last_sd_stats[i] = (long long)st3[i];
         if (ANG) {
             // "Angular Step Depth" = m_cumangle of every cell the search resolved (vgaangulardepth.cpp:53-55)
             std::vector<unsigned long long> kh((size_t)C);
             std::vector<float> ch((size_t)C);
-            HIPCHK(hipMemcpy(kh.data(), d_key.p, C * 8, hipMemcpyDeviceToHost));
-            HIPCHK(hipMemcpy(ch.data(), d_cum.p, C * 4, hipMemcpyDeviceToHost));
+            HIPCHK(copy_sync(ctx->stream, kh.data(), d_key.p, C * 8, hipMemcpyDeviceToHost));
+            HIPCHK(copy_sync(ctx->stream, ch.data(), d_cum.p, C * 4, hipMemcpyDeviceToHost));
             for (int64_t k = 0; k < N; k++) {
                 const int c = g->pm->node_cell[k];
                 out[k] = kh[c] != SD_INF ? ch[c] : -1.0f;
             }
         } else if (N) {
-            HIPCHK(hipMemcpy(out, d_out.p, N * 3 * 4, hipMemcpyDeviceToHost));
+            HIPCHK(copy_sync(ctx->stream, out, d_out.p, N * 3 * 4, hipMemcpyDeviceToHost));
         }
         return DMX_OK;
     }
@@ -1862,7 +1877,7 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
     rc = vga_tile_impl(ctx, g, -1.0, 0, 0, 1, dummy.data(), false, nullptr, tw, th, d_seeds.p, (int)seeds.size(), d_level.p);
     if (rc) return rc;
     std::vector<int32_t> lv((size_t)nt * 64);
-    HIPCHK(hipMemcpy(lv.data(), d_level.p, lv.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(copy_sync(ctx->stream, lv.data(), d_level.p, lv.size() * 4, hipMemcpyDeviceToHost));
     for (int64_t k = 0; k < N; k++) {
         const int c = g->pm->node_cell[k];
         const int x = c / rows, y = c % rows;

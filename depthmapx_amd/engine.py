@@ -197,6 +197,24 @@ class Graph:
             out["runs"] = rr[:i["nruns"]]
         return out
 
+    def copy_range(self, node_begin, node_end, runs=True):
+        """bins/attrs/gridconn (and node-ordered runs) of the local nodes [node_begin, node_end) only:
+        block checks at 1000^2+ without moving the whole 36-90 GB run pool to the host."""
+        n = node_end - node_begin
+        attrs = np.zeros((n, 3), dtype=np.float32)
+        bins = np.zeros((n, 32, 4), dtype=np.int32)
+        gc = np.zeros(n, dtype=np.uint8)
+        nr = ctypes.c_int64()
+        N.check(N.lib().dmx_graph_copy_range(self.h, int(node_begin), int(node_end), N.ptr(attrs), N.ptr(bins), None,
+                                             -1, ctypes.byref(nr), N.ptr(gc)))
+        out = dict(attrs=attrs, bins=bins, gridconn=gc)
+        if runs:
+            rr = np.zeros((max(nr.value, 1), 4), dtype=np.int16)
+            N.check(N.lib().dmx_graph_copy_range(self.h, int(node_begin), int(node_end), None, None, N.ptr(rr),
+                                                 len(rr), None, None))
+            out["runs"] = rr[:nr.value]
+        return out
+
     def blob_size(self):
         b = ctypes.c_int64()
         N.check(N.lib().dmx_graph_blob_size(self.h, ctypes.byref(b)))

@@ -103,6 +103,11 @@ int dmx_graph_info(const dmx_graph* g, int64_t* nnodes, int64_t* node_begin, int
  *   gridconn[n]  Point::m_grid_connections (pointdata.cpp:1735-1768)
  * Any pointer may be NULL. */
 int dmx_graph_copy(dmx_graph* g, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn);
+/* The same for the local nodes [node_b, node_e) only (node_e < 0: to the end): bins/attrs/gridconn
+ * sized for the range, runs node-ordered (capacity runs_cap entries, < 0: unchecked); *nruns_out
+ * = the range's run count (runs may be NULL to query it). */
+int dmx_graph_copy_range(dmx_graph* g, int64_t node_b, int64_t node_e, float* attrs, int32_t* bins, int16_t* runs,
+                         int64_t runs_cap, int64_t* nruns_out, uint8_t* gridconn);
 
 /* Shard exchange for multi-GPU runs: a graph's built range serialises into one flat blob
  * (device memory) that another rank's dmx_graph_assemble can consume. */

@@ -13,7 +13,7 @@ from golden_io import case_input_lines, load_case, node_digests
 pytestmark = pytest.mark.gpu
 
 MK_CASES = ["kat", "syn16", "syn32", "gallery", "syn64", "barnsbury", "syn256mk"]
-VGA_CASES = ["kat", "syn16", "syn32", "gallery", "syn64", "barnsbury"]
+VGA_CASES = ["kat", "syn16", "syn32", "gallery", "syn64", "barnsbury", "syn128"]
 VGA_RTOL = 1e-6
 
 

@@ -1,0 +1,168 @@
+"""GPU parity at the benchmark sizes (BASELINE.json configs[2]/[3] 1000^2, configs[4] 2000^2/5000).
+
+The oracle (oracle/dmx_oracle.c, pinned to the reference) cannot build these graphs whole in test
+time, so the checks are seeded blocks and size-independent properties:
+  * makeGraph (PointMap::sparkGraph2, salalib/pointdata.cpp:1246-1341): blocks of 64 sources --
+    a corner, the middle, cells next to an occluder, a seeded random block -- bin records, runs,
+    the 3 float attributes and the grid connections bit-exact against OracleMap.make_graph on the
+    same node range;
+  * VGA global (VGAVisualGlobal::run, vgavisualglobal.cpp:23-216) at 1000^2: seeded source blocks
+    against the oracle's BFS over the same graph (node counts exact, floats within 1e-6);
+  * metric step depth at 2000^2/5000 (VGAMetricDepth::run, vgametricdepth.cpp:23-92): the
+    whole-GPU batched search against the serial pop-order kernel (itself pinned to the reference
+    fixtures at small sizes), bit-exact on every column, plus invariants of the result.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import depthmapx_amd as dmx
+from golden_io import GOLDEN, read_csv_lines
+
+pytestmark = pytest.mark.gpu
+
+BLOCK = 64
+FILLED, BLOCKED = 2, 4
+
+
+def _blocks(pm, N, seed):
+    """Node ranges: a corner, the middle, the node of an occluder-adjacent cell, a seeded random one."""
+    st = pm.state()
+    filled = np.nonzero(st & FILLED)[0]          # node k <-> cell filled[k] (x-major)
+    blocked = np.nonzero(st & BLOCKED)[0]
+    near = blocked[len(blocked) // 2]             # a cell on an occluder near the middle of the list
+    k_near = min(max(0, int(np.searchsorted(filled, near)) - BLOCK // 2), N - BLOCK)
+    rng = np.random.default_rng(seed)
+    starts = [0, N // 2 - BLOCK // 2, k_near, int(rng.integers(0, N - BLOCK))]
+    return [(b, b + BLOCK) for b in starts]
+
+
+def _check_makegraph_blocks(pm, g, om, blocks, threads=16):
+    for (b, e) in blocks:
+        got = g.copy_range(b, e)
+        om.make_graph(node_begin=b, node_end=e, threads=threads)
+        ref = om.graph()
+        rb = ref["bins"][b:e]
+        off = np.concatenate([[0], np.cumsum(ref["bins"][:, :, 3].sum(axis=1))])
+        rr = ref["runs"][off[b]:off[e]]
+        np.testing.assert_array_equal(got["bins"], rb, err_msg="bins of nodes [%d,%d)" % (b, e))
+        np.testing.assert_array_equal(got["runs"], rr, err_msg="runs of nodes [%d,%d)" % (b, e))
+        np.testing.assert_array_equal(got["attrs"].view(np.uint32), ref["attrs"][b:e].view(np.uint32))
+        np.testing.assert_array_equal(got["gridconn"], ref["gridconn"][b:e])
+        assert got["bins"][:, :, 3].sum() > 0
+
+
+def _release(ctx, *objs):
+    for o in objs:
+        o.close()
+    import ctypes  # noqa: F401
+    from depthmapx_amd import _native as N
+    N.lib().dmx_release_cached_memory()
+
+
+@pytest.fixture(scope="module")
+def big1000(ctx):
+    from pyoracle import OracleMap
+    lines = read_csv_lines(os.path.join(GOLDEN, "inputs", "syn1000.csv"))
+    region = [0.0, 0.0, 1000.0, 1000.0]
+    pm = dmx.PointMap(region, lines, 1.0)
+    assert pm.make_points(0.5, 0.5)
+    g = pm.make_graph(ctx)
+    om = OracleMap(region, 1.0, lines)
+    assert om.fill(0.5, 0.5)
+    yield pm, g, om
+    _release(ctx, g)
+
+
+def test_1000_makegraph_blocks_match_oracle(big1000):
+    """configs[2]: 1001^2 cells, 50 occluders.  Node count, run total and 4 blocks bit-exact."""
+    pm, g, om = big1000
+    info = g.info()
+    assert info["nnodes"] == pm.info()["filled"] == 998001
+    np.testing.assert_array_equal(pm.state(), om.state())
+    _check_makegraph_blocks(pm, g, om, _blocks(pm, info["nnodes"], seed=1000))
+
+
+def test_1000_vga_blocks_match_oracle(big1000):
+    """configs[2] VGA global: 2 seeded blocks of 16 sources, the oracle's BFS over the same graph
+    (the GPU graph copied to the host; its makeGraph blocks are pinned by the test above)."""
+    pm, g, om = big1000
+    N = g.info()["nnodes"]
+    rng = np.random.default_rng(7)
+    blocks = [(N // 2, N // 2 + 16), (int(rng.integers(0, N - 16)),) * 2]
+    blocks[1] = (blocks[1][0], blocks[1][0] + 16)
+    outs = [g.vga_visual_global(src_begin=b, src_end=e) for (b, e) in blocks]
+    full = g.copy(runs=True)
+    om.set_graph(full["bins"], full["runs"])
+    del full
+    for (b, e), out in zip(blocks, outs):
+        ref = om.vga_global(node_begin=b, node_end=e, threads=16)
+        got, want = out[b:e].astype(np.float64), ref[b:e].astype(np.float64)
+        np.testing.assert_array_equal(got[:, 5], want[:, 5])            # node count: exact
+        assert (np.abs(got - want) <= 1e-6 * np.maximum(1.0, np.abs(want))).all()
+        assert (want[:, 5] > 0.5 * N).all()
+
+
+def test_1000_vga_kernels_agree_at_size(big1000, ctx, monkeypatch):
+    """The tile-resolved BFS with its line summaries (default above ~1010^2 the coarser per-tile
+    summary) against the direction-optimising kernel, bit-for-bit, on a block of 256 sources."""
+    pm, g, om = big1000
+    N = g.info()["nnodes"]
+    b, e = N // 3, N // 3 + 256
+    a = g.vga_visual_global(src_begin=b, src_end=e)
+    assert ctx.last_stats()["vga_kernel"] == "tile-resolved"
+    monkeypatch.setenv("DMX_VGA_KERNEL", "do")
+    g2 = pm.make_graph(ctx)
+    c = g2.vga_visual_global(src_begin=b, src_end=e)
+    _release(ctx, g2)
+    np.testing.assert_array_equal(a[b:e].view(np.uint32), c[b:e].view(np.uint32))
+
+
+@pytest.fixture(scope="module")
+def big2000(ctx):
+    from pyoracle import OracleMap
+    lines = read_csv_lines(os.path.join(GOLDEN, "inputs", "syn2000_5000.csv"))
+    region = [0.0, 0.0, 1999.0, 1999.0]
+    pm = dmx.PointMap(region, lines, 1.0)
+    assert pm.make_points(0.5, 0.5)
+    g = pm.make_graph(ctx)
+    om = OracleMap(region, 1.0, lines)
+    assert om.fill(0.5, 0.5)
+    yield pm, g, om
+    _release(ctx, g)
+
+
+def test_2000_makegraph_blocks_match_oracle(big2000):
+    """configs[4]: 2000^2 cells, 5000 short occluders (dense): 4 blocks bit-exact."""
+    pm, g, om = big2000
+    info = g.info()
+    assert info["nnodes"] == pm.info()["filled"]
+    assert info["nnodes"] > 3_900_000
+    np.testing.assert_array_equal(pm.state(), om.state())
+    _check_makegraph_blocks(pm, g, om, _blocks(pm, info["nnodes"], seed=2000))
+
+
+def test_2000_metric_stepdepth_batched_equals_serial(big2000, ctx, monkeypatch):
+    """configs[4] step depth from the cell nearest the centre: batched == serial on every column, and
+    the result's invariants (every reached cell's length >= its straight-line distance; the selected
+    cell at 0; the expander count and relaxations identical)."""
+    import bench
+    pm, g, om = big2000
+    cell = bench.nearest_filled(pm, 1000.0, 1000.0)
+    monkeypatch.delenv("DMX_SD_KERNEL", raising=False)
+    a = g.metric_step_depth(cells=[cell])
+    sa = ctx.last_stepdepth()
+    assert sa["mode"] == "batched"
+    monkeypatch.setenv("DMX_SD_KERNEL", "serial")
+    b = g.metric_step_depth(cells=[cell])
+    sb = ctx.last_stepdepth()
+    assert sb["mode"] == "serial"
+    assert (sa["expanders_popped"], sa["cells_relaxed"]) == (sb["expanders_popped"], sb["cells_relaxed"])
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    reached = a[:, 1] >= 0
+    assert reached.mean() > 0.99
+    assert (a[reached, 1] >= a[reached, 2] * (1 - 1e-6)).all()
+    st = pm.state()
+    k_sel = int(np.searchsorted(np.nonzero(st & FILLED)[0], cell))
+    assert a[k_sel, 1] == 0.0 and a[k_sel, 2] == 0.0
