@@ -14,7 +14,7 @@ STATUS_NAMES = {-1: "DMX_ERR_ARG", -2: "DMX_ERR_HIP", -3: "DMX_ERR_CAPACITY", -4
                 -5: "DMX_ERR_UNSUPPORTED", -6: "DMX_ERR_OUTSIDE"}
 
 # every symbol include/dmx.h declares, with (restype, argtypes)
-_vp, _i64, _i32, _dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double
+_vp, _i64, _i32, _dbl, _cs = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_char_p
 SIGNATURES = {
     "dmx_abi_version": (_i32, []),
     "dmx_last_error": (ctypes.c_char_p, []),
@@ -59,6 +59,24 @@ SIGNATURES = {
     "dmx_chunk_arrays": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_chunk_load": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_graph_from_runs": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
+    "dmx_graph_set_merges": (_i32, [_vp, _vp, _i64]),
+    "dmx_chunk_flags": (_i32, [_vp, _vp, _vp, _vp, _vp]),
+    "dmx_chunk_set_column": (_i32, [_vp, _cs, _vp, _vp, _i32, _i32]),
+    "dmx_chunk_set_displayed": (_i32, [_vp, _i32]),
+    "dmx_chunk_set_name": (_i32, [_vp, _cs]),
+    "dmx_chunk_select_cells": (_i32, [_vp, _vp, _i64]),
+    "dmx_chunk_unmake": (_i32, [_vp, _i32]),
+    "dmx_chunk_serialize": (_i32, [_vp, _vp, _i64, _vp]),
+    "dmx_graphfile_read": (_i32, [_cs, _vp]),
+    "dmx_graphfile_free": (_i32, [_vp]),
+    "dmx_graphfile_write": (_i32, [_vp, _cs]),
+    "dmx_graphfile_info": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "dmx_graphfile_lines": (_i32, [_vp, _vp]),
+    "dmx_graphfile_set_view": (_i32, [_vp, _i32, _i32]),
+    "dmx_graphfile_pointmap": (_i32, [_vp, _i32, _vp, _vp]),
+    "dmx_graphfile_put_pointmap": (_i32, [_vp, _i32, _vp, _i64]),
+    "dmx_graphfile_new_pointmap_name": (_i32, [_vp, _vp, _i32]),
+    "dmx_view_vga_top": (_i32, [_i32]),
 }
 
 

@@ -10,7 +10,7 @@ OUT = os.path.join(HERE, "_lib", "libdmx.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("DMX_OFFLOAD_ARCH", "gfx950")
 
-SOURCES = ["dmx_api.hip", "host/pointmap.cpp", "host/graphio.cpp"]
+SOURCES = ["dmx_api.hip", "host/pointmap.cpp", "host/graphio.cpp", "host/graphfile.cpp"]
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-Wno-unused-variable", "-Wno-unused-function"]
 

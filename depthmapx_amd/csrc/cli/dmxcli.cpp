@@ -8,10 +8,10 @@
 //   :735-778 (runStepDepth), performancewriter.cpp:60-76, salalib/gridproperties.cpp:4-13.
 // Host code over the C ABI (include/dmx.h); every analysis runs on the GPU.
 //
-// Files: the input of VISPREP is a drawing -- a CSV of lines (header x1,y1,x2,y2; what
-// "depthmapXcli -m IMPORT -it drawing" ingests) or a container written by this tool.  Output
-// containers (".dmxg") hold the region, the drawing lines and the PointMap chunk of the .graph
-// format, byte-identical to what PointMap::write emits ("The .graph boundary").
+// Files: a depthmapX .graph (MetaGraph::readFromFile / write, mgraph.cpp:2475-2757, through
+// dmx_graphfile_*), written back as .graph; or a drawing as a CSV of lines (header x1,y1,x2,y2; what
+// "depthmapXcli -m IMPORT -it drawing" ingests) whose output container (".dmxg") holds the region, the
+// lines and one PointMap chunk of the .graph format.
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
@@ -118,29 +118,72 @@ std::vector<std::pair<double, double>> points_from_args(const std::vector<std::s
     return parse_points(ss, ',');
 }
 
-// ---------------------------------------------------------------- the document (".dmxg" container)
-struct Column {
-    std::string name;
-    std::vector<float> values;
-    bool locked = false;
-    std::vector<uint8_t> set;
-};
+// ---------------------------------------------------------------- the document
+// A depthmapX .graph file (MetaGraph container, read and written through dmx_graphfile_*), or this
+// tool's ".dmxg" container for a drawing imported from CSV (region, lines and one PointMap chunk of the
+// .graph format).  Output goes out in the input's container.
+const char kMagic[4] = {'D', 'M', 'X', 'G'};
+// MetaGraph m_state bits (mgraph.h:71-73)
+enum { MG_POINTMAPS = 0x0002, MG_LINEDATA = 0x0004, MG_ANGULARGRAPH = 0x0010 };
 
 struct Document {
     double region[4] = {0, 0, 0, 0};
-    std::vector<double> lines;        // [L][4]
-    bool has_map = false;
-    std::vector<uint8_t> chunk;       // PointMap::write bytes
+    std::vector<double> lines;        // [L][4] as PointMap::blockLines reads them
+    dmx_graphfile* gf = nullptr;      // .graph input
+    bool has_map = false;             // .dmxg: one point map
+    std::vector<uint8_t> chunk;
+    int32_t state = 0, view = 0;
+    Document() {}
+    Document(const Document&) = delete;
+    Document& operator=(const Document&) = delete;
+    ~Document() { if (gf) dmx_graphfile_free(gf); }
+    bool line_data() const { return gf ? (state & MG_LINEDATA) != 0 : !lines.empty(); }
+    bool any_map() const {
+        if (!gf) return has_map;
+        int32_t n = 0;
+        check(dmx_graphfile_info(gf, nullptr, nullptr, nullptr, nullptr, &n, nullptr));
+        return n > 0;
+    }
+    // the displayed point map (MetaGraph::getDisplayedPointMap)
+    std::vector<uint8_t> displayed_chunk() const {
+        if (!gf) return chunk;
+        int32_t disp = -1;
+        check(dmx_graphfile_info(gf, nullptr, nullptr, nullptr, nullptr, nullptr, &disp));
+        const uint8_t* p = nullptr;
+        int64_t n = 0;
+        check(dmx_graphfile_pointmap(gf, disp, &p, &n));
+        return std::vector<uint8_t>(p, p + n);
+    }
+    void put_displayed(const std::vector<uint8_t>& c, bool new_map) {
+        if (!gf) { chunk = c; has_map = true; return; }
+        int32_t disp = -1;
+        check(dmx_graphfile_info(gf, nullptr, nullptr, nullptr, nullptr, nullptr, &disp));
+        check(dmx_graphfile_put_pointmap(gf, new_map ? -1 : disp, c.data(), (int64_t)c.size()));
+    }
+    std::string new_map_name() const {
+        if (!gf) return "VGA Map";
+        char name[256];
+        check(dmx_graphfile_new_pointmap_name(gf, name, sizeof(name)));
+        return name;
+    }
 };
 
-const char kMagic[4] = {'D', 'M', 'X', 'G'};
-
-Document read_document(const std::string& path) {
+void read_document(const std::string& path, Document& d) {
     std::ifstream f(path, std::ios::binary);
     if (!f) throw RuntimeException("Failed to load graph from file " + path + ", error -1");
-    Document d;
     char magic[4] = {0, 0, 0, 0};
     f.read(magic, 4);
+    if (magic[0] == 'g' && magic[1] == 'r' && magic[2] == 'f') {
+        f.close();
+        const int rc = dmx_graphfile_read(path.c_str(), &d.gf);
+        if (rc) throw RuntimeException("Failed to load graph from file " + path + ", error " + std::to_string(rc) + " (" +
+                                       dmx_last_error() + ")");
+        int64_t nl = 0;
+        check(dmx_graphfile_info(d.gf, &d.state, &d.view, d.region, &nl, nullptr, nullptr));
+        d.lines.resize((size_t)nl * 4);
+        check(dmx_graphfile_lines(d.gf, d.lines.data()));
+        return;
+    }
     if (std::memcmp(magic, kMagic, 4) != 0) {
         // a drawing: CSV of lines x1,y1,x2,y2 (the reference's IMPORT -it drawing input)
         f.close();
@@ -161,7 +204,7 @@ Document read_document(const std::string& path) {
         }
         if (d.lines.empty()) throw RuntimeException("Failed to load graph from file " + path + ", error -1");
         d.region[0] = mn[0]; d.region[1] = mn[1]; d.region[2] = mx[0]; d.region[3] = mx[1];
-        return d;
+        return;
     }
     uint32_t version = 0;
     f.read((char*)&version, 4);
@@ -180,10 +223,14 @@ Document read_document(const std::string& path) {
         f.read((char*)d.chunk.data(), (std::streamsize)n);
     }
     if (!f) throw RuntimeException("Failed to load graph from file " + path + ", error -1");
-    return d;
 }
 
-void write_document(const std::string& path, const Document& d) {
+void write_document(const std::string& path, Document& d) {
+    if (d.gf) {
+        check(dmx_graphfile_set_view(d.gf, d.state, d.view));
+        check(dmx_graphfile_write(d.gf, path.c_str()));
+        return;
+    }
     std::ofstream f(path, std::ios::binary | std::ios::trunc);
     if (!f) throw RuntimeException("Failed to write " + path);
     f.write(kMagic, 4);
@@ -208,63 +255,67 @@ struct Context {
     ~Context() { dmx_ctx_free(ctx); }
 };
 
+// A parsed point map chunk (library-owned) with its graph uploaded to the GPU: what the reference's
+// VGA / STEPDEPTH steps analyse after loadGraph (runmethods.cpp:33-45).
 struct LoadedMap {
     dmx_chunk* chunk = nullptr;
     dmx_pointmap* pm = nullptr;
     dmx_graph* g = nullptr;
-    int64_t nnodes = 0, nruns = 0;
-    std::vector<Column> columns;
-    std::vector<int32_t> bins;
-    std::vector<int16_t> runs;
-    std::vector<uint8_t> gridconn;
+    int64_t nnodes = 0;
     ~LoadedMap() {
         if (g) dmx_graph_free(g);
         if (pm) dmx_pointmap_free(pm);
         if (chunk) dmx_chunk_free(chunk);
     }
+    // add / reset a column of the analysis (values and set mask in node = attribute row order)
+    void column(const std::string& name, const float* values, const uint8_t* set, bool locked, bool displayed) {
+        check(dmx_chunk_set_column(chunk, name.c_str(), values, set, locked ? 1 : 0, displayed ? 1 : 0));
+    }
+    std::vector<uint8_t> bytes() const {
+        int64_t size = 0;
+        check(dmx_chunk_serialize(chunk, nullptr, 0, &size));
+        std::vector<uint8_t> out((size_t)size);
+        check(dmx_chunk_serialize(chunk, out.data(), size, &size));
+        return out;
+    }
 };
 
-// loadGraph for an analysis step: the PointMap chunk decoded (4-bit shift quirk included) and its
-// graph uploaded to the GPU.
 void load_map(Context& C, const Document& d, LoadedMap& m) {
-    if (!d.has_map) throw RuntimeException("No map exists to use. Please create a new one by providing a grid size");
-    check(dmx_chunk_parse(d.chunk.data(), (int64_t)d.chunk.size(), &m.chunk));
-    int32_t ncols = 0, disp = 0;
-    check(dmx_chunk_info(m.chunk, nullptr, nullptr, nullptr, nullptr, &m.nnodes, &m.nruns, &ncols, &disp, nullptr));
-    m.columns.resize(ncols);
-    for (int i = 0; i < ncols; i++) {
-        char name[512];
-        int locked = 0;
-        m.columns[i].values.resize(m.nnodes);
-        check(dmx_chunk_column(m.chunk, i, name, sizeof(name), m.columns[i].values.data(), &locked));
-        m.columns[i].name = name;
-        m.columns[i].locked = locked != 0;
-    }
-    m.bins.resize((size_t)m.nnodes * 128);
-    m.runs.resize((size_t)std::max<int64_t>(m.nruns, 1) * 4);
-    m.gridconn.resize((size_t)m.nnodes);
-    check(dmx_chunk_arrays(m.chunk, nullptr, m.bins.data(), m.runs.data(), m.gridconn.data()));
+    if (!d.any_map()) throw RuntimeException("No map exists to use. Please create a new one by providing a grid size");
+    const std::vector<uint8_t> bytes = d.displayed_chunk();
+    check(dmx_chunk_parse(bytes.data(), (int64_t)bytes.size(), &m.chunk));
+    check(dmx_chunk_info(m.chunk, nullptr, nullptr, nullptr, nullptr, &m.nnodes, nullptr, nullptr, nullptr, nullptr));
+    int64_t nrows = 0;
+    check(dmx_chunk_flags(m.chunk, nullptr, nullptr, nullptr, &nrows));
+    if (nrows != m.nnodes) throw RuntimeException("attribute rows do not match the graph's nodes");
     check(dmx_chunk_load(C.ctx, m.chunk, d.region, &m.pm, &m.g));
 }
 
+// PointMap::write of a freshly built map (dmx_chunk_write), named like the map it replaces / adds
 std::vector<uint8_t> write_chunk(dmx_pointmap* pm, int64_t n, const int32_t* bins, const int16_t* runs, int64_t nruns,
-                                 const uint8_t* gc, const std::vector<Column>& cols, int displayed) {
-    std::vector<const char*> names;
+                                 const uint8_t* gc, const std::vector<std::string>& names,
+                                 const std::vector<std::vector<float>>& cols, const std::vector<uint8_t>& locked,
+                                 int displayed, bool boundary, const std::string& map_name) {
+    std::vector<const char*> nm;
     std::vector<float> vals;
-    std::vector<uint8_t> locked, masks;
-    for (auto& c : cols) {
-        names.push_back(c.name.c_str());
-        vals.insert(vals.end(), c.values.begin(), c.values.end());
-        locked.push_back(c.locked ? 1 : 0);
-        if (c.set.empty()) masks.insert(masks.end(), (size_t)n, (uint8_t)1);
-        else masks.insert(masks.end(), c.set.begin(), c.set.end());
+    for (size_t i = 0; i < names.size(); i++) {
+        nm.push_back(names[i].c_str());
+        vals.insert(vals.end(), cols[i].begin(), cols[i].end());
     }
     int64_t size = 0;
-    check(dmx_chunk_write(pm, n, bins, runs, nruns, gc, (int)cols.size(), names.data(), vals.data(), locked.data(),
-                          masks.data(), displayed, 0, nullptr, 0, &size));
+    check(dmx_chunk_write(pm, n, bins, runs, nruns, gc, (int)names.size(), nm.data(), vals.data(), locked.data(), nullptr,
+                          displayed, boundary ? 1 : 0, nullptr, 0, &size));
     std::vector<uint8_t> out((size_t)size);
-    check(dmx_chunk_write(pm, n, bins, runs, nruns, gc, (int)cols.size(), names.data(), vals.data(), locked.data(),
-                          masks.data(), displayed, 0, out.data(), size, &size));
+    check(dmx_chunk_write(pm, n, bins, runs, nruns, gc, (int)names.size(), nm.data(), vals.data(), locked.data(), nullptr,
+                          displayed, boundary ? 1 : 0, out.data(), size, &size));
+    if (map_name == "VGA Map") return out;
+    dmx_chunk* c = nullptr;
+    check(dmx_chunk_parse(out.data(), size, &c));
+    std::unique_ptr<dmx_chunk, int (*)(dmx_chunk*)> guard(c, dmx_chunk_free);
+    check(dmx_chunk_set_name(c, map_name.c_str()));
+    check(dmx_chunk_serialize(c, nullptr, 0, &size));
+    out.resize((size_t)size);
+    check(dmx_chunk_serialize(c, out.data(), size, &size));
     return out;
 }
 
@@ -339,13 +390,14 @@ struct VisPrep : Mode {
     }
     void run(const Args& a, Perf& perf) override {
         Document d;
-        timed(perf, "Load graph file", [&] { d = read_document(a.file); });
+        timed(perf, "Load graph file", [&] { read_document(a.file, d); });
         std::cout << "Initial checks... " << std::flush;
-        if (d.lines.empty()) throw RuntimeException("Graph must have line data before preparing VGA");
-        Context C;
+        if (!d.line_data()) throw RuntimeException("Graph must have line data before preparing VGA");
         dmx_pointmap* pm = nullptr;
         std::unique_ptr<dmx_pointmap, int (*)(dmx_pointmap*)> pmguard(nullptr, dmx_pointmap_free);
-        double spacing = grid;
+        std::unique_ptr<dmx_chunk, int (*)(dmx_chunk*)> existing(nullptr, dmx_chunk_free);
+        std::string map_name = "VGA Map";
+        bool new_map = false;
         if (grid > 0) {
             // GridProperties (salalib/gridproperties.cpp:4-13)
             const double maxdim = std::max(d.region[2] - d.region[0], d.region[3] - d.region[1]);
@@ -360,24 +412,61 @@ struct VisPrep : Mode {
                 throw RuntimeException(m.str());
             }
             std::cout << "ok\nSetting up grid... " << std::flush;
+            // MetaGraph::addNewPointMap + setGrid (mgraph.cpp:2791-2809, :222-234)
+            map_name = d.new_map_name();
+            new_map = true;
             timed(perf, "Setting grid", [&] {
                 check(dmx_pointmap_create(d.region, grid, d.lines.data(), (int64_t)d.lines.size() / 4, &pm));
             });
             pmguard.reset(pm);
+            d.state |= MG_POINTMAPS;
+            d.view = dmx_view_vga_top(d.view);
         } else {
-            if (!d.has_map) throw RuntimeException("No map exists to use. Please create a new one by providing a grid size");
+            if (!d.any_map()) throw RuntimeException("No map exists to use. Please create a new one by providing a grid size");
+            const std::vector<uint8_t> bytes = d.displayed_chunk();
             dmx_chunk* ch = nullptr;
-            check(dmx_chunk_parse(d.chunk.data(), (int64_t)d.chunk.size(), &ch));
+            check(dmx_chunk_parse(bytes.data(), (int64_t)bytes.size(), &ch));
+            existing.reset(ch);
             int32_t cols = 0, rows = 0;
+            double spacing = 0;
             check(dmx_chunk_info(ch, &cols, &rows, &spacing, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr));
             std::vector<int32_t> st((size_t)cols * rows);
             check(dmx_chunk_arrays(ch, st.data(), nullptr, nullptr, nullptr));
-            dmx_chunk_free(ch);
             check(dmx_pointmap_create(d.region, spacing, d.lines.data(), (int64_t)d.lines.size() / 4, &pm));
             pmguard.reset(pm);
             check(dmx_pointmap_set_state(pm, st.data()));
+            char nm[512];
+            (void)nm;
+            int processed = 0;
+            int64_t merges = 0;
+            check(dmx_chunk_flags(ch, &processed, nullptr, &merges, nullptr));
+            if (unmake) {
+                if (!processed)
+                    throw RuntimeException("Current map has not had its graph made so there's nothing to unmake");
+            } else if (merges || (processed && (!fills.empty() || make))) {
+                throw RuntimeException("Filling or making a point map that already has a graph or merge links is not "
+                                       "part of the accelerated path");
+            }
+            // the map keeps its name: read it back from the chunk header (dXstring: u32 length + bytes)
+            uint32_t len = 0;
+            std::memcpy(&len, bytes.data(), 4);
+            map_name.assign((const char*)bytes.data() + 4, len);
         }
-        if (unmake) throw RuntimeException("Unmaking a graph is not part of the accelerated path");
+        if (unmake) {
+            // PointMap::unmake (runmethods.cpp:319-325 -> pointdata.cpp:1343-1374)
+            timed(perf, "Unmaking graph", [&] { check(dmx_chunk_unmake(existing.get(), removeLinks ? 1 : 0)); });
+            std::cout << " ok\nWriting out result..." << std::flush;
+            timed(perf, "Writing graph", [&] {
+                int64_t size = 0;
+                check(dmx_chunk_serialize(existing.get(), nullptr, 0, &size));
+                std::vector<uint8_t> out((size_t)size);
+                check(dmx_chunk_serialize(existing.get(), out.data(), size, &size));
+                d.put_displayed(out, false);
+                write_document(a.out, d);
+            });
+            std::cout << " ok" << std::endl;
+            return;
+        }
         if (!fills.empty()) {
             std::cout << "ok\nFilling grid... " << std::flush;
             timed(perf, "Filling grid", [&] {
@@ -388,46 +477,38 @@ struct VisPrep : Mode {
                 }
             });
         }
-        std::vector<Column> cols;
         dmx_graph* g = nullptr;
-        int64_t n = 0, nr = 0;
+        std::unique_ptr<Context> C;   // the GPU is only needed to make the graph
         if (make) {
             std::cout << "ok\nMaking graph... " << std::flush;
-            timed(perf, "Making graph", [&] { check(dmx_makegraph(C.ctx, pm, maxvis, boundary ? 1 : 0, 0, -1, &g)); });
+            d.state |= MG_ANGULARGRAPH;   // MetaGraph::makeGraph (mgraph.cpp:264-284)
+            C.reset(new Context());
+            timed(perf, "Making graph", [&] { check(dmx_makegraph(C->ctx, pm, maxvis, boundary ? 1 : 0, 0, -1, &g)); });
+            d.view = dmx_view_vga_top(d.view);
         }
         std::cout << " ok\nWriting out result..." << std::flush;
         timed(perf, "Writing graph", [&] {
-            std::vector<int32_t> bins;
-            std::vector<int16_t> runs;
-            std::vector<uint8_t> gc;
+            std::vector<uint8_t> out;
             if (g) {
-                int64_t b, e;
+                int64_t n = 0, b, e, nr = 0;
                 check(dmx_graph_info(g, &n, &b, &e, &nr));
                 std::vector<float> attrs((size_t)n * 3);
-                bins.resize((size_t)n * 128);
-                runs.resize((size_t)std::max<int64_t>(nr, 1) * 4);
-                gc.resize((size_t)n);
+                std::vector<int32_t> bins((size_t)n * 128);
+                std::vector<int16_t> runs((size_t)std::max<int64_t>(nr, 1) * 4);
+                std::vector<uint8_t> gc((size_t)n);
                 check(dmx_graph_copy(g, attrs.data(), bins.data(), runs.data(), gc.data()));
-                const char* mk[3] = {"Connectivity", "Point First Moment", "Point Second Moment"};
-                for (int j = 0; j < 3; j++) {
-                    Column c;
-                    c.name = mk[j];
-                    c.locked = j == 0;
-                    c.values.resize((size_t)n);
-                    for (int64_t k = 0; k < n; k++) c.values[k] = attrs[k * 3 + j];
-                    cols.push_back(c);
-                }
                 dmx_graph_free(g);
+                // sparkGraph2 columns (pointdata.cpp:1268-1270), displayed = Connectivity
+                const std::vector<std::string> names = {"Connectivity", "Point First Moment", "Point Second Moment"};
+                std::vector<std::vector<float>> cols(3, std::vector<float>((size_t)n));
+                for (int j = 0; j < 3; j++)
+                    for (int64_t k = 0; k < n; k++) cols[j][k] = attrs[k * 3 + j];
+                out = write_chunk(pm, n, bins.data(), runs.data(), nr, gc.data(), names, cols, {1, 0, 0}, 0, boundary,
+                                  map_name);
             } else {
-                int64_t filled = 0;
-                check(dmx_pointmap_info(pm, nullptr, nullptr, nullptr, nullptr, &filled));
-                n = filled;
-                bins.assign((size_t)n * 128, 0);
-                gc.assign((size_t)n, 0);
-                runs.assign(4, 0);
+                out = write_chunk(pm, 0, nullptr, nullptr, 0, nullptr, {}, {}, {}, -2, false, map_name);
             }
-            d.chunk = write_chunk(pm, n, bins.data(), runs.data(), nr, gc.data(), cols, cols.empty() ? -1 : 0);
-            d.has_map = true;
+            d.put_displayed(out, new_map);
             write_document(a.out, d);
         });
         std::cout << " ok" << std::endl;
@@ -513,26 +594,20 @@ struct Vga : Mode {
                                      "Metric Mean Straight-Line Distance", "Metric Node Count"};
             // VGAAngular inserts Mean Depth, Total Depth, Node Count (vgaangular.cpp:43-48)
             const char* anames[3] = {"Angular Mean Depth", "Angular Total Depth", "Angular Node Count"};
-            int displayed = -1;
+            std::vector<float> v((size_t)m.nnodes);
             for (int j = 0; j < nc; j++) {
-                Column c;
-                c.name = std::string(ang ? anames[j] : mnames[j]) + suffix;
-                c.values.resize((size_t)m.nnodes);
-                c.set.assign((size_t)m.nnodes, 1);
-                for (int64_t i = 0; i < m.nnodes; i++) c.values[i] = out[i * nc + j];
+                for (int64_t i = 0; i < m.nnodes; i++) v[i] = out[i * nc + j];
                 // setDisplayedAttribute(mspl_col) / (mean_depth_col)
-                if (j == (ang ? 0 : 1)) displayed = (int)m.columns.size();
-                m.columns.push_back(c);
+                m.column(std::string(ang ? anames[j] : mnames[j]) + suffix, v.data(), nullptr, false, j == (ang ? 0 : 1));
             }
-            d.chunk = write_chunk(m.pm, m.nnodes, m.bins.data(), m.runs.data(), m.nruns, m.gridconn.data(), m.columns,
-                                  displayed);
+            d.put_displayed(m.bytes(), false);
             write_document(a.out, d);
         });
         std::cout << " ok" << std::endl;
     }
     void run(const Args& a, Perf& perf) override {
         Document d;
-        timed(perf, "Load graph file", [&] { d = read_document(a.file); });
+        timed(perf, "Load graph file", [&] { read_document(a.file, d); });
         Context C;
         LoadedMap m;
         load_map(C, d, m);
@@ -572,7 +647,8 @@ struct Vga : Mode {
                                    {"Visual Integration [P-value]", 2, false}, {"Visual Integration [Tekl]", 3, false},
                                    {"Visual Mean Depth", 4, false}, {"Visual Node Count", 5, false},
                                    {"Visual Relativised Entropy", 6, false}};
-            int displayed = -1;
+            std::vector<float> v((size_t)m.nnodes);
+            std::vector<uint8_t> set((size_t)m.nnodes);
             if (local && !a.simple) {
                 // VGAVisualLocal: three columns (vgavisuallocal.cpp:31-35), set for every source it does
                 // not skip (context-filled odd cells), displayed = clustering coefficient (:109-112)
@@ -589,39 +665,24 @@ struct Vga : Mode {
                 }
                 const char* lnames[3] = {"Visual Clustering Coefficient", "Visual Control", "Visual Controllability"};
                 for (int j = 0; j < 3; j++) {
-                    Column c;
-                    c.name = lnames[j];
-                    c.values.resize((size_t)m.nnodes);
-                    c.set.resize((size_t)m.nnodes);
-                    for (int64_t i = 0; i < m.nnodes; i++) {
-                        c.values[i] = ran[i] ? lout[i * 3 + j] : -1.0f;
-                        c.set[i] = ran[i];
-                    }
-                    if (j == 0) displayed = (int)m.columns.size();
-                    m.columns.push_back(c);
+                    for (int64_t i = 0; i < m.nnodes; i++) v[i] = lout[i * 3 + j];
+                    m.column(lnames[j], v.data(), ran.data(), false, j == 0);
                 }
             }
             if (global)
                 for (auto& sp : specs) {
                     if (a.simple && !sp.simple) continue;
-                    Column c;
-                    c.name = std::string(sp.name) + suffix;
-                    c.values.resize((size_t)m.nnodes);
-                    c.set.resize((size_t)m.nnodes);
                     for (int64_t k = 0; k < m.nnodes; k++) {
                         const float tn = out[k * 7 + 5];
                         const bool ran = tn >= 1.0f;   // skipped sources set nothing
-                        c.values[k] = out[k * 7 + sp.outcol];
-                        bool set = ran;
-                        if (sp.outcol >= 1 && sp.outcol <= 3) set = ran && tn > 1.0f;   // HH / P / Tekl need > 1 node
-                        c.set[k] = set ? 1 : 0;
-                        if (!set) c.values[k] = -1.0f;
+                        bool on = ran;
+                        if (sp.outcol >= 1 && sp.outcol <= 3) on = ran && tn > 1.0f;   // HH / P / Tekl need > 1 node
+                        v[k] = out[k * 7 + sp.outcol];
+                        set[k] = on ? 1 : 0;
                     }
-                    if (sp.outcol == 1) displayed = (int)m.columns.size();
-                    m.columns.push_back(c);
+                    m.column(sp.name + suffix, v.data(), set.data(), false, sp.outcol == 1);
                 }
-            d.chunk = write_chunk(m.pm, m.nnodes, m.bins.data(), m.runs.data(), m.nruns, m.gridconn.data(), m.columns,
-                                  displayed);
+            d.put_displayed(m.bytes(), false);
             write_document(a.out, d);
         });
         std::cout << " ok" << std::endl;
@@ -664,7 +725,7 @@ struct StepDepth : Mode {
     }
     void run(const Args& a, Perf& perf) override {
         Document d;
-        timed(perf, "Load graph file", [&] { d = read_document(a.file); });
+        timed(perf, "Load graph file", [&] { read_document(a.file, d); });
         Context C;
         LoadedMap m;
         load_map(C, d, m);
@@ -694,17 +755,16 @@ struct StepDepth : Mode {
         if (rc != DMX_OK && rc != DMX_ERR_STATE) check(rc);   // no selection: analyseGraph returns false
         std::cout << " ok\nWriting out result..." << std::flush;
         timed(perf, "Writing graph", [&] {
-            int displayed = -1;
+            std::vector<float> v((size_t)m.nnodes);
+            std::vector<uint8_t> set((size_t)m.nnodes);
             if (rc == DMX_OK && (type == VISUAL || type == ANGULAR)) {
                 // VGAVisualGlobalDepth::run / VGAAngularDepth::run: one column, reset to -1, set on every
                 // reached cell (vgavisualglobaldepth.cpp:28, :49; vgaangulardepth.cpp:27, :53-55)
-                Column c;
-                c.name = type == VISUAL ? "Visual Step Depth" : "Angular Step Depth";
-                c.values.assign(out.begin(), out.begin() + m.nnodes);
-                c.set.resize((size_t)m.nnodes);
-                for (int64_t k = 0; k < m.nnodes; k++) c.set[k] = out[k] >= 0.0f ? 1 : 0;
-                displayed = (int)m.columns.size();
-                m.columns.push_back(c);
+                for (int64_t k = 0; k < m.nnodes; k++) {
+                    v[k] = out[k];
+                    set[k] = out[k] >= 0.0f ? 1 : 0;
+                }
+                m.column(type == VISUAL ? "Visual Step Depth" : "Angular Step Depth", v.data(), set.data(), false, true);
             } else if (rc == DMX_OK) {
                 // VGAMetricDepth::run column order (vgametricdepth.cpp:27-33); cells it never pops keep -1
                 const bool single = [&] {   // PointMap::setCurSel keeps FILLED cells only
@@ -720,20 +780,16 @@ struct StepDepth : Mode {
                 const char* names[3] = {"Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length",
                                         "Metric Straight-Line Distance"};
                 for (int j = 0; j < (single ? 3 : 2); j++) {
-                    Column c;
-                    c.name = names[j];
-                    c.values.resize((size_t)m.nnodes);
-                    c.set.resize((size_t)m.nnodes);
                     for (int64_t k = 0; k < m.nnodes; k++) {
-                        c.values[k] = out[k * 3 + j];
-                        c.set[k] = out[k * 3 + 1] >= 0.0f ? 1 : 0;
+                        v[k] = out[k * 3 + j];
+                        set[k] = out[k * 3 + 1] >= 0.0f ? 1 : 0;
                     }
-                    if (j == 1) displayed = (int)m.columns.size();
-                    m.columns.push_back(c);
+                    m.column(names[j], v.data(), set.data(), false, j == 1);
                 }
             }
-            d.chunk = write_chunk(m.pm, m.nnodes, m.bins.data(), m.runs.data(), m.nruns, m.gridconn.data(), m.columns,
-                                  displayed);
+            // the selection stays on the map the CLI writes (Point::SELECTED)
+            check(dmx_chunk_select_cells(m.chunk, sel.data(), (int64_t)sel.size()));
+            d.put_displayed(m.bytes(), false);
             write_document(a.out, d);
         });
         std::cout << " ok" << std::endl;
@@ -746,7 +802,8 @@ void print_help() {
                  "  VISPREP   -pg <grid spacing> -pp <x,y> | -pf <points file> [-pr <max visibility>] [-pb] [-pm]\n"
                  "  VGA       -vm visibility [-vl] [-vg -vr <radius|n>] | -vm metric -vr <radius|n> | -vm angular\n"
                  "  STEPDEPTH -sdt metric|visual|angular -sdp <x,y> | -sdf <points file>\n"
-                 "Input: a CSV drawing (x1,y1,x2,y2) or a .dmxg written by this tool; output: .dmxg\n";
+                 "Input: a depthmapX .graph (written back as .graph), or a CSV drawing (x1,y1,x2,y2) / a .dmxg\n"
+                 "written by this tool (written as .dmxg)\n";
 }
 
 } // namespace

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/dmx.h"
+#include "host/graphfile.hpp"
 #include "host/graphio.hpp"
 #include "host/pointmap.hpp"
 #include "kernels/makegraph.hip"
@@ -181,6 +182,7 @@ struct dmx_pointmap {
 struct dmx_graph {
     dmx_ctx* ctx = nullptr;
     dmx_pointmap* pm = nullptr;
+    std::vector<int32_t> merges;   // [m][2] merge links (cell, partner cell), x-major (Point::m_merge)
     int64_t nnodes = 0, node_begin = 0, node_end = 0;
     int64_t nruns = 0;
     DevBuf<Run> pool;
@@ -1172,7 +1174,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
     Q.bext = BEXT_DEFAULT;
     if (const char* b = getenv("DMX_VGA_BEXT")) Q.bext = std::max(0, atoi(b));
-    Q.crk = 2;   // the 2 longest common runs: the next two rarely resolve a tile the TT rows miss
+    Q.crk = 4;   // all 4 tile-common runs: the last two save ~20% of the phase-B cell tests
     if (const char* c = getenv("DMX_VGA_CRK")) Q.crk = std::min(CRK, std::max(0, atoi(c)));
     Q.work_counter = ctx->counters.p + 0; Q.error = ctx->counters.p + 1;
     DevBuf<int32_t> d_hist, d_nlev;
@@ -1234,7 +1236,10 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[21] = (long long)st[19];                          // phase-B cells
     ctx->last_stats[22] = (long long)st[20];                          // phase-B tiles resolved by ttvis
     ctx->last_stats[27] = (long long)st[25];                          // phase-B tiles pruned by ttany
-    ctx->last_stats[28] = (long long)st[26];                          // phase-B1 clocks
+    ctx->last_stats[28] = (long long)st[26];                          // phase-B row-test clocks (wave)
+    ctx->last_stats[29] = (long long)st[27];                          // phase-B tiles with cell tests
+    ctx->last_stats[30] = (long long)st[28];                          // phase-B cell-test clocks (wave)
+    ctx->last_stats[31] = (long long)st[29];                          // phase-B cells past hint + 4 heads
     ctx->last_stats[23] = (long long)st[21];                          // phase-C busy clocks summed over waves
     ctx->last_stats[24] = (long long)st[22];                          // phase-C run-scan clocks summed over waves
     ctx->last_stats[25] = (long long)st[23];                          // phase-C special-node clocks
@@ -1378,13 +1383,27 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     return DMX_OK;
 }
 
+// getMergePixel (vgavisualglobal.cpp:113-122, vgavisualglobaldepth.cpp:55-64, vgametric.cpp:97-104,
+// vgaangular.cpp:95-102, vgametricdepth.cpp:68-82, vgaangulardepth.cpp:57-66): a merge link joins two
+// cells' neighbourhoods, with per-analysis bookkeeping of the partner.  The GPU searches do not follow
+// merge links; maps that have them are refused rather than analysed differently (VGA visual local
+// has no merge logic and runs).
+static int refuse_merges(const dmx_graph* g) {
+    if (g && !g->merges.empty())
+        return fail(DMX_ERR_UNSUPPORTED, "point maps with merge links (LINK mode) are not on the accelerated path of "
+                                         "this analysis");
+    return DMX_OK;
+}
+
 int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
                    int64_t* levels) {
+    if (int rc = refuse_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out, false, levels);
 }
 
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se,
                           float* out_device) {
+    if (int rc = refuse_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out_device, true, nullptr);
 }
 
@@ -1393,6 +1412,7 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
 int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
                                int64_t n, float* out_device) {
     if (!ctx || !g || !out_device || (n > 0 && !nodes)) return fail(DMX_ERR_ARG, "bad arguments");
+    if (int rc = refuse_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
     HIPCHK(hipSetDevice(ctx->device));
@@ -1504,10 +1524,12 @@ static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
 }
 
 int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    if (int rc = refuse_merges(g)) return rc;
     return vga_search_all<false>(ctx, g, radius, gates_only, sb, se, out);
 }
 
 int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    if (int rc = refuse_merges(g)) return rc;
     return vga_search_all<true>(ctx, g, radius, gates_only, sb, se, out);
 }
 
@@ -1815,10 +1837,12 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
 }
 
 int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    if (int rc = refuse_merges(g)) return rc;
     return stepdepth_impl<false>(ctx, g, sel_cells, nsel, out);
 }
 
 int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    if (int rc = refuse_merges(g)) return rc;
     return stepdepth_impl<true>(ctx, g, sel_cells, nsel, out);
 }
 
@@ -1836,6 +1860,7 @@ int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {
 // are not expanded.  Runs on the tile-resolved BFS in seed mode (one workgroup).
 int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
+    if (int rc = refuse_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
     HIPCHK(hipSetDevice(ctx->device));
@@ -2054,6 +2079,7 @@ int dmx_pointmap_set_state(dmx_pointmap* pm, const int32_t* state) {
 int dmx_chunk_load(dmx_ctx* ctx, const dmx_chunk* c, const double* region, dmx_pointmap** pm_out, dmx_graph** g_out) {
     if (!ctx || !c || !region || !pm_out || !g_out) return fail(DMX_ERR_ARG, "bad arguments");
     const ParsedChunk& p = c->pc;
+    if (!p.processed) return fail(DMX_ERR_STATE, "the point map has no graph (run VISPREP -pm first)");
     Rect r{region[0], region[1], region[2], region[3]};
     std::unique_ptr<dmx_pointmap> pm(new dmx_pointmap());
     pm->host.reset(new PointMapHost(r, p.spacing, nullptr, 0));
@@ -2069,9 +2095,178 @@ int dmx_chunk_load(dmx_ctx* ctx, const dmx_chunk* c, const double* region, dmx_p
     int rc = dmx_graph_from_runs(ctx, pm.get(), N, p.bins.data(), p.runs.data(), (int64_t)p.runs.size() / 4,
                                  p.gridconn.data(), attrs.data(), &g);
     if (rc) return rc;
+    g->merges = p.merge_pairs;
     *pm_out = pm.release();
     *g_out = g;
     return DMX_OK;
 }
+
+int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n) {
+    if (!g || n < 0 || (n && !cell_pairs)) return fail(DMX_ERR_ARG, "bad arguments");
+    g->merges.assign(cell_pairs, cell_pairs + 2 * n);
+    return DMX_OK;
+}
+
+int dmx_chunk_flags(const dmx_chunk* c, int* processed, int* boundary, int64_t* merges, int64_t* nrows) {
+    if (!c) return fail(DMX_ERR_ARG, "chunk is NULL");
+    if (processed) *processed = c->pc.processed ? 1 : 0;
+    if (boundary) *boundary = c->pc.boundary ? 1 : 0;
+    if (merges) *merges = c->pc.merges;
+    if (nrows) *nrows = (int64_t)c->pc.row_keys.size();
+    return DMX_OK;
+}
+
+int dmx_chunk_set_column(dmx_chunk* c, const char* name, const float* values, const uint8_t* setmask, int locked,
+                         int make_displayed) {
+    if (!c || !name || (!values && !c->pc.row_keys.empty())) return fail(DMX_ERR_ARG, "bad arguments");
+    const int idx = chunk_set_column(c->pc, name, values, setmask, locked != 0);
+    if (make_displayed) c->pc.displayed_phys = idx;
+    return DMX_OK;
+}
+
+int dmx_chunk_set_displayed(dmx_chunk* c, int physical_column) {
+    if (!c) return fail(DMX_ERR_ARG, "chunk is NULL");
+    c->pc.displayed_phys = physical_column;
+    return DMX_OK;
+}
+
+int dmx_chunk_set_name(dmx_chunk* c, const char* name) {
+    if (!c || !name) return fail(DMX_ERR_ARG, "bad arguments");
+    c->pc.name = name;
+    return DMX_OK;
+}
+
+int dmx_chunk_select_cells(dmx_chunk* c, const int32_t* cells, int64_t n) {
+    if (!c || (n && !cells)) return fail(DMX_ERR_ARG, "bad arguments");
+    ParsedChunk& p = c->pc;
+    const int64_t C = (int64_t)p.cols * p.rows;
+    if ((int64_t)p.point_off.size() != C + 1) return fail(DMX_ERR_STATE, "chunk has no point records");
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t cell = cells[i];
+        if (cell < 0 || cell >= C) return fail(DMX_ERR_ARG, "cell outside the grid");
+        if (!(p.state[cell] & CELL_FILLED)) continue;   // PointMap::setCurSel keeps filled cells only
+        int32_t st;
+        std::memcpy(&st, &p.points_raw[p.point_off[cell]], 4);
+        st |= CELL_SELECTED;
+        std::memcpy(&p.points_raw[p.point_off[cell]], &st, 4);
+    }
+    return DMX_OK;
+}
+
+int dmx_chunk_unmake(dmx_chunk* c, int remove_links) {
+    if (!c) return fail(DMX_ERR_ARG, "chunk is NULL");
+    std::string err;
+    if (chunk_unmake(c->pc, remove_links != 0, err)) return fail(DMX_ERR_STATE, err);
+    return DMX_OK;
+}
+
+int dmx_chunk_serialize(const dmx_chunk* c, uint8_t* buf, int64_t cap, int64_t* size) {
+    if (!c || !size) return fail(DMX_ERR_ARG, "bad arguments");
+    std::vector<uint8_t> out;
+    std::string err;
+    if (write_parsed_chunk(c->pc, out, err)) return fail(DMX_ERR_STATE, err);
+    *size = (int64_t)out.size();
+    if (buf) {
+        if (cap < (int64_t)out.size()) return fail(DMX_ERR_ARG, "buffer too small");
+        std::memcpy(buf, out.data(), out.size());
+    }
+    return DMX_OK;
+}
+
+// ---------------------------------------------------------------- .graph file (MetaGraph container)
+struct dmx_graphfile {
+    GraphFile gf;
+    std::vector<double> lines;
+};
+
+int dmx_graphfile_read(const char* path, dmx_graphfile** out) {
+    if (!path || !out) return fail(DMX_ERR_ARG, "bad arguments");
+    FILE* f = fopen(path, "rb");
+    if (!f) return fail(DMX_ERR_ARG, std::string("cannot open ") + path);
+    std::vector<uint8_t> buf;
+    uint8_t tmp[1 << 16];
+    size_t k;
+    while ((k = fread(tmp, 1, sizeof(tmp), f)) > 0) buf.insert(buf.end(), tmp, tmp + k);
+    fclose(f);
+    std::unique_ptr<dmx_graphfile> g(new dmx_graphfile());
+    std::string err;
+    const int rc = read_graphfile(buf.data(), buf.size(), g->gf, err);
+    if (rc == -2) return fail(DMX_ERR_UNSUPPORTED, err);
+    if (rc) return fail(DMX_ERR_ARG, err);
+    g->lines = graphfile_lines(g->gf);
+    *out = g.release();
+    return DMX_OK;
+}
+
+int dmx_graphfile_free(dmx_graphfile* g) {
+    delete g;
+    return DMX_OK;
+}
+
+int dmx_graphfile_write(const dmx_graphfile* g, const char* path) {
+    if (!g || !path) return fail(DMX_ERR_ARG, "bad arguments");
+    std::vector<uint8_t> out;
+    std::string err;
+    if (write_graphfile(g->gf, out, err)) return fail(DMX_ERR_STATE, err);
+    FILE* f = fopen(path, "wb");
+    if (!f) return fail(DMX_ERR_ARG, std::string("cannot write ") + path);
+    const size_t w = fwrite(out.data(), 1, out.size(), f);
+    fclose(f);
+    if (w != out.size()) return fail(DMX_ERR_ARG, std::string("short write to ") + path);
+    return DMX_OK;
+}
+
+int dmx_graphfile_info(const dmx_graphfile* g, int32_t* state, int32_t* view_class, double* region, int64_t* nlines,
+                       int32_t* npointmaps, int32_t* displayed) {
+    if (!g) return fail(DMX_ERR_ARG, "graph file is NULL");
+    if (state) *state = g->gf.state;
+    if (view_class) *view_class = g->gf.view_class;
+    if (region) std::memcpy(region, g->gf.region, sizeof(g->gf.region));
+    if (nlines) *nlines = (int64_t)g->lines.size() / 4;
+    if (npointmaps) *npointmaps = (int32_t)g->gf.pointmaps.size();
+    if (displayed) *displayed = g->gf.displayed_pointmap;
+    return DMX_OK;
+}
+
+int dmx_graphfile_lines(const dmx_graphfile* g, double* lines) {
+    if (!g || (!lines && !g->lines.empty())) return fail(DMX_ERR_ARG, "bad arguments");
+    if (!g->lines.empty()) std::memcpy(lines, g->lines.data(), g->lines.size() * sizeof(double));
+    return DMX_OK;
+}
+
+int dmx_graphfile_set_view(dmx_graphfile* g, int32_t state, int32_t view_class) {
+    if (!g) return fail(DMX_ERR_ARG, "graph file is NULL");
+    g->gf.state = state;
+    g->gf.view_class = view_class;
+    return DMX_OK;
+}
+
+int dmx_graphfile_pointmap(const dmx_graphfile* g, int i, const uint8_t** chunk, int64_t* size) {
+    if (!g || !chunk || !size || i < 0 || i >= (int)g->gf.pointmaps.size()) return fail(DMX_ERR_ARG, "bad point map index");
+    *chunk = g->gf.pointmaps[i].data();
+    *size = (int64_t)g->gf.pointmaps[i].size();
+    return DMX_OK;
+}
+
+int dmx_graphfile_put_pointmap(dmx_graphfile* g, int i, const uint8_t* chunk, int64_t size) {
+    if (!g || !chunk || size <= 0 || i < -1 || i >= (int)g->gf.pointmaps.size()) return fail(DMX_ERR_ARG, "bad arguments");
+    if (i < 0) {   // MetaGraph::addNewPointMap: appended and displayed
+        g->gf.pointmaps.emplace_back(chunk, chunk + size);
+        g->gf.displayed_pointmap = (int32_t)g->gf.pointmaps.size() - 1;
+    } else {
+        g->gf.pointmaps[i].assign(chunk, chunk + size);
+    }
+    return DMX_OK;
+}
+
+int dmx_graphfile_new_pointmap_name(const dmx_graphfile* g, char* name, int cap) {
+    if (!g || !name || cap <= 0) return fail(DMX_ERR_ARG, "bad arguments");
+    const std::string n = new_pointmap_name(g->gf, "VGA Map");
+    if ((int)n.size() + 1 > cap) return fail(DMX_ERR_ARG, "buffer too small");
+    std::memcpy(name, n.c_str(), n.size() + 1);
+    return DMX_OK;
+}
+
+int32_t dmx_view_vga_top(int32_t view_class) { return view_vga_top(view_class); }
 
 } // extern "C"

@@ -101,6 +101,10 @@ int write_pointmap_chunk(const PointMapHost& h, int64_t nnodes, const int32_t* b
     w.put<int32_t>((int32_t)h.filled_count());
     w.put<double>(h.bottom_left().x);
     w.put<double>(h.bottom_left().y);
+    // no graph (VISPREP without -pm): no Node records, an empty attribute table (rows are added by
+    // sparkGraph2, pointdata.cpp:1294), m_processed false, displayed attribute -2
+    const bool graph = bins != nullptr;
+    if (!graph) nnodes = 0;
     std::vector<int> order(cols.size());
     std::iota(order.begin(), order.end(), 0);
     std::sort(order.begin(), order.end(), [&](int a, int b) { return cols[a].name < cols[b].name; });
@@ -108,6 +112,7 @@ int write_pointmap_chunk(const PointMapHost& h, int64_t nnodes, const int32_t* b
     for (size_t i = 0; i < order.size(); i++)
         if (order[i] == displayed) sorted_disp = (int)i;
     if (displayed < 0) sorted_disp = displayed;
+    if (!graph) sorted_disp = -2;
     w.put<int32_t>(sorted_disp);
     // ---- AttributeTable::write: layer manager with the single "Everything" layer
     w.put<int64_t>(0xC0000000LL);   // availableLayers = 0xffffffff << (32 + 0xfffffffe) (unsigned wrap: << 30)
@@ -133,7 +138,7 @@ int write_pointmap_chunk(const PointMapHost& h, int64_t nnodes, const int32_t* b
     }
     w.put<int32_t>((int32_t)nnodes);
     const auto& st = h.state();
-    {
+    if (graph) {
         int64_t k = 0;
         for (int x = 0; x < C_cols; x++)
             for (int y = 0; y < C_rows; y++) {
@@ -155,7 +160,7 @@ int write_pointmap_chunk(const PointMapHost& h, int64_t nnodes, const int32_t* b
     for (int x = 0; x < C_cols; x++)
         for (int y = 0; y < C_rows; y++) {
             const int32_t s = st[h.index(x, y)];
-            const bool node = (s & CELL_FILLED) != 0;
+            const bool node = graph && (s & CELL_FILLED) != 0;
             w.put<int32_t>(s);
             w.put<int32_t>(0);   // m_block
             w.put<int32_t>(0);   // dummy
@@ -210,9 +215,135 @@ int write_pointmap_chunk(const PointMapHost& h, int64_t nnodes, const int32_t* b
             w.put<double>(loc.x);
             w.put<double>(loc.y);
         }
-    if (ro != nruns) { err = "run count does not match the bins"; return -1; }
-    w.put<uint8_t>(1);                 // m_processed
-    w.put<uint8_t>(boundary ? 1 : 0);  // m_boundarygraph
+    if (graph && ro != nruns) { err = "run count does not match the bins"; return -1; }
+    w.put<uint8_t>(graph ? 1 : 0);     // m_processed
+    w.put<uint8_t>(graph && boundary ? 1 : 0);  // m_boundarygraph
+    return 0;
+}
+
+int write_parsed_chunk(const ParsedChunk& pc, std::vector<uint8_t>& out, std::string& err) {
+    out.clear();
+    Writer w{out};
+    const int ncols = (int)pc.columns.size();
+    const int64_t nrows = (int64_t)pc.row_keys.size();
+    for (const auto& c : pc.columns)
+        if ((int64_t)c.values.size() != nrows) { err = "column length does not match the attribute rows"; return -1; }
+    w.str(pc.name);
+    w.put<double>(pc.spacing);
+    w.put<int32_t>(pc.rows);
+    w.put<int32_t>(pc.cols);
+    w.put<int32_t>(pc.filled);
+    w.put<double>(pc.blx);
+    w.put<double>(pc.bly);
+    std::vector<int> order(ncols);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return pc.columns[a].name < pc.columns[b].name; });
+    // AttributeTable::getColumnSortedIndex (attributetable.cpp:479-485)
+    int32_t sd = pc.displayed_phys;
+    if (sd >= 0) {
+        if (sd >= ncols) sd = -1;
+        else
+            for (int i = 0; i < ncols; i++)
+                if (order[i] == pc.displayed_phys) sd = i;
+    }
+    w.put<int32_t>(sd);
+    out.insert(out.end(), pc.layers_raw.begin(), pc.layers_raw.end());
+    w.put<int32_t>(ncols);
+    for (int ci : order) {
+        const ChunkColumn& c = pc.columns[ci];
+        float mn = c.min, mx = c.max;
+        double tot = c.total;
+        if (!c.from_file) {
+            const Stats s = replay_stats(c.values.data(), c.set.empty() ? nullptr : c.set.data(), nrows);
+            mn = (float)s.min;
+            mx = (float)s.max;
+            tot = s.total;
+        }
+        w.str(c.name);
+        w.put<float>(mn);
+        w.put<float>(mx);
+        w.put<double>(tot);
+        w.put<int32_t>(ci);
+        w.put<uint8_t>(c.hidden);
+        w.put<uint8_t>(c.locked ? 1 : 0);
+        out.insert(out.end(), c.display, c.display + 12);
+        w.str(c.formula);
+    }
+    w.put<int32_t>((int32_t)nrows);
+    for (int64_t i = 0; i < nrows; i++) {
+        w.put<int32_t>(pc.row_keys[i]);
+        w.put<int64_t>(i < (int64_t)pc.row_layers.size() ? pc.row_layers[i] : 1);
+        w.put<uint32_t>((uint32_t)ncols);
+        for (const ChunkColumn& c : pc.columns) w.put<float>(c.values[i]);
+    }
+    out.insert(out.end(), pc.table_display, pc.table_display + 12);
+    out.insert(out.end(), pc.points_raw.begin(), pc.points_raw.end());
+    w.put<uint8_t>(pc.processed ? 1 : 0);
+    w.put<uint8_t>(pc.boundary ? 1 : 0);
+    return 0;
+}
+
+int chunk_set_column(ParsedChunk& pc, const std::string& name, const float* values, const uint8_t* set, bool locked) {
+    const int64_t nrows = (int64_t)pc.row_keys.size();
+    int idx = -1;
+    for (size_t i = 0; i < pc.columns.size(); i++)
+        if (pc.columns[i].name == name) idx = (int)i;
+    if (idx < 0) {   // addColumnInternal: appended, default display params, every row -1
+        ChunkColumn c;
+        c.name = name;
+        pc.columns.push_back(c);
+        idx = (int)pc.columns.size() - 1;
+    }
+    ChunkColumn& c = pc.columns[idx];   // reset: stats default, values -1, lock as asked
+    c.from_file = false;
+    c.locked = locked;
+    c.values.assign((size_t)nrows, -1.0f);
+    c.set.assign((size_t)nrows, 0);
+    for (int64_t i = 0; i < nrows; i++)
+        if (!set || set[i]) {
+            c.values[i] = values[i];
+            c.set[i] = 1;
+        }
+    return idx;
+}
+
+int chunk_unmake(ParsedChunk& pc, bool remove_links, std::string& err) {
+    std::vector<uint8_t> pts;
+    const size_t C = (size_t)pc.cols * pc.rows;
+    if (pc.point_off.size() != C + 1) { err = "chunk has no point records"; return -1; }
+    std::vector<uint64_t> off(C + 1, 0);
+    for (size_t i = 0; i < C; i++) {
+        const uint8_t* rec = pc.points_raw.data() + pc.point_off[i];
+        const size_t len = (size_t)(pc.point_off[i + 1] - pc.point_off[i]);
+        off[i] = pts.size();
+        int32_t st;
+        std::memcpy(&st, rec, 4);
+        if (!(st & CELL_FILLED)) {
+            pts.insert(pts.end(), rec, rec + len);
+            continue;
+        }
+        st &= ~CELL_BLOCKED;                            // setBlock(false)
+        const size_t at = pts.size();
+        pts.insert(pts.end(), rec, rec + 18);           // state, block, dummy, grid conn, merge, has_node
+        std::memcpy(&pts[at], &st, 4);
+        pts[at + 12] = 0;                               // m_grid_connections
+        if (remove_links) std::memset(&pts[at + 13], 0xFF, 4);   // m_merge = NoPixel
+        pts[at + 17] = 0;                               // m_node = nullptr
+        pts.insert(pts.end(), rec + len - 16, rec + len);   // m_location
+    }
+    off[C] = pts.size();
+    pc.points_raw.swap(pts);
+    pc.point_off.swap(off);
+    pc.columns.clear();                                 // m_attributes->clear(): columns and rows
+    pc.row_keys.clear();
+    pc.row_layers.clear();
+    pc.processed = false;
+    pc.boundary = false;
+    pc.displayed_phys = -2;
+    pc.gridconn.clear();
+    pc.bins.clear();
+    pc.runs.clear();
+    for (size_t i = 0; i < C; i++) pc.state[i] &= ~CELL_BLOCKED;
     return 0;
 }
 
@@ -227,6 +358,8 @@ int read_pointmap_chunk(const uint8_t* buf, size_t size, ParsedChunk& pc, std::s
     pc.blx = r.get<double>();
     pc.bly = r.get<double>();
     pc.displayed_sorted = r.get<int32_t>();
+    pc.displayed_phys = pc.displayed_sorted;   // PointMap::read: setDisplayedAttribute(value read)
+    const size_t lay0 = r.o;
     (void)r.get<int64_t>();
     (void)r.get<int64_t>();
     const int32_t nlayers = r.get<int32_t>();
@@ -234,6 +367,8 @@ int read_pointmap_chunk(const uint8_t* buf, size_t size, ParsedChunk& pc, std::s
         (void)r.get<int64_t>();
         (void)r.str();
     }
+    if (!r.ok || nlayers < 0) { err = "not a PointMap chunk"; return -1; }
+    pc.layers_raw.assign(buf + lay0, buf + r.o);
     const int32_t ncols = r.get<int32_t>();
     if (!r.ok || ncols < 0 || ncols > 4096 || pc.rows <= 0 || pc.cols <= 0) { err = "not a PointMap chunk"; return -1; }
     std::vector<ChunkColumn> sorted(ncols);
@@ -244,12 +379,12 @@ int read_pointmap_chunk(const uint8_t* buf, size_t size, ParsedChunk& pc, std::s
         sorted[i].max = r.get<float>();
         sorted[i].total = r.get<double>();
         phys[i] = r.get<int32_t>();
-        (void)r.get<uint8_t>();
+        sorted[i].hidden = r.get<uint8_t>();
         sorted[i].locked = r.get<uint8_t>() != 0;
-        (void)r.get<float>();
-        (void)r.get<float>();
-        (void)r.get<int32_t>();
-        (void)r.str();
+        if (r.o + 12 <= size) std::memcpy(sorted[i].display, buf + r.o, 12);
+        r.o += 12;
+        sorted[i].formula = r.str();
+        sorted[i].from_file = true;
     }
     pc.columns.assign(ncols, ChunkColumn());
     for (int i = 0; i < ncols; i++) {
@@ -260,30 +395,41 @@ int read_pointmap_chunk(const uint8_t* buf, size_t size, ParsedChunk& pc, std::s
     if (!r.ok || nrows < 0) { err = "truncated attribute table"; return -1; }
     for (auto& c : pc.columns) c.values.assign(nrows, -1.0f);
     pc.row_keys.resize(nrows);
+    pc.row_layers.resize(nrows);
     for (int32_t i = 0; i < nrows && r.ok; i++) {
         pc.row_keys[i] = r.get<int32_t>();
-        (void)r.get<int64_t>();
+        pc.row_layers[i] = r.get<int64_t>();
         const uint32_t n = r.get<uint32_t>();
         for (uint32_t j = 0; j < n && r.ok; j++) {
             const float v = r.get<float>();
             if ((int)j < ncols) pc.columns[j].values[i] = v;
         }
     }
-    (void)r.get<float>();
-    (void)r.get<float>();
-    (void)r.get<int32_t>();
+    if (r.o + 12 <= size) std::memcpy(pc.table_display, buf + r.o, 12);
+    r.o += 12;
     const int64_t C = (int64_t)pc.cols * pc.rows;
     pc.state.resize(C);
     pc.gridconn.clear();
     pc.bins.clear();
     pc.runs.clear();
+    pc.points_raw.clear();
+    pc.point_off.assign((size_t)C + 1, 0);
+    pc.merges = 0;
+    pc.merge_pairs.clear();
     for (int x = 0; x < pc.cols && r.ok; x++)
         for (int y = 0; y < pc.rows && r.ok; y++) {
+            const size_t rec0 = r.o;
             pc.state[(int64_t)x * pc.rows + y] = r.get<int32_t>();
             (void)r.get<int32_t>();
             (void)r.get<int32_t>();
             const int8_t gc = r.get<int8_t>();
-            (void)r.get<int32_t>();   // merge
+            const int32_t merge = r.get<int32_t>();
+            if (merge != -1) {   // PixelRef NoPixel = (-1, -1); {short x, short y} little-endian
+                pc.merges++;
+                const int mx = (int16_t)(merge & 0xFFFF), my = (int16_t)((uint32_t)merge >> 16);
+                pc.merge_pairs.push_back((int32_t)((int64_t)x * pc.rows + y));
+                pc.merge_pairs.push_back((int32_t)((int64_t)mx * pc.rows + my));
+            }
             const bool node = r.get<uint8_t>() != 0;
             if (node) {
                 pc.gridconn.push_back((uint8_t)gc);
@@ -333,7 +479,18 @@ int read_pointmap_chunk(const uint8_t* buf, size_t size, ParsedChunk& pc, std::s
             }
             (void)r.get<double>();
             (void)r.get<double>();
+            if (!r.ok) break;
+            // the record as Point::write re-emits it: PointMap::read masks the state (pointdata.cpp:1128)
+            // and Point::write writes a zero dummy (point.cpp:57-58)
+            const size_t at = pc.points_raw.size();
+            pc.point_off[(size_t)x * pc.rows + y] = at;
+            pc.points_raw.insert(pc.points_raw.end(), buf + rec0, buf + r.o);
+            int32_t st = pc.state[(int64_t)x * pc.rows + y] & (CELL_EMPTY | CELL_FILLED | CELL_MERGED | CELL_BLOCKED |
+                                                               CELL_CONTEXTFILLED | CELL_EDGE);
+            std::memcpy(&pc.points_raw[at], &st, 4);
+            std::memset(&pc.points_raw[at + 8], 0, 4);
         }
+    pc.point_off[(size_t)C] = pc.points_raw.size();
     pc.processed = r.get<uint8_t>() != 0;
     pc.boundary = r.get<uint8_t>() != 0;
     if (!r.ok) { err = "truncated PointMap chunk"; return -1; }

@@ -43,7 +43,8 @@ void PointMapHost::load_state(int cols, int rows, double spacing, Vec2 bl, const
 }
 
 void PointMapHost::restore_fill(const int32_t* state) {
-    const int32_t keep = CELL_FILLED | CELL_EDGE | CELL_CONTEXTFILLED | CELL_EMPTY;
+    // PointMap::read keeps MERGED as well (pointdata.cpp:1128); unmake clears the link, not the bit
+    const int32_t keep = CELL_FILLED | CELL_EDGE | CELL_CONTEXTFILLED | CELL_EMPTY | CELL_MERGED;
     filled_ = 0;
     for (int64_t c = 0; c < cells(); c++) {
         state_[c] = (state_[c] & ~keep) | (state[c] & keep);

@@ -25,7 +25,7 @@ namespace dmx {
 
 constexpr int KH = 8;        // head runs per cell (first KH entries of its scan order)
 constexpr int CRK = 4;       // tile-common runs per tile
-constexpr int BEXT_DEFAULT = 16;   // runs after the heads a cell scans on its own lane before going wave-cooperative
+constexpr int BEXT_DEFAULT = 4;   // runs after the heads a cell scans on its own lane before going wave-cooperative
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
 
 struct VgaTileParams {
@@ -198,16 +198,25 @@ __device__ __forceinline__ bool line_hits(const unsigned long long* F, const uns
 // Diagonal run (Bin::make's single first-to-last span, ngraph.cpp:243-258): walked tile by tile;
 // the run's cells inside one 8x8 tile are a shifted (anti-)diagonal bit pattern, so a tile costs
 // one summary bit and at most one frontier word instead of up to 8 per-cell tests.
+// The tile sequence of a run does not depend on the frontier, so the frontier words of 8 tiles are
+// read per round (independent LDS reads, OR-accumulated): a run across the grid costs ~16 dependent
+// LDS round trips instead of ~125.
 __device__ __forceinline__ bool diag_hits(const FView& V, Run ru) {
     const int dy = (ru.y1 > ru.y0) ? 1 : -1;
     int x = ru.x0, y = ru.y0;
     while (x <= ru.x1) {
-        int n;
-        const unsigned long long m = diag_tile_mask(x, y, dy, ru.x1, n);
-        const int tx = x >> 3, ty = y >> 3;
-        if (((V.Fsr[ty * V.wr + (tx >> 6)] >> (tx & 63)) & 1ull) && (V.F[ty * V.tw + tx] & m)) return true;
-        x += n;
-        y += dy * n;
+        unsigned long long acc = 0ull;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            if (x <= ru.x1) {
+                int n;
+                const unsigned long long m = diag_tile_mask(x, y, dy, ru.x1, n);
+                acc |= V.F[(y >> 3) * V.tw + (x >> 3)] & m;
+                x += n;
+                y += dy * n;
+            }
+        }
+        if (acc) return true;
     }
     return false;
 }
@@ -490,118 +499,110 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 sync_global();
                 if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(9, n - tmark); tmark = n; }
                 const int qn = S.qn;
-                // ---- B1: tile-to-tile certain test, a wave per queued tile, 4 tiles per step (their
-                // TT rows in flight together); the cells of tiles it does not resolve go to B2
-                int32_t* LB = L + (size_t)nt * 64;
-                for (int it0 = wave * 4; it0 < qn; it0 += NW * 4) {
-                    int4 e[4];
+                // ---- B: a wave per queued tile, lane = cell of the tile.  The tile-to-tile rows
+                // (ttvis: a frontier tile every regular cell of t sees completely resolves them all;
+                // ttany: no frontier tile in view of any regular cell of t, none is at this level)
+                // and the cells' first runs (scan start, run count, hint, 4 heads -- coalesced, tile
+                // order) are loaded in one round, independently of each other; the cells the rows
+                // leave open then test the hint run, the heads and the next bext runs of their scan
+                // order.  Misses go to the hard list.
+                for (;;) {
+                    // dynamic: the few tiles that need cell tests cost ~100x a row-resolved one
+                    int it = 0;
+                    if (lane == 0) it = atomicAdd(&S.bn, 1);
+                    it = __shfl(it, 0);
+                    if (it >= qn) break;
+                    const int4 e = Q[it];
+                    const int t = e.x;
+                    unsigned long long mask = (unsigned long long)(unsigned)e.z | ((unsigned long long)(unsigned)e.w << 32);
+                    const int id = (t << 6) | lane;
+                    const unsigned long long reg = P.regular_tiles[t];
+                    const bool lreg = !SPECIAL || ((reg >> lane) & 1ull);
+                    const bool cand = ((mask >> lane) & 1ull) && lreg;
+                    int64_t ss = 0;
+                    int nr = 0, hp = 0xFFFF;
+                    constexpr int KH0 = 4;
+                    Run hd[KH0];
+                    if (cand) {
+                        ss = P.tscan_start[id];
+                        nr = P.tnruns[id];
+                        hp = Hn[id];
 #pragma unroll
-                    for (int j = 0; j < 4; j++) e[j] = (it0 + j < qn) ? Q[it0 + j] : make_int4(-1, 0, 0, 0);
-                    unsigned long long acc[4] = {0ull, 0ull, 0ull, 0ull}, acca[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+                        for (int r = 0; r < KH0; r++) hd[r] = P.heads[r * hstride + id];
+                    }
+                    unsigned long long acc = 0ull, acca = ~0ull;
                     if (P.ttvis) {
-#pragma unroll
-                        for (int j = 0; j < 4; j++) acca[j] = 0ull;
+                        acca = 0ull;
 #pragma unroll
                         for (int k = 0; k < 4; k++) {
                             const int w = k * 64 + lane;
                             const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
                             if (fs) {
-#pragma unroll
-                                for (int j = 0; j < 4; j++)
-                                    if (e[j].x >= 0) {
-                                        acc[j] |= P.ttvis[(size_t)e[j].x * P.tvw + w] & fs;
-                                        acca[j] |= P.ttany[(size_t)e[j].x * P.tvw + w] & fs;
-                                    }
+                                acc |= P.ttvis[(size_t)t * P.tvw + w] & fs;
+                                acca |= P.ttany[(size_t)t * P.tvw + w] & fs;
                             }
                         }
                     }
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const int t = e[j].x;
-                        if (t < 0) break;
-                        unsigned long long mask = (unsigned long long)(unsigned)e[j].z | ((unsigned long long)(unsigned)e[j].w << 32);
-                        const unsigned long long reg = P.regular_tiles[t];
-                        if (lane == 0) { ST(18, 1); ST(19, __popcll(mask)); }
-                        if (__ballot(acc[j] != 0ull) != 0ull) {
-                            // a frontier tile every regular cell of t sees completely
-                            const unsigned long long R = mask & reg;
-                            if (lane == 0) { or_wg(&Xg[t], R); ST(20, 1); }
-                            mask &= ~R;
-                        } else if (__ballot(acca[j] != 0ull) == 0ull) {
-                            // no regular cell of t sees any frontier tile: none is at the next level
-                            if (lane == 0) ST(25, 1);
-                            mask &= ~reg;
-                        }
-                        const bool mine = (mask >> lane) & 1ull;
-                        const unsigned long long bm = __ballot(mine);
-                        if (bm) {
-                            int base = 0;
-                            if (lane == 0) base = atomicAdd(&S.bn, __popcll(bm));
-                            base = __shfl(base, 0);
-                            const int id = (t << 6) | lane;
-                            const bool lreg = !SPECIAL || ((reg >> lane) & 1ull);
-                            if (mine) LB[base + __popcll(bm & ((1ull << lane) - 1ull))] = lreg ? id : (-1 - id);
-                        }
+                    if (lane == 0) { ST(18, 1); ST(19, __popcll(mask)); }
+                    const unsigned long long bt0 = __builtin_amdgcn_s_memtime();
+                    if (__ballot(acc != 0ull) != 0ull) {
+                        // a frontier tile every regular cell of t sees completely
+                        const unsigned long long R = mask & reg;
+                        if (lane == 0) { or_wg(&Xg[t], R); ST(20, 1); }
+                        mask &= ~R;
+                    } else if (__ballot(acca != 0ull) == 0ull) {
+                        // no regular cell of t sees any frontier tile: none is at the next level
+                        if (lane == 0) ST(25, 1);
+                        mask &= ~reg;
                     }
-                }
-                sync_global();
-                if (tid == 0) ST(26, __builtin_amdgcn_s_memtime() - tmark);   // B1 share of the heads clock
-                const int bn = S.bn;
-                // ---- B2: per cell (lane = cell, full waves): the hint run, the heads, then the next
-                // bext runs of the scan order; misses go to the hard list
-                for (int b0 = wave * 64; b0 < bn; b0 += NW * 64) {
-                    const int i = b0 + lane;
+                    const bool mine = (mask >> lane) & 1ull;
+                    const unsigned long long bt1 = __builtin_amdgcn_s_memtime();
+                    if (lane == 0) { ST(26, bt1 - bt0); if (__ballot(mine)) ST(27, 1); }
                     bool hit = false, to_hard = false;
                     int hard_val = 0;
-                    if (i < bn) {
-                        const int v = LB[i];
-                        if (v < 0) {
-                            to_hard = true;
-                            hard_val = v;   // special node: exact path
-                        } else {
-                            const int id = v;
-                            const int64_t ss = P.tscan_start[id];
-                            const int nr = P.tnruns[id];
-                            const int hp = Hn[id];
-                            constexpr int KH0 = 4;
-                            Run hd[KH0];
-#pragma unroll
-                            for (int r = 0; r < KH0; r++) hd[r] = P.heads[r * hstride + id];
-                            if (hp >= KH && hp < nr) {   // the run that hit for a recent source
-                                rt++;
-                                hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
-                            }
+                    if (mine && !lreg) {
+                        to_hard = true;
+                        hard_val = -1 - id;   // special node: exact path
+                    } else if (mine) {
+                        if (hp >= KH && hp < nr) {   // the run that hit for a recent source
+                            rt++;
+                            hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
+                        }
 #pragma unroll 1
-                            for (int r = 0; r < KH0; r++)
-                                if (!hit && r < nr) {
-                                    rt++;
-                                    if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != r) Hn[id] = (uint16_t)r; }
-                                }
-                            const int lim = min(nr, KH + P.bext);
-                            for (int base = KH0; base < lim && !hit; base += 4) {
-                                Run rr[4];
-#pragma unroll
-                                for (int j = 0; j < 4; j++) {
-                                    const int r = base + j;
-                                    if (r < KH) rr[j] = P.heads[r * hstride + id];
-                                    else if (r < lim) rr[j] = P.scan_pool[ss + r];
-                                    else rr[j].x0 = -1;
-                                }
-                                bool h4[4];
-#pragma unroll
-                                for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
-                                int fj = -1;
-#pragma unroll
-                                for (int j = 3; j >= 0; j--)
-                                    if (h4[j]) fj = j;
-                                rt += (unsigned)min(4, lim - base);
-                                if (fj >= 0) { hit = true; if (hp != base + fj) Hn[id] = (uint16_t)(base + fj); }
+                        for (int r = 0; r < KH0; r++)
+                            if (!hit && r < nr) {
+                                rt++;
+                                if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != r) Hn[id] = (uint16_t)r; }
                             }
-                            if (hit) or_wg(&Xg[id >> 6], 1ull << (id & 63));
-                            else if (nr > KH + P.bext) { to_hard = true; hard_val = id; }
+                        const int lim = min(nr, KH + P.bext);
+                        if (!hit) ST(29, 1);
+                        for (int base = KH0; base < lim && !hit; base += 4) {
+                            Run rr[4];
+#pragma unroll
+                            for (int j = 0; j < 4; j++) {
+                                const int r = base + j;
+                                if (r < KH) rr[j] = P.heads[r * hstride + id];
+                                else if (r < lim) rr[j] = P.scan_pool[ss + r];
+                                else rr[j].x0 = -1;
+                            }
+                            bool h4[4];
+#pragma unroll
+                            for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
+                            int fj = -1;
+#pragma unroll
+                            for (int j = 3; j >= 0; j--)
+                                if (h4[j]) fj = j;
+                            rt += (unsigned)min(4, lim - base);
+                            if (fj >= 0) { hit = true; if (hp != base + fj) Hn[id] = (uint16_t)(base + fj); }
+                        }
+                        if (!hit) {
+                            if (nr > KH + P.bext) { to_hard = true; hard_val = id; }
                             else { ST(5, 1); ST(6, nr); }
                         }
                     }
+                    const unsigned long long hm = __ballot(hit);
+                    if (lane == 0) ST(28, __builtin_amdgcn_s_memtime() - bt1);
+                    if (hm && lane == 0) or_wg(&Xg[t], hm);
                     const unsigned long long hw = __ballot(to_hard);
                     if (hw) {
                         int base = 0;
@@ -613,93 +614,122 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
                 sync_global();
                 if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(10, n - tmark); tmark = n; }
                 const int hn = S.hn;
-                // ---- C: hard cells, a wave scans 64 runs at a time (dynamic work counter)
+                // ---- C: hard cells.  A wave grabs CCH list entries at once (one coalesced load);
+                // C0 tests their tile-visibility rows two cells at a time (16 row words a lane in
+                // flight): a frontier tile the cell sees completely is a certain hit (regular cell:
+                // in-set == out-set), no tile in view holding a frontier cell a certain miss.  C1
+                // scans the run lists of the undecided cells, 256 runs a step (4 loads a lane).
+                constexpr int CCH = 16;
                 const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
                 for (;;) {
-                    int it = 0;
-                    if (lane == 0) it = atomicAdd(&S.item, 1);
-                    it = __shfl(it, 0);
-                    if (it >= hn) break;
-                    int id = L[it];
-                    const bool special = id < 0;
-                    if (special) id = -1 - id;
-                    bool found = false;
-                    int nr = 0;
-                    if (SPECIAL && special) {
-                        int x, y;
-                        xy_of_tile_id(id, tw, x, y);
-                        const unsigned long long sp_t0 = __builtin_amdgcn_s_memtime();
-                        found = special_hit(P, FV, id, x, y, &nr);
-                        if (lane == 0) { ST(23, __builtin_amdgcn_s_memtime() - sp_t0); ST(24, 1); }
-                        if (lane == 0) rt += (unsigned)nr;
-                    } else {
-                        const int64_t rs = P.tscan_start[id];
-                        nr = P.tnruns[id];
-                        int base = KH + P.bext;   // the first KH + bext runs were tested in phase B
-                        bool pruned_now = false, certain = false;
-                        if (P.tvis) {
-                            // A frontier tile the cell sees completely is a certain hit (regular cell:
-                            // in-set == out-set); no tile the cell sees holding a frontier cell means
-                            // no run can hit.  Both rows (tvw <= 256: 4 words a lane) are loaded at once.
-                            const unsigned long long* tv = P.tvis + (size_t)id * P.tvw;
-                            const unsigned long long* ftv = P.ftvis ? P.ftvis + (size_t)id * P.tvw : nullptr;
-                            unsigned long long fa = 0ull, ta = 0ull;
+                    int it0 = 0;
+                    if (lane == 0) it0 = atomicAdd(&S.item, CCH);
+                    it0 = __shfl(it0, 0);
+                    if (it0 >= hn) break;
+                    const int cn = min(CCH, hn - it0);
+                    const int myv = lane < cn ? L[it0 + lane] : -1;
+                    unsigned long long certain_m = 0ull, pruned_m = 0ull;   // bit j: chunk entry j
+                    if (P.tvis) {
+                        for (int j = 0; j < cn; j += 2) {
+                            const int v0 = __builtin_amdgcn_readlane(myv, j);
+                            const int v1 = __builtin_amdgcn_readlane(myv, j + 1);
+                            const bool r0 = v0 >= 0, r1 = j + 1 < cn && v1 >= 0;
+                            const unsigned long long* tv0 = P.tvis + (size_t)(r0 ? v0 : 0) * P.tvw;
+                            const unsigned long long* tv1 = P.tvis + (size_t)(r1 ? v1 : 0) * P.tvw;
+                            const unsigned long long* fv0 = P.ftvis ? P.ftvis + (size_t)(r0 ? v0 : 0) * P.tvw : nullptr;
+                            const unsigned long long* fv1 = P.ftvis ? P.ftvis + (size_t)(r1 ? v1 : 0) * P.tvw : nullptr;
+                            unsigned long long fa0 = 0ull, ta0 = 0ull, fa1 = 0ull, ta1 = 0ull;
 #pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const int w = j * 64 + lane;
+                            for (int k = 0; k < 4; k++) {
+                                const int w = k * 64 + lane;
                                 const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
                                 if (fs) {   // rows are read only under frontier tile rows
-                                    ta |= tv[w] & fs;
-                                    if (ftv) fa |= ftv[w] & fs;
+                                    if (r0) {
+                                        ta0 |= tv0[w] & fs;
+                                        if (fv0) fa0 |= fv0[w] & fs;
+                                    }
+                                    if (r1) {
+                                        ta1 |= tv1[w] & fs;
+                                        if (fv1) fa1 |= fv1[w] & fs;
+                                    }
                                 }
                             }
-                            certain = __ballot(fa != 0ull) != 0ull;
-                            if (lane == 0) ST(14, 1);
-                            if (certain) {
-                                found = true;
-                                if (lane == 0) { ST(16, 1); ST(1, 1); }
-                            } else if (__ballot(ta != 0ull) == 0ull) {
-                                base = nr;
-                                pruned_now = true;
-                                if (lane == 0) ST(13, 1);
+                            if (r0) {
+                                if (__ballot(fa0 != 0ull)) certain_m |= 1ull << j;
+                                else if (!__ballot(ta0 != 0ull)) pruned_m |= 1ull << j;
+                            }
+                            if (r1) {
+                                if (__ballot(fa1 != 0ull)) certain_m |= 2ull << j;
+                                else if (!__ballot(ta1 != 0ull)) pruned_m |= 2ull << j;
                             }
                         }
-                        // 4 runs per lane per step (256 per wave): four independent loads in flight
-                        const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
-                        for (; base < nr && !found; base += 256) {
-                            Run rr[4];
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const int r = base + j * 64 + lane;
-                                if (r < nr) rr[j] = P.scan_pool[rs + r];
-                                else rr[j].x0 = -1;
-                            }
-                            // the four tests are independent (no early-out between them), so their
-                            // LDS round trips overlap
-                            bool h4[4];
-#pragma unroll
-                            for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
-                            int fpos = -1;
-#pragma unroll
-                            for (int j = 3; j >= 0; j--) {
-                                const unsigned long long hm = __ballot(h4[j]);
-                                if (hm) fpos = base + j * 64 + __ffsll((long long)hm) - 1;
-                            }
-                            found = fpos >= 0;
-                            if (found && lane == 0) Hn[id] = (uint16_t)min(fpos, 0xFFFE);
-                        }
-                        if (lane == 0) ST(22, __builtin_amdgcn_s_memtime() - s_t0);
-                        if (lane == 0 && !certain && !(P.tvis && base == nr && !found && nr > KH + P.bext && pruned_now)) {
-                            const unsigned long long sc = (unsigned long long)max(min(base, nr) - KH - P.bext, 0);
-                            rt += (unsigned)sc;
-                            ST(15, sc);
-                            if (found) ST(1, 1);
+                        const unsigned long long regm = __ballot(lane < cn && myv >= 0);
+                        if (lane == 0) {
+                            ST(14, __popcll(regm));
+                            ST(16, __popcll(certain_m));
+                            ST(1, __popcll(certain_m));
+                            ST(13, __popcll(pruned_m));
                         }
                     }
-                    if (lane == 0) {
-                        if (found) or_wg(&Xg[id >> 6], 1ull << (id & 63));
-                        else { ST(5, 1); ST(6, nr); }
+                    unsigned long long found_m = certain_m;
+                    for (int j = 0; j < cn; j++) {
+                        if (((certain_m | pruned_m) >> j) & 1ull) continue;
+                        int id = __builtin_amdgcn_readlane(myv, j);
+                        const bool special = id < 0;
+                        if (special) id = -1 - id;
+                        bool found = false;
+                        int nr = 0;
+                        if (SPECIAL && special) {
+                            int x, y;
+                            xy_of_tile_id(id, tw, x, y);
+                            const unsigned long long sp_t0 = __builtin_amdgcn_s_memtime();
+                            found = special_hit(P, FV, id, x, y, &nr);
+                            if (lane == 0) { ST(23, __builtin_amdgcn_s_memtime() - sp_t0); ST(24, 1); }
+                            if (lane == 0) rt += (unsigned)nr;
+                        } else {
+                            const int64_t rs = P.tscan_start[id];
+                            nr = P.tnruns[id];
+                            int base = KH + P.bext;   // the first KH + bext runs were tested in phase B
+                            const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
+                            for (; base < nr && !found; base += 256) {
+                                Run rr[4];
+#pragma unroll
+                                for (int k = 0; k < 4; k++) {
+                                    const int r = base + k * 64 + lane;
+                                    if (r < nr) rr[k] = P.scan_pool[rs + r];
+                                    else rr[k].x0 = -1;
+                                }
+                                // the four tests are independent (no early-out between them), so
+                                // their LDS round trips overlap
+                                bool h4[4];
+#pragma unroll
+                                for (int k = 0; k < 4; k++) h4[k] = rr[k].x0 >= 0 && run_hits_fs(FV, rr[k]);
+                                int fpos = -1;
+#pragma unroll
+                                for (int k = 3; k >= 0; k--) {
+                                    const unsigned long long hmk = __ballot(h4[k]);
+                                    if (hmk) fpos = base + k * 64 + __ffsll((long long)hmk) - 1;
+                                }
+                                found = fpos >= 0;
+                                if (found && lane == 0) Hn[id] = (uint16_t)min(fpos, 0xFFFE);
+                            }
+                            if (lane == 0) {
+                                ST(22, __builtin_amdgcn_s_memtime() - s_t0);
+                                const unsigned long long sc = (unsigned long long)max(min(base, nr) - KH - P.bext, 0);
+                                rt += (unsigned)sc;
+                                ST(15, sc);
+                                if (found) ST(1, 1);
+                            }
+                        }
+                        if (found) found_m |= 1ull << j;
+                        else if (lane == 0) ST(6, nr);
                     }
+                    // publish the hits of the chunk (tile order: one atomic per entry that hit)
+                    if (lane < cn && ((found_m >> lane) & 1ull)) {
+                        const int id = myv < 0 ? -1 - myv : myv;
+                        or_wg(&Xg[id >> 6], 1ull << (id & 63));
+                    }
+                    if (lane == 0) ST(5, cn - __popcll(found_m));
                 }
                 if (lane == 0) ST(21, __builtin_amdgcn_s_memtime() - c_t0);
             } else {

@@ -226,6 +226,59 @@ int dmx_chunk_load(dmx_ctx* ctx, const dmx_chunk* c, const double* region, dmx_p
 /* Device graph from host node records (e.g. a graph the reference itself built or loaded). */
 int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const int32_t* bins, const int16_t* runs,
                         int64_t nruns, const uint8_t* gridconn, const float* attrs, dmx_graph** out);
+/* Merge links of the map (Point::m_merge, set by the LINK mode): n pairs (cell, partner cell), x-major
+ * indices.  dmx_chunk_load sets them from the chunk.  The searches that follow merge links in the
+ * reference (VGA global, metric, angular, and the three step depths: getMergePixel in
+ * vgavisualglobal.cpp:113-122, vgametric.cpp:97-104, vgaangular.cpp:95-102, vgametricdepth.cpp:68-82,
+ * vgaangulardepth.cpp:57-66, vgavisualglobaldepth.cpp:55-64) return DMX_ERR_UNSUPPORTED on a graph with
+ * merge links; VGA visual local has no merge logic and runs. */
+int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n);
+/* Editing a parsed chunk the way the reference edits a PointMap it read (PointMap::read then ::write,
+ * pointdata.cpp:1073-1188): columns that are not set keep their bytes (stats, display parameters,
+ * formula), point records are re-emitted with the state bits PointMap::read keeps.
+ * processed / boundary flags, points with merge links, attribute rows. */
+int dmx_chunk_flags(const dmx_chunk* c, int* processed, int* boundary, int64_t* merges, int64_t* nrows);
+/* AttributeTable::insertOrResetColumn / insertOrResetLockedColumn (attributetable.cpp:303-326) + setValue on
+ * the rows of setmask (NULL: all; values [nrows] in row = node order); make_displayed: the analysis's
+ * setDisplayedAttribute.  The chunk's dmx_chunk_column / dmx_chunk_info views are not refreshed. */
+int dmx_chunk_set_column(dmx_chunk* c, const char* name, const float* values, const uint8_t* setmask, int locked,
+                         int make_displayed);
+int dmx_chunk_set_displayed(dmx_chunk* c, int physical_column);
+int dmx_chunk_set_name(dmx_chunk* c, const char* name);
+/* PointMap::setCurSel(r, add) of the STEPDEPTH selection (runmethods.cpp:745-753): Point::SELECTED on the
+ * filled cells among `cells` (x-major indices); MetaGraph::write then saves it. */
+int dmx_chunk_select_cells(dmx_chunk* c, const int32_t* cells, int64_t n);
+/* PointMap::unmake(removeLinks) (pointdata.cpp:1343-1374): VISPREP -pu [-pl]. */
+int dmx_chunk_unmake(dmx_chunk* c, int remove_links);
+/* PointMap::write of the (edited) chunk; buf NULL or cap too small: only *size. */
+int dmx_chunk_serialize(const dmx_chunk* c, uint8_t* buf, int64_t cap, int64_t* size);
+
+/* ---- .graph file (host) ---------------------------------------------------------------------- */
+/* The MetaGraph container, METAGRAPH_VERSION 440: MetaGraph::readFromFile / readFromStream
+ * (salalib/mgraph.cpp:2475-2654) and MetaGraph::write(file, 440, false) (mgraph.cpp:2656-2757, as
+ * depthmapXcli calls it, runmethods.cpp:113,265,339,776).  Drawing layers (SpacePixelFile / ShapeMap /
+ * SalaShape, spacepixfile.cpp:28-57, shapemap.cpp:49-76,2273-2449) are parsed and re-emitted as the
+ * reference re-emits them; point maps are PointMap chunks (dmx_chunk_*); shape graphs and data maps are
+ * carried through unchanged.  Older file versions need the reference's legacy mgraph440 reader:
+ * DMX_ERR_UNSUPPORTED. */
+typedef struct dmx_graphfile dmx_graphfile;
+int dmx_graphfile_read(const char* path, dmx_graphfile** out);
+int dmx_graphfile_free(dmx_graphfile* g);
+int dmx_graphfile_write(const dmx_graphfile* g, const char* path);
+/* MetaGraph m_state / m_view_class, m_region ([4] blx, bly, trx, try), the drawing lines PointMap::blockLines
+ * reads (every shown layer, pointdata.cpp:308-320), point map count, displayed point map. */
+int dmx_graphfile_info(const dmx_graphfile* g, int32_t* state, int32_t* view_class, double* region, int64_t* nlines,
+                       int32_t* npointmaps, int32_t* displayed);
+int dmx_graphfile_lines(const dmx_graphfile* g, double* lines /* [nlines][4] */);
+int dmx_graphfile_set_view(dmx_graphfile* g, int32_t state, int32_t view_class);
+/* Point map i (the pointer stays valid until the next put on the same file). */
+int dmx_graphfile_pointmap(const dmx_graphfile* g, int i, const uint8_t** chunk, int64_t* size);
+/* Replace point map i, or (i = -1) append it and make it the displayed one (MetaGraph::addNewPointMap). */
+int dmx_graphfile_put_pointmap(dmx_graphfile* g, int i, const uint8_t* chunk, int64_t size);
+/* The name addNewPointMap gives the next map ("VGA Map", then "VGA Map 1", ...; mgraph.cpp:2791-2809). */
+int dmx_graphfile_new_pointmap_name(const dmx_graphfile* g, char* name, int cap);
+/* MetaGraph::setViewClass(SHOWVGATOP) applied to a view class (mgraph.cpp:167-177). */
+int32_t dmx_view_vga_top(int32_t view_class);
 
 #ifdef __cplusplus
 }

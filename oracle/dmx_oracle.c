@@ -782,6 +782,44 @@ int dmxo_makegraph(dmxo_map* m, double maxdist, int boundary, int64_t nb, int64_
     return 0;
 }
 
+/* bench.py cpu_baseline: makeGraph (sparkPixel2) of a sample of nodes, each on one thread, its wall
+ * time in secs[i].  The graph arrays of the map are allocated on first use (no boundary graph). */
+int dmxo_makegraph_sample(dmxo_map* m, double maxdist, const int64_t* nodes, int64_t n, int nthreads, double* secs) {
+    if (!m->blocked_lines) block_lines(m);
+    if (!m->nodes) {
+        index_nodes(m);
+        int64_t N = m->nnodes;
+        m->nodes = (NodeG*)calloc(N ? N : 1, sizeof(NodeG));
+        free(m->attrs); m->attrs = (float*)calloc((N ? N : 1) * 3, sizeof(float));
+        free(m->gridconn); m->gridconn = (uint8_t*)calloc(N ? N : 1, 1);
+    }
+    for (int64_t i = 0; i < n; i++)
+        if (nodes[i] < 0 || nodes[i] >= m->nnodes) return -1;
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        Work w;
+        memset(&w, 0, sizeof(w));
+        w.sv.capg = 64; w.sv.gaps = (Zone*)malloc(64 * sizeof(Zone));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 1)
+#endif
+        for (int64_t i = 0; i < n; i++) {
+            const int64_t k = nodes[i];
+            const double t0 = omp_get_wtime();
+            free(m->nodes[k].runs);
+            memset(&m->nodes[k], 0, sizeof(NodeG));
+            int32_t c = m->node_cell[k];
+            spark_pixel(m, &w, (int)(c / m->rows), (int)(c % m->rows), maxdist, &m->nodes[k], &m->attrs[3 * k]);
+            secs[i] = omp_get_wtime() - t0;
+        }
+        free_work(&w);
+    }
+    return 0;
+}
+
 int64_t dmxo_num_nodes(const dmxo_map* m) { return m->nnodes; }
 int64_t dmxo_num_runs(const dmxo_map* m) {
     int64_t r = 0;
@@ -1447,6 +1485,24 @@ int dmxo_vga_local(dmxo_map* m, int gates_only, int64_t nb, int64_t ne, int nthr
             for (int64_t i = 0; i < ntot; i++) intotal[total[i]] = 0;
         }
         free(inhood); free(intotal); free(hood); free(total);
+    }
+    return 0;
+}
+
+/* bench.py cpu_baseline: VGA global BFS of a sample of source nodes, each on one thread (the graph must
+ * be set: dmxo_set_graph), its wall time in secs[i]; out [N][7] rows of the sample. */
+int dmxo_vga_global_sample(dmxo_map* m, double radius, const int64_t* nodes, int64_t n, int nthreads, float* out,
+                           double* secs) {
+    for (int64_t i = 0; i < n; i++)
+        if (nodes[i] < 0 || nodes[i] >= m->nnodes) return -1;
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < n; i++) {
+        const double t0 = omp_get_wtime();
+        dmxo_vga_global(m, radius, 0, nodes[i], nodes[i] + 1, 1, out, NULL);
+        secs[i] = omp_get_wtime() - t0;
     }
     return 0;
 }

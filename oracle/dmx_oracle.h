@@ -78,6 +78,11 @@ int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
  * -1 for skipped sources (context-filled odd cells, gates_only) and for neighbourhoods of <= 1 cell;
  * rows outside the range untouched. */
 int dmxo_vga_local(dmxo_map* m, int gates_only, int64_t node_begin, int64_t node_end, int nthreads, float* out);
+/* CPU-baseline sampling (bench.py): makeGraph / VGA global for a list of nodes, one node per thread,
+ * per-node wall seconds in secs[n]. */
+int dmxo_makegraph_sample(dmxo_map* m, double maxdist, const int64_t* nodes, int64_t n, int nthreads, double* secs);
+int dmxo_vga_global_sample(dmxo_map* m, double radius, const int64_t* nodes, int64_t n, int nthreads, float* out,
+                           double* secs);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,10 @@ def lib():
         L.dmxo_vga_local.argtypes = [vp, i32, i64, i64, i32, vp]
         L.dmxo_vga_global.restype = i32
         L.dmxo_vga_global.argtypes = [vp, dbl, i32, i64, i64, i32, vp, vp]
+        L.dmxo_makegraph_sample.restype = i32
+        L.dmxo_makegraph_sample.argtypes = [vp, dbl, vp, i64, i32, vp]
+        L.dmxo_vga_global_sample.restype = i32
+        L.dmxo_vga_global_sample.argtypes = [vp, dbl, vp, i64, i32, vp, vp]
         _lib = L
     return _lib
 
@@ -175,3 +179,21 @@ class OracleMap:
         out = np.full(self.num_nodes, -1.0, dtype=np.float32)
         lib().dmxo_angular_stepdepth(self.h, _p(sel), len(sel), _p(out))
         return out
+
+    def make_graph_sample(self, nodes, maxdist=-1.0, threads=1):
+        """sparkPixel2 for each listed node (one node per thread); per-node seconds."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.int64)
+        secs = np.zeros(len(nodes))
+        if lib().dmxo_makegraph_sample(self.h, float(maxdist), _p(nodes), len(nodes), int(threads), _p(secs)):
+            raise ValueError("node out of range")
+        return secs
+
+    def vga_global_sample(self, nodes, radius=-1.0, threads=1):
+        """VGA global BFS from each listed source (one source per thread): ([N][7] rows, per-source seconds)."""
+        nodes = np.ascontiguousarray(nodes, dtype=np.int64)
+        out = np.full((self.num_nodes, 7), -1.0, dtype=np.float32)
+        secs = np.zeros(len(nodes))
+        if lib().dmxo_vga_global_sample(self.h, float(radius), _p(nodes), len(nodes), int(threads), _p(out), _p(secs)):
+            raise ValueError("node out of range")
+        return out, secs
+

@@ -52,7 +52,8 @@ for k, v in configs:
                       "topdown_cycles_per_src": st["vga_topdown_cycles"] / nsrc,
                       "b_tiles_per_src": st["vga_b_tiles"] / nsrc, "b_cells_per_src": st["vga_b_cells"] / nsrc,
                       "tt_tiles_per_src": st["vga_tt_tiles"] / nsrc, "tt_pruned_per_src": st["vga_tt_pruned"] / nsrc,
-                      "b1_cycles_per_src": st["vga_b1_cycles"] / nsrc,
+                      "b_row_cycles_per_src": st["vga_b_row_cycles"] / nsrc, "b_cell_tiles_per_src": st["vga_b_cell_tiles"] / nsrc,
+                      "b_cell_cycles_per_src": st["vga_b_cell_cycles"] / nsrc, "b_ext_cells_per_src": st["vga_b_ext_cells"] / nsrc,
                       "c_busy_per_src": st["vga_c_busy"] / nsrc, "c_scan_per_src": st["vga_c_scan"] / nsrc,
                       "c_spec_per_src": st["vga_c_spec"] / nsrc, "n_spec_per_src": st["vga_n_spec"] / nsrc,
                       "levels_bu_per_src": st["vga_bottom_up_levels"] / nsrc, "kernel": st["vga_kernel"], "special_nodes": st["vga_special_nodes"],

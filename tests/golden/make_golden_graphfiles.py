@@ -1,0 +1,132 @@
+"""Generate the .graph regression fixtures under tests/golden/graphfiles/ from the REAL reference.
+
+Runs oracle/_ref/ref_cli (our replay of depthmapXcli's runVisualPrep / runVga / runStepDepth on the
+reference library built from /root/reference by oracle/Makefile) on the reference's own test inputs
+(/root/reference/testdata, the files its RegressionTest cases use, regressionconfig.json) and stores:
+  inputs/<file>.graph.xz     the reference's input files (data), xz-compressed
+  cases.json                 per case: the command, sha256 + size of the reference's output .graph, the
+                             analysis columns, and the sha256 of the output with those columns' values
+                             and stats zeroed (graphfile_util.masked_digest)
+  <case>_cols.npz            the analysis columns of the reference's output (float32 per attribute row)
+The regression runner's check is a byte compare of the output files (RegressionTest/depthmaprunner.py:
+72-75); the tests apply it, and where GPU floating-point columns may differ in the last bits they fall
+back to the masked compare plus the north-star tolerance on the columns.
+
+Run in this container only (it needs oracle/_ref/ref_cli):  python tests/golden/make_golden_graphfiles.py
+"""
+import hashlib
+import json
+import lzma
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(HERE))
+import graphfile_util as gu  # noqa: E402
+
+TESTDATA = "/root/reference/testdata"
+REF_CLI = os.path.join(REPO, "oracle", "_ref", "ref_cli")
+OUT = os.path.join(HERE, "graphfiles")
+
+INPUTS = ["gallery_empty.graph", "gallery_connected.graph", "turns_connected.graph", "rect1x1.graph",
+          "barnsbury_drawing.graph", "polygons_drawing.graph"]
+
+VGA_VIS = ["Visual Entropy", "Visual Integration [HH]", "Visual Integration [P-value]", "Visual Integration [Tekl]",
+           "Visual Mean Depth", "Visual Node Count", "Visual Relativised Entropy"]
+MK = ["Connectivity", "Point First Moment", "Point Second Moment"]
+
+# name, input (testdata file or "@case" = an earlier case's output), mode + args, analysis columns,
+# GPU needed, regression case it mirrors (RegressionTest/regressionconfig.json)
+CASES = [
+    ("dense_fill", "rect1x1.graph", ["-m", "VISPREP", "-pg", "0.02", "-pp", "0.5,0.5"], [], False,
+     "dense_pointmap_create_fill_make"),
+    ("gallery_grid", "gallery_empty.graph", ["-m", "VISPREP", "-pg", "0.04"], [], False,
+     "pointmap_create_fill_make_unmake step 1"),
+    ("gallery_fill", "@gallery_grid", ["-m", "VISPREP", "-pp", "1.32,7.24,4.88,5.24"], [], False,
+     "pointmap_create_fill_make_unmake step 2"),
+    ("gallery_make", "@gallery_fill", ["-m", "VISPREP", "-pm"], [], True, "pointmap_create_fill_make_unmake step 3"),
+    ("gallery_unmake", "@gallery_make", ["-m", "VISPREP", "-pu"], [], False, "pointmap_create_fill_make_unmake step 4"),
+    ("gallery_one_op", "gallery_empty.graph", ["-m", "VISPREP", "-pg", "0.04", "-pp", "1.32,7.24,4.88,5.24", "-pm"], [],
+     True, "pointmap_create_fill_make_one_operation"),
+    ("gallery_boundary", "gallery_empty.graph", ["-m", "VISPREP", "-pg", "0.04", "-pp", "1.32,7.24", "-pm", "-pb"], [],
+     True, "(-pb boundary graph)"),
+    ("gallery_maxdist", "gallery_empty.graph", ["-m", "VISPREP", "-pg", "0.04", "-pp", "1.32,7.24", "-pm", "-pr", "1.5"],
+     [], True, "(-pr restricted visibility)"),
+    ("barnsbury_make", "barnsbury_drawing.graph", ["-m", "VISPREP", "-pg", "2", "-pp", "531000,184000", "-pm"], [], True,
+     "BASELINE configs[0] VISPREP"),
+    ("barnsbury_vga", "@barnsbury_make", ["-m", "VGA", "-vm", "visibility", "-vg", "-vr", "n"], VGA_VIS, True,
+     "BASELINE configs[0] VGA"),
+    # the analyses on the gallery map made above (no merge links)
+    ("vis_global_n", "@gallery_one_op", ["-m", "VGA", "-vm", "visibility", "-vg", "-vr", "n"], VGA_VIS, True,
+     "visibility_global_n (on the made gallery map)"),
+    ("vis_global_3", "@gallery_one_op", ["-m", "VGA", "-vm", "visibility", "-vg", "-vr", "3"],
+     [c + " R3" for c in VGA_VIS], True, "visibility_global_3 (on the made gallery map)"),
+    ("vis_global_simple", "@gallery_one_op", ["-s", "-m", "VGA", "-vm", "visibility", "-vg", "-vr", "n"],
+     ["Visual Integration [HH]"], True, "(-s simple mode)"),
+    ("sd_visual", "@gallery_one_op", ["-m", "STEPDEPTH", "-sdt", "visual", "-sdp", "3,5"], ["Visual Step Depth"],
+     True, "vga_visual_step_depth (on the made gallery map)"),
+    ("sd_metric", "@gallery_one_op", ["-m", "STEPDEPTH", "-sdt", "metric", "-sdp", "3,5"],
+     ["Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length", "Metric Straight-Line Distance"], True,
+     "vga_metric_step_depth (on the made gallery map)"),
+    ("sd_angular", "@gallery_one_op", ["-m", "STEPDEPTH", "-sdt", "angular", "-sdp", "3,5"],
+     ["Angular Step Depth"], True, "vga_angular_step_depth (on the made gallery map)"),
+    # turns_connected without its merge links: VISPREP -pu -pl, then -pm
+    ("turns_unlink", "turns_connected.graph", ["-m", "VISPREP", "-pu", "-pl"], [], False, "(-pu -pl unmake + unlink)"),
+    ("turns_remake", "@turns_unlink", ["-m", "VISPREP", "-pm"], [], True, "(remake after unlink)"),
+    ("vga_metric", "@turns_remake", ["-m", "VGA", "-vm", "metric", "-vr", "n"],
+     ["Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance", "Metric Mean Straight-Line Distance",
+      "Metric Node Count"], True, "vga_metric (turns map without merge links)"),
+    ("vga_angular", "@turns_remake", ["-m", "VGA", "-vm", "angular"],
+     ["Angular Mean Depth", "Angular Total Depth", "Angular Node Count"], True, "vga_angular (turns map without merge "
+                                                                              "links)"),
+    # the regression inputs with merge links (LINK mode): VGA visual local has no merge logic and runs; the
+    # searches that follow merge links are refused (dmx.h, dmx_graph_set_merges)
+    ("vis_local", "gallery_connected.graph", ["-m", "VGA", "-vm", "visibility", "-vl"],
+     ["Visual Clustering Coefficient", "Visual Control", "Visual Controllability"], True, "visibility_local"),
+    ("merge_vis_global_n", "gallery_connected.graph", ["-m", "VGA", "-vm", "visibility", "-vg", "-vr", "n"], VGA_VIS,
+     True, "visibility_global_n (merge links: refused)"),
+    ("merge_sd_metric", "gallery_connected.graph", ["-m", "STEPDEPTH", "-sdt", "metric", "-sdp", "3,5"],
+     ["Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length", "Metric Straight-Line Distance"], True,
+     "vga_metric_step_depth (merge links: refused)"),
+    ("merge_vga_metric", "turns_connected.graph", ["-m", "VGA", "-vm", "metric", "-vr", "n"],
+     ["Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance", "Metric Mean Straight-Line Distance",
+      "Metric Node Count"], True, "vga_metric (merge links: refused)"),
+]
+
+
+def main():
+    os.makedirs(os.path.join(OUT, "inputs"), exist_ok=True)
+    for f in INPUTS:
+        with open(os.path.join(TESTDATA, f), "rb") as src, lzma.open(os.path.join(OUT, "inputs", f + ".xz"), "wb",
+                                                                     preset=9) as dst:
+            shutil.copyfileobj(src, dst)
+    meta = {}
+    outputs = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, inp, args, cols, gpu, regression in CASES:
+            src = outputs[inp[1:]] if inp.startswith("@") else os.path.join(TESTDATA, inp)
+            dst = os.path.join(tmp, name + ".graph")
+            subprocess.check_call([REF_CLI, "-f", src, "-o", dst] + args, stdout=subprocess.DEVNULL)
+            outputs[name] = dst
+            b = open(dst, "rb").read()
+            m = {"input": inp, "args": args, "gpu": gpu, "regression": regression, "size": len(b),
+                 "sha256": hashlib.sha256(b).hexdigest(), "columns": cols, "refused": name.startswith("merge_")}
+            if cols:
+                m["masked_sha256"] = gu.masked_digest(b, cols)
+                got = gu.columns(b, cols)
+                assert sorted(got) == sorted(cols), (name, sorted(got))
+                np.savez_compressed(os.path.join(OUT, name + "_cols.npz"), **got)
+            meta[name] = m
+            print(name, len(b), m["sha256"][:16])
+    with open(os.path.join(OUT, "cases.json"), "w") as f:
+        json.dump(meta, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+"""Test-side reader of depthmapX .graph files (METAGRAPH_VERSION 440), used to compare the CLI's output
+files with the reference's where floating-point analysis columns may differ in the last bits.
+
+It locates, in the displayed point map, the attribute columns and their per-row values, so that a test
+can compare everything else byte for byte (`masked_digest`) and the analysis columns within the
+north-star tolerance (`columns`).  Layout: MetaGraph::write (salalib/mgraph.cpp:2656-2757), ShapeMap::write
+(shapemap.cpp:2385-2449), PointMap::write (pointdata.cpp:1158-1188), AttributeTable::write
+(attributetable.cpp:427-456).  Test infrastructure only.
+"""
+import hashlib
+import struct
+
+import numpy as np
+
+
+class _R:
+    def __init__(self, b, o=0):
+        self.b, self.o = b, o
+
+    def get(self, fmt):
+        v = struct.unpack_from("<" + fmt, self.b, self.o)
+        self.o += struct.calcsize("<" + fmt)
+        return v if len(v) > 1 else v[0]
+
+    def skip_n(self, unit):
+        """Skip a u32 count followed by count * unit bytes."""
+        n = self.get("I")
+        self.o += unit * n
+
+    def str(self):
+        n = self.get("I")
+        s = self.b[self.o:self.o + n].decode("latin1")
+        self.o += n
+        return s
+
+
+def _skip_table(r):
+    r.get("qq")
+    for _ in range(r.get("i")):
+        r.get("q")
+        r.str()
+    cols = []
+    for _ in range(r.get("i")):
+        name = r.str()
+        stats_at = r.o
+        r.o += 4 + 4 + 8
+        phys = r.get("i")
+        r.o += 2 + 12
+        r.str()
+        cols.append((name, stats_at, phys))
+    rows = []
+    for _ in range(r.get("i")):
+        r.o += 12
+        k = r.get("I")
+        rows.append((r.o, k))
+        r.o += 4 * k
+    r.o += 12
+    return cols, rows
+
+
+def _skip_layer(r):
+    r.str()
+    r.o += 4 + 2 + 32 + 16
+    for _ in range(r.get("i")):
+        r.o += 4 + 1 + 40 + 32
+        r.skip_n(16)
+    for _ in range(r.get("i")):
+        r.get("i")
+        r.skip_n(4)
+    _skip_table(r)
+    r.o += 4
+    for _ in range(r.get("i")):
+        r.skip_n(4)
+        r.o += 4
+        for _ in range(2):
+            r.skip_n(12)
+    for _ in range(2):
+        r.skip_n(8)
+    if r.b[r.o:r.o + 1] == b"m":
+        r.o += 1
+        r.str()
+        r.str()
+        r.o += 1
+        r.str()
+        r.str()
+        r.str()
+    else:
+        r.o += 1
+
+
+def parse(buf):
+    """Header fields and, for the displayed point map: name, columns [(name, stats_offset, physical)],
+    row value offsets [(offset, n)]."""
+    assert buf[:3] == b"grf"
+    r = _R(buf, 3)
+    version, state, view = r.get("iii")
+    r.o += 2
+    t = buf[r.o:r.o + 1]
+    r.o += 1
+    out = {"version": version, "state": state, "view_class": view, "maps": []}
+    if t == b"x":
+        out["props"] = [r.str() for _ in range(7)]
+        t = buf[r.o:r.o + 1]
+        r.o += 1
+    if t == b"l":
+        r.str()
+        r.o += 32
+        for _ in range(r.get("i")):
+            r.str()
+            r.o += 32
+            for _ in range(r.get("i")):
+                _skip_layer(r)
+        t = buf[r.o:r.o + 1]
+        r.o += 1
+    if t == b"p":
+        out["displayed"], n = r.get("ii")
+        for _ in range(n):
+            start = r.o
+            name = r.str()
+            r.o += 8
+            rows, cols_, filled = r.get("iii")
+            r.o += 16
+            disp = r.get("i")
+            cols, rows_at = _skip_table(r)
+            out["maps"].append({"name": name, "start": start, "displayed_sorted": disp, "columns": cols,
+                                "rows": rows_at, "grid": (cols_, rows)})
+            break   # the files under test keep one point map; later maps are not located
+    return out
+
+
+def columns(buf, names):
+    """{name: float32[nrows]} of the displayed (first) point map's columns with these names."""
+    p = parse(buf)
+    m = p["maps"][0]
+    out = {}
+    for name, _, phys in m["columns"]:
+        if name in names:
+            out[name] = np.array([struct.unpack_from("<f", buf, o + 4 * phys)[0] for o, _ in m["rows"]],
+                                 dtype=np.float32)
+    return out
+
+
+def masked_digest(buf, names):
+    """sha256 of the file with the stats and row values of the named columns zeroed."""
+    p = parse(buf)
+    b = bytearray(buf)
+    if p["maps"]:
+        m = p["maps"][0]
+        for name, stats_at, phys in m["columns"]:
+            if name in names:
+                b[stats_at:stats_at + 16] = bytes(16)
+                for o, _ in m["rows"]:
+                    b[o + 4 * phys:o + 4 * phys + 4] = bytes(4)
+    return hashlib.sha256(bytes(b)).hexdigest()
+
+
+def column_names(buf):
+    p = parse(buf)
+    return [c[0] for c in p["maps"][0]["columns"]] if p["maps"] else []

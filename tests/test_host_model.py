@@ -22,7 +22,7 @@ def built():
 
 def test_library_exports_every_declared_symbol():
     hdr = open(os.path.join(REPO, "include", "dmx.h")).read()
-    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(dmx_\w+)\s*\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:int|int32_t|const char\*)\s+(dmx_\w+)\s*\(", hdr, re.M))
     assert declared and declared == set(_native.SIGNATURES)
     L = _native.lib()
     for name in declared:
