@@ -83,20 +83,32 @@ BlockCache& block_cache() {
     static BlockCache* c = new BlockCache();   // never destroyed: frees at exit would race the runtime
     return *c;
 }
+// free device memory plus the blocks the cache would release on an allocation failure
+size_t cached_bytes() {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.m);
+    return c.cached;
+}
 hipError_t cached_malloc(void** p, size_t bytes) {
     BlockCache& c = block_cache();
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (bytes >= BlockCache::kMin) {
-        std::lock_guard<std::mutex> g(c.m);
-        auto it = c.free_blocks.lower_bound({dev, bytes});
-        if (it != c.free_blocks.end() && it->first.first == dev && it->first.second - it->first.second / 8 <= bytes) {
-            *p = it->second;
-            c.cached -= it->first.second;
-            c.live[*p] = it->first;
-            c.free_blocks.erase(it);
-            return hipSuccess;
+        bool hit = false;
+        {
+            std::lock_guard<std::mutex> g(c.m);
+            auto it = c.free_blocks.lower_bound({dev, bytes});
+            if (it != c.free_blocks.end() && it->first.first == dev && it->first.second - it->first.second / 8 <= bytes) {
+                *p = it->second;
+                c.cached -= it->first.second;
+                c.live[*p] = it->first;
+                c.free_blocks.erase(it);
+                hit = true;
+            }
         }
+        // a cached block may have been freed by another context while kernels on its stream still used
+        // it: wait for the device before handing it out again (what hipFree would have done)
+        if (hit) return hipDeviceSynchronize();
     }
     hipError_t e = hipMalloc(p, bytes);
     if (e != hipSuccess) {
@@ -306,8 +318,7 @@ size_t makegraph_lds(int gcap, int bcap, int D) {
     b += 4 * 32 * 3 + 4 * 32;                        // binc, bfar, bnr, misc
     b += 16 * (size_t)bcap;                          // bsorted
     b += 4 * (size_t)gcap + 8 * (size_t)gcap + 4 * (size_t)bcap + 4 * ((size_t)gcap + 4);
-    b += 4 * ((size_t)D + 4);
-    b += 2 * (3 * ((size_t)D + 1) + 2);
+    b += 4 * ((size_t)D + 4);   // open-run state per row (the run counters live in HBM scratch)
     return (b + 15) & ~(size_t)15;
 }
 
@@ -426,6 +437,21 @@ int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, i
     return DMX_OK;
 }
 
+// makeGraph kernel variant: VGPR budget (waves per SIMD) chosen at launch (DMX_MK_WPE, default 5).
+// The kernel is latency-bound (one wave walks one source's sieve depth by depth), so waves beat
+// registers: at 1000^2, 3 waves/SIMD 6.9 s, 4: 5.7 s, 5: 5.3 s (96 VGPRs, some spills), 6: 5.4 s.
+typedef void (*mk_kernel_t)(MakeGraphParams);
+static mk_kernel_t mk_kernel() {
+    const char* e = getenv("DMX_MK_WPE");
+    const int w = e ? atoi(e) : 5;
+    const bool prof = verbose() != 0;
+    if (w >= 8) return prof ? makegraph_kernel<8, true> : makegraph_kernel<8, false>;
+    if (w >= 6) return prof ? makegraph_kernel<6, true> : makegraph_kernel<6, false>;
+    if (w == 5) return prof ? makegraph_kernel<5, true> : makegraph_kernel<5, false>;
+    if (w == 4) return prof ? makegraph_kernel<4, true> : makegraph_kernel<4, false>;
+    return prof ? makegraph_kernel<3, true> : makegraph_kernel<3, false>;
+}
+
 int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int64_t node_begin, int64_t node_end,
                   dmx_graph** out) {
     if (!ctx || !pm || !out) return fail(DMX_ERR_ARG, "bad arguments");
@@ -457,7 +483,10 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     HIPCHK(g->gridconn.alloc(std::max<int64_t>(n, 1)));
 
     // capacities (retried on overflow)
-    int gcap = 64, bcap = 64;   // (10 waves per CU; larger lists spill to HBM or retry)
+    // LDS gap / block lists: small lists keep the per-wave LDS near 12 KB at 1000^2 (13 waves per CU
+    // instead of 10 with 64-entry lists: 8.27 s -> 6.6 s); longer block lists spill to HBM, longer gap
+    // lists re-run the source with larger capacities
+    int gcap = 16, bcap = 32;
     int spill_cap = 4096;      // per-wave HBM blocks past bcap
     int64_t capB = 32 * (int64_t)D + 2048;
     if (const char* e = getenv("DMX_MK_GCAP")) gcap = std::max(2, atoi(e));   // test hooks for the retry path
@@ -479,11 +508,12 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), ctx->stream));
         size_t lds0 = makegraph_lds(gcap, bcap, D);
         int occ0 = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, makegraph_kernel, 64, lds0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, mk_kernel(), 64, lds0));
         {
             const int64_t waves0 = std::min<int64_t>((int64_t)ctx->num_cu * std::max(occ0, 1), std::max<int64_t>(n, 1));
             const size_t stage0 = (size_t)waves0 * (capB * 16 + (3 * ((size_t)D + 1) + 4) * 4) * 4;   // headroom for retries
             HIPCHK(hipMemGetInfo(&free_b, &total_b));
+            free_b += cached_bytes();   // released by cached_malloc if the fresh allocation needs them
             const size_t pool_bytes_max = free_b > stage0 + (1ull << 30) ? (free_b - stage0 - (1ull << 30)) : 0;
             if ((size_t)pool_cap * sizeof(Run) > pool_bytes_max) pool_cap = (int64_t)(pool_bytes_max / sizeof(Run));
             if (pool_cap <= 0) return fail(DMX_ERR_HIP, "not enough device memory for the run pool");
@@ -495,17 +525,19 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             size_t lds = makegraph_lds(gcap, bcap, D);
             if (lds > 160 * 1024) return fail(DMX_ERR_CAPACITY, "makegraph LDS requirement exceeds 160 KiB");
             int occ = 0;
-            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, makegraph_kernel, 64, lds));
+            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mk_kernel(), 64, lds));
             if (occ < 1) occ = 1;
             const int64_t todo = list_n < 0 ? n : list_n;
             const int64_t waves = std::min<int64_t>((int64_t)ctx->num_cu * occ, std::max<int64_t>(todo, 1));
             const int64_t capA = capB;
             DevBuf<unsigned long long> stA;
             DevBuf<Run> stB;
-            DevBuf<uint32_t> pref;
+            DevBuf<uint32_t> pref, rcnt;
             HIPCHK(stA.alloc((size_t)waves * capA));
             HIPCHK(stB.alloc((size_t)waves * capB));
             HIPCHK(pref.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
+            HIPCHK(rcnt.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
+            HIPCHK(hipMemsetAsync(rcnt.p, 0, (size_t)waves * (3 * ((size_t)D + 1) + 4) * 4, ctx->stream));
             DevBuf<double2> bsp;
             DevBuf<int> bspf;
             HIPCHK(bsp.alloc((size_t)waves * 2 * spill_cap));
@@ -525,7 +557,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.pool_capacity = pool_cap; P.pool = g->pool.p;
             P.node_run_start = g->node_run_start.p; P.bin_nruns = g->bin_nruns.p; P.bin_count = g->bin_count.p;
             P.bin_dist = g->bin_dist.p; P.attrs = g->attrs.p;
-            P.stageA = stA.p; P.stageB = stB.p; P.prefix = pref.p;
+            P.stageA = stA.p; P.stageB = stB.p; P.prefix = pref.p; P.runcnt = rcnt.p;
             P.capA = (int)capA; P.capB = (int)capB; P.gcap = gcap; P.bcap = bcap; P.dmax = D;
             P.bspill = bsp.p; P.bspill_flag = bspf.p; P.spill_cap = spill_cap;
             P.stats = ctx->stats.p;
@@ -538,7 +570,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.exact_moments = (list_n >= 0 || getenv("DMX_MK_EXACT")) ? 1 : 0;
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
-                hipLaunchKernelGGL(makegraph_kernel, dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
+                hipLaunchKernelGGL(mk_kernel(), dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
                 HIPCHK(hipGetLastError());
             }
             HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));

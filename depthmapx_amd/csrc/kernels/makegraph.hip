@@ -41,6 +41,7 @@ struct MakeGraphParams {
     unsigned long long* stageA;  // per wave: capA packed emission records
     Run* stageB;               // per wave: capB runs (canonical octant segments)
     uint32_t* prefix;          // per wave: 3*(D+1)+2 counts/prefix
+    uint32_t* runcnt;          // per wave: 3*(D+1)+1 runs per (slot, row) of the octant (zero between octants)
     int capA, capB;
     int gcap, bcap;            // LDS gap / block capacities
     double2* bspill;           // per wave: [2][spill_cap] blocks past bcap (raw, sorted)
@@ -61,7 +62,7 @@ struct MakeGraphParams {
 
 // phase clocks (profile builds of a run only; wave-uniform scalar reads)
 #define MK_T(i)                                                           \
-    if (P.profile) {                                                      \
+    if (PROF) {                                                           \
         const unsigned long long n_ = __builtin_amdgcn_s_memtime();       \
         cyc[i] += n_ - tmark;                                             \
         tmark = n_;                                                       \
@@ -181,6 +182,10 @@ __device__ __forceinline__ Run make_run(int q, int cx, int cy, int ind, int ds, 
     return r;
 }
 
+// per-wave counters in HBM scratch, read and written through L2 (a wave reads back its own stores)
+__device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ void st_l2(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
 // open-run state per row: valid(1) | slot(2) | start(14) | last(14)
 __device__ __forceinline__ uint32_t pack_open(int slot, int s, int l) {
     return 1u | ((uint32_t)slot << 1) | ((uint32_t)s << 3) | ((uint32_t)l << 17);
@@ -235,7 +240,6 @@ struct Lds {
     int2* gc;         // [gcap] centregap ind range per gap: ceil(fl(start*depth)), floor(fl(end*depth))
     int* gpre;        // [gcap+1] exclusive prefix of visited counts
     uint32_t* openr;  // [dmax+2]
-    uint16_t* cnt;    // [3*(dmax+1)]
     unsigned* binc;   // [32] node counts per bin
     unsigned* bfar;   // [32] far distance (float bits)
     int* bnr;         // [32] runs per bin
@@ -244,7 +248,10 @@ struct Lds {
     int* bflag;       // [bcap] first-occurrence flags
 };
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) makegraph_kernel(MakeGraphParams P) {
+// WPE: waves per SIMD the register allocation targets; PROF: per-phase clocks (DMX_VERBOSE builds of
+// a run) -- a template flag so that the 8 clock counters cost no registers otherwise
+template <int WPE, bool PROF>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) makegraph_kernel(MakeGraphParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int gcap = P.gcap, bcap = P.bcap, D = P.dmax;
@@ -264,7 +271,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
         L.bflag = (int*)p; p += 4 * bcap;
         L.gpre = (int*)p; p += 4 * (gcap + 4);
         L.openr = (uint32_t*)p; p += 4 * (D + 4);
-        L.cnt = (uint16_t*)p;
     }
     const int wave_global = blockIdx.x;
     unsigned long long* stA = P.stageA + (size_t)wave_global * P.capA;
@@ -287,17 +293,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
     };
     auto get_sorted = [&](int i) -> double2 { return i < bcap ? L.bsorted[i] : spill[P.spill_cap + i - bcap]; };
     uint32_t* pref = P.prefix + (size_t)wave_global * (3 * (D + 1) + 4);
+    uint32_t* rcnt = P.runcnt + (size_t)wave_global * (3 * (D + 1) + 4);   // zeroed by the host
     const double sp = P.spacing;
 
     // LDS state that persists across sources is reset here once
-    const int AX = 3 * (D + 1); // cnt[AX] counts the runs of the axis row (ind 0)
+    const int AX = 3 * (D + 1); // rcnt[AX] counts the runs of the axis row (ind 0)
     for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
-    for (int i = lane; i <= AX; i += 64) L.cnt[i] = 0;
     __syncthreads();
     // 0 depth-0 + collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible: bins,
     // 4 visible: serial moments, 5 visible: run tracking, 6 octant flush + placement, 7 publish
     unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tmark = P.profile ? __builtin_amdgcn_s_memtime() : 0;
+    unsigned long long tmark = PROF ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
         int s_idx = 0;
@@ -375,9 +381,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                 }
             }
             int depth = 0;
+            // cell word of candidate t = lane of the next depth, loaded while this depth finishes: the
+            // next depth's candidates are known before its collectgarbage, and they stay the same
+            // when that adds no block (nb == 0: the gap list is unchanged)
+            uint32_t pf_w = 0;
+            bool pf_ok = false;
             for (;;) {
                 // ---------------- collectgarbage (sparksieve2.cpp:89-132) for the previous depth
                 int nb = L.misc[1];
+                if (nb > 0) pf_ok = false;
                 if (nb > bcap + P.spill_cap) { failed = true; if (lane == 0) atomicOr(P.error, KERR_BLOCK_CAPACITY); }
                 if (failed) break;
                 if (nb > 0 && nb <= 64 && nb <= bcap && ng <= 64) {
@@ -593,7 +605,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                     }
                     if (ingrid) {
                         const int hc = hx * P.rows + hy;
-                        w = P.cellw[hc];
+                        w = (pf_ok && t0 == 0) ? pf_w : P.cellw[hc];
                         const int nl = cell_nseg(w), off = cell_seg_off(w);
                         // (double)ind >= start*depth && (double)ind <= end*depth, on the integer
                         // bounds of the two FP64 products (computed once per gap and depth)
@@ -692,12 +704,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                                 if ((o & 1u) && oslot == slot && ol == depth - 1) {
                                     L.openr[ind] = pack_open(slot, os, depth);
                                 } else {
-                                    if (o & 1u) {
-                                        const int ci = (oslot == 3) ? AX : oslot * (D + 1) + ind;
-                                        const int k = L.cnt[ci];
-                                        L.cnt[ci] = (uint16_t)(k + 1);
+                                    if (o & 1u) {   // the rank within (slot, row) is set after the octant
                                         emit = true;
-                                        rec = pack_emit(oslot, ind, os, ol, k);
+                                        rec = pack_emit(oslot, ind, os, ol, 0);
                                     }
                                     L.openr[ind] = pack_open(slot, depth, depth);
                                 }
@@ -724,6 +733,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                 if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
                 if (!hasgaps) break;      // sieve2 returned false (pointdata.cpp:1458)
                 dq = depth;
+                // prefetch: candidate t = lane of depth + 1 under the current gap list (few-gap case)
+                pf_ok = false;
+                if (ng <= 8 && !failed) {
+                    const int d1 = depth + 1;
+                    int F1 = 0, T1 = 0, pind = -1;
+                    for (int g = 0; g < ng; g++) {
+                        const double2 z = L.gaps[g];
+                        const int lo = (int)ceil(z.x * (d1 - 0.5) - 0.5);
+                        const int hi = (int)floor(z.y * (d1 + 0.5) + 0.5);
+                        const int b = min(hi, d1);
+                        const int a = max(lo, F1);
+                        const int c = (b >= a) ? (b - a + 1) : 0;
+                        if (lane >= T1 && lane < T1 + c) pind = a + (lane - T1);
+                        T1 += c;
+                        if (b >= lo) F1 = max(F1, b);
+                    }
+                    if (pind >= 0) {
+                        int px, py;
+                        octant_cell(q, cx, cy, d1, pind, px, py);
+                        if (px >= 0 && px < P.cols && py >= 0 && py < P.rows) pf_w = P.cellw[px * P.rows + py];
+                    }
+                    pf_ok = true;
+                }
                 __syncthreads();
             }
             if (failed) break;
@@ -737,11 +769,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                     uint32_t o = L.openr[ind];
                     if (o & 1u) {
                         int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
-                        const int ci = (oslot == 3) ? AX : oslot * (D + 1) + ind;
-                        const int k = L.cnt[ci];
-                        L.cnt[ci] = (uint16_t)(k + 1);
                         emit = true;
-                        rec = pack_emit(oslot, ind, os, ol, k);
+                        rec = pack_emit(oslot, ind, os, ol, 0);
                     }
                     L.openr[ind] = 0;
                 }
@@ -754,6 +783,36 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
             }
             if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); break; }
             __syncthreads();
+            // ranks within (slot, row): the runs of one row and slot are staged in depth order, so a
+            // record's rank is the number of earlier records with its key (earlier chunks: the running
+            // count in rcnt; this chunk: earlier lanes with the same key)
+            for (int base = 0; base < nA; base += 64) {
+                const int i = base + lane;
+                unsigned long long rec = 0;
+                int key = -1;
+                if (i < nA) {
+                    rec = stA[i];
+                    const int slot = (int)(rec & 3ull), ind = (int)((rec >> 2) & 0x3fff);
+                    key = (slot == 3) ? AX : slot * (D + 1) + ind;
+                }
+                int r = 0;
+                bool last = true;
+                const int n = min(64, nA - base);
+                for (int j = 0; j < n; j++) {
+                    const int kj = __builtin_amdgcn_readlane(key, j);
+                    if (kj == key) {
+                        if (j < lane) r++;
+                        else if (j > lane) last = false;
+                    }
+                }
+                if (key >= 0) {
+                    const uint32_t k = ld_l2(&rcnt[key]) + (uint32_t)r;
+                    stA[i] = rec | ((unsigned long long)k << 44);
+                    if (last) st_l2(&rcnt[key], k + 1);
+                }
+                __syncthreads();   // the next chunk reads these counters (other lanes, same wave)
+            }
+            __syncthreads();
             // exclusive prefix over (slot, canonical row) -> pref[]
             const int R1 = dq + 1;
             const int nkeys = 3 * R1;
@@ -765,14 +824,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
                 if (key < nkeys) {
                     int slot = key / R1, r = key % R1;
                     int ind = rasc ? r : (dq - r);
-                    c = L.cnt[slot * (D + 1) + ind];
+                    c = (int)ld_l2(&rcnt[slot * (D + 1) + ind]);
                 }
                 int ci = wave_incl_sum(c);
                 if (key < nkeys) pref[key] = carry + ci - c;
                 carry += __shfl(ci, 63);
             }
             const int nsector = carry;
-            const int axis_runs = L.cnt[AX];
+            const int axis_runs = (int)ld_l2(&rcnt[AX]);
             if (lane == 0) pref[nkeys] = carry;
             // per-bin run counts for the sectors
             {
@@ -829,8 +888,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
             // reset the per-row counters used by this octant
             __syncthreads();
             for (int i = lane; i < AX; i += 64)
-                if (i % (D + 1) <= dq) L.cnt[i] = 0;
-            if (lane == 0) { L.cnt[AX] = 0; L.misc[16 + q] = bpos; L.misc[24 + q] = seg_len; }
+                if (i % (D + 1) <= dq) st_l2(&rcnt[i], 0u);
+            if (lane == 0) { st_l2(&rcnt[AX], 0u); L.misc[16 + q] = bpos; L.misc[24 + q] = seg_len; }
             bpos += seg_len;
             __syncthreads();
             MK_T(6);
@@ -858,7 +917,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
             if (lane == 0) P.fail_list[atomicAdd(P.fail_count, 1)] = node;
             // leave the wave in a clean LDS state and drop this source
             for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
-            for (int i = lane; i <= AX; i += 64) L.cnt[i] = 0;
+            for (int i = lane; i <= AX; i += 64) st_l2(&rcnt[i], 0u);
             __syncthreads();
             continue;
         }
@@ -890,7 +949,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) ma
         if (lane == 0) {
             atomicAdd(&P.stats[0], examined);
             atomicAdd(&P.stats[1], (unsigned long long)nsize);
-            if (P.profile)
+            if (PROF)
                 for (int i = 0; i < 8; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
             P.attrs[k * 3 + 0] = (float)nsize;
             P.attrs[k * 3 + 1] = m1f;
