@@ -69,76 +69,131 @@ def nearest_filled(pm, x, y):
     raise RuntimeError("no filled cell")
 
 
-def load_traffic(workload):
-    """HBM bytes per launch from a committed rocprofv3 --pmc pass (profiles/pmc_traffic.json)."""
-    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
-    if not os.path.exists(p):
-        return None
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r2_pmc_1000.json")
+FP64_PEAK_TF = 78.6    # MI355X FP64 vector (MI355X_MICROARCH.md)
+
+
+def load_pmc(workload):
+    """Per-kernel PMC summary of the same workload and build (scripts/gpu_pmc.sh -> scripts/pmc_summary.py ->
+    profiles/r2_pmc_1000.json): HBM bytes raw and 2x-FETCH corrected, VALU issue, FP64 instruction counts."""
+    if not os.path.exists(PMC_SUMMARY):
+        return {}
     try:
-        return json.load(open(p)).get(workload)
+        return json.load(open(PMC_SUMMARY)).get(workload, {})
+    except Exception:
+        return {}
+
+
+def cpu_threads():
+    """Threads for the all-cores leg: the job's CPU share (OMP_NUM_THREADS, 16 on the GPU box), at most the
+    affinity set."""
+    n = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, min(n, 16))
+
+
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def calibration():
+    """ref_over_port: the reference (oracle/_ref, built from /root/reference) over the C restatement, seconds
+    on identical inputs in the build container (scripts/calibrate_oracle.py -> tests/golden/oracle_calibration.json)."""
+    p = os.path.join(REPO, "tests", "golden", "oracle_calibration.json")
+    try:
+        d = json.load(open(p))
+        return {"makegraph": d["ref_over_port_makegraph"], "vga": d["ref_over_port_vga"], "measured_on": d["cpu"]}
     except Exception:
         return None
 
 
-def cpu_baseline(region, lines, spacing, fill, g, budget_s):
-    """The C restatement (oracle/, bit-exact vs the reference) timed single-threaded on a bounded
-    sample of the same workload: makeGraph on a contiguous block of sources, then VGA global BFS
-    on a block of sources over the full graph (copied from the GPU result, identical bits)."""
+def _oracle_map(region, lines, spacing, fill):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     from pyoracle import OracleMap
     om = OracleMap(region, spacing, lines)
     om.fill(*fill)
-    N = g.info()["nnodes"]
-    mid = N // 2
-    k, t_mk = 4, 0.0
-    while True:
-        t0 = time.perf_counter()
-        om.make_graph(node_begin=mid, node_end=min(N, mid + k), threads=1)
-        t_mk = time.perf_counter() - t0
-        if t_mk > 0.3 * budget_s or mid + k >= N:
-            break
-        k = min(N - mid, max(k * 2, int(k * 0.3 * budget_s / max(t_mk, 1e-3))))
-    mk_per_src = t_mk / min(k, N - mid)
-    gn = g.copy(runs=True)
-    om.set_graph(gn["bins"], gn["runs"])
-    del gn
-    kv, t_v = 1, 0.0
-    while True:
-        t0 = time.perf_counter()
-        om.vga_global(node_begin=mid, node_end=min(N, mid + kv), threads=1)
-        t_v = time.perf_counter() - t0
-        if t_v > 0.4 * budget_s or mid + kv >= N:
-            break
-        kv = min(N - mid, max(kv * 2, int(kv * 0.4 * budget_s / max(t_v, 1e-3))))
-    vga_per_src = t_v / min(kv, N - mid)
-    return {"value": 1.0 / (mk_per_src + vga_per_src), "unit": "cells/s", "cores": 1, "kind": "port",
-            "sample": "oracle/dmx_oracle.c single thread: makeGraph on %d sources (%.2f s) + VGA global BFS "
-                      "on %d sources (%.2f s) from node %d over the full graph; per-source times -> cells/s"
-                      % (min(k, N - mid), t_mk, min(kv, N - mid), t_v, mid),
-            "makegraph_s_per_source": mk_per_src, "vga_s_per_source": vga_per_src}
+    return om
 
 
-def cpu_baseline_mk(region, lines, spacing, fill, N, budget_s):
-    """Config 5: the C restatement's makeGraph timed single-threaded on a contiguous source block.
-    The step-depth leg is not sampled (it needs the whole ~94 GB graph on the host), so the CPU
-    figure omits it and overstates the CPU rate."""
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    from pyoracle import OracleMap
-    om = OracleMap(region, spacing, lines)
-    om.fill(*fill)
-    mid, k = N // 2, 4
-    while True:
+def _legs(mk1, mkT, v1=None, vT=None):
+    """cells/s of a whole step from per-source seconds: every cell is one makeGraph source and one BFS source."""
+    one = 1.0 / (mk1 + (v1 or 0.0))
+    allc = 1.0 / (mkT + (vT or 0.0))
+    return one, allc
+
+
+def cpu_baseline(region, lines, spacing, fill, g, budget_s, seed=2026, stepdepth=False, N=None):
+    """The C restatement (oracle/dmx_oracle.c, bit-exact vs the reference) on the GPU box's host cores, on a
+    bounded seeded sample of the same workload:
+      makeGraph: S=200 random sources (seed 2026): one thread, then all cores (OpenMP over sources);
+      VGA global BFS (over the whole graph, copied from the GPU and read in place): S=20 random sources on all
+      cores, and the first of them one at a time on one thread until half the budget is spent (>= 2).
+    value = the all-cores rate; `single_thread` = the one-thread rate (the reference is single-threaded);
+    `reference_equivalent` = the one-thread rate divided by the committed reference/restatement ratio."""
+    om = _oracle_map(region, lines, spacing, fill)
+    N = N if N is not None else g.info()["nnodes"]
+    rng = np.random.default_rng(seed)
+    mk_nodes = np.sort(rng.choice(N, size=min(200, N), replace=False))
+    bfs_nodes = np.sort(rng.choice(N, size=min(20, N), replace=False))
+    T = cpu_threads()
+    t0 = time.perf_counter()
+    mk_secs = om.make_graph_sample(mk_nodes, threads=1)
+    mk1_wall = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    om.make_graph_sample(mk_nodes, threads=T)
+    mkT_wall = time.perf_counter() - t0
+    mk1, mkT = mk1_wall / len(mk_nodes), mkT_wall / len(mk_nodes)
+    rec = {"unit": "cells/s", "kind": "port", "cores": T, "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+           "seed": seed, "makegraph": {"sources": len(mk_nodes), "one_thread_s": mk1_wall, "all_cores_s": mkT_wall,
+                                       "s_per_source_one_thread": mk1, "source_s_mean": float(mk_secs.mean()),
+                                       "source_s_max": float(mk_secs.max())}}
+    cal = calibration()
+    if stepdepth:
+        # config 5: the step-depth leg needs the whole ~94 GB graph on the host; not sampled (rate overstated)
+        one, allc = _legs(mk1, mkT)
+        rec["sample"] = ("oracle/dmx_oracle.c: makeGraph on %d seeded random sources, 1 thread %.2f s, %d threads "
+                         "%.2f s; metric step depth not sampled (CPU rate overstated)" % (len(mk_nodes), mk1_wall, T,
+                                                                                          mkT_wall))
+    else:
+        gn = g.copy(runs=True)
+        om.set_graph_view(gn["bins"], gn["runs"])
+        single = []
+        t_start = time.perf_counter()
+        for s in bfs_nodes:
+            _, sec = om.vga_global_sample([int(s)], threads=1)
+            single.append(float(sec[0]))
+            if len(single) >= 2 and time.perf_counter() - t_start > 0.5 * budget_s:
+                break
         t0 = time.perf_counter()
-        om.make_graph(node_begin=mid, node_end=min(N, mid + k), threads=1)
-        t_mk = time.perf_counter() - t0
-        if t_mk > 0.5 * budget_s or mid + k >= N:
-            break
-        k = min(N - mid, max(k * 2, int(k * 0.5 * budget_s / max(t_mk, 1e-3))))
-    k = min(k, N - mid)
-    return {"value": k / t_mk, "unit": "cells/s", "cores": 1, "kind": "port",
-            "sample": "oracle/dmx_oracle.c single thread: makeGraph on %d sources (%.2f s) from node %d; "
-                      "step depth not sampled (CPU rate overstated)" % (k, t_mk, mid),
-            "makegraph_s_per_source": t_mk / k}
+        _, secs = om.vga_global_sample(bfs_nodes, threads=T)
+        vT_wall = time.perf_counter() - t0
+        del om, gn
+        v1, vT = float(np.mean(single)), vT_wall / len(bfs_nodes)
+        one, allc = _legs(mk1, mkT, v1, vT)
+        rec["vga"] = {"sources": len(bfs_nodes), "one_thread_sources": len(single), "s_per_source_one_thread": v1,
+                      "all_cores_s": vT_wall, "s_per_source_all_cores": vT,
+                      "source_s_mean_under_all_cores": float(secs.mean())}
+        rec["sample"] = ("oracle/dmx_oracle.c on seeded random sources (seed %d): makeGraph S=%d (1 thread %.2f s, "
+                         "%d threads %.2f s); VGA global BFS over the full graph S=%d on %d threads (%.2f s) and "
+                         "%d of them on 1 thread (%.2f s each); per-source seconds -> cells/s"
+                         % (seed, len(mk_nodes), mk1_wall, T, mkT_wall, len(bfs_nodes), T, vT_wall, len(single), v1))
+    rec["value"] = allc
+    rec["single_thread"] = {"value": one, "cores": 1}
+    if cal:
+        ref = 1.0 / (mk1 * cal["makegraph"] + (rec["vga"]["s_per_source_one_thread"] * cal["vga"]
+                                                if "vga" in rec else 0.0))
+        rec["reference_equivalent"] = {"value": ref, "cores": 1, "ref_over_port": cal,
+                                       "note": "one-thread rate / the reference-over-restatement ratio measured on "
+                                               "identical inputs (tests/golden/oracle_calibration.json)"}
+    return rec
 
 
 def main():
@@ -170,23 +225,40 @@ def main():
     import torch.distributed as dist
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world == 1 and args.mk_mode == "shard":
+        # one-rank rehearsal of the sharded path: blob write, RCCL all-gather (a local copy at world 1) and
+        # assembly are all timed; only the xGMI transfer itself is absent
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + os.getpid() % 1000))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    dist_on = world > 1 or args.mk_mode == "shard"
+    if dist_on:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
     import depthmapx_amd as dmx
-    from depthmapx_amd.sharded import (allgather_blobs, allgather_rows_chunked, prep_allreduce, shard_range,
-                                       vga_nodes)
+    from depthmapx_amd.sharded import (allgather_rows_chunked, choose_mk_mode, exchange_graph, prep_allreduce,
+                                       shard_range, vga_nodes)
 
     stepdepth = args.config == 5
     if stepdepth:
         W, args.occluders, lmin, lmax = 1999, 5000, 0.0025, 0.01
     else:
         W, lmin, lmax = args.grid or (256 if args.config == 1 else 1000), 0.02, 0.10
+    # makeGraph across ranks: "auto" runs the first warm-up step sharded, measures the shard build and the
+    # graph exchange, then keeps whichever of shard / replicate the measurement predicts faster (max over
+    # ranks: sharded.choose_mk_mode).  With no warm-up step it stays sharded (the
+    # exchange moves ~36 GB at 1000^2, well under a second at xGMI all-gather rates, against ~5 s of makeGraph
+    # that replicate repeats on every rank).
     mk_mode = args.mk_mode
-    if mk_mode == "auto":
+    mk_auto = None
+    if world == 1 and mk_mode == "auto":
+        mk_mode = "replicate"
+    elif mk_mode == "auto":
         mk_mode = "shard"
+        mk_auto = {}
     lines = load_lines(W, args.occluders, lmin, lmax)
     region = [0.0, 0.0, float(W), float(W)]
     fill = (0.5, 0.5)
@@ -207,25 +279,28 @@ def main():
 
     out_full = None if stepdepth else torch.full((N, 7), -1.0, dtype=torch.float32, device=dev)
     sd_out = [None]
-    kt = {"makegraph_s": 0.0, "vga_s": 0.0, "n": 0}
+    kt = {"makegraph_s": 0.0, "vga_s": 0.0, "n": 0, "exchange_s": 0.0, "allgather_s": 0.0, "xbytes": 0}
     stats = {}
 
     def step(record):
         # 1. makeGraph: this rank's sources (shard) or all of them (replicate)
-        if world > 1 and mk_mode == "shard":
+        if mk_mode == "shard":
             shard = pm.make_graph(ctx, node_begin=b, node_end=e)
         else:
             shard = pm.make_graph(ctx)
         t_mk = ctx.last_timing()[0]
         st = dict(ctx.last_stats())
-        if world > 1 and mk_mode == "shard":
+        if mk_mode == "shard":
             # 2. all-gather the run-length graph shards (RCCL), assemble the whole graph
-            blob = torch.empty(shard.blob_size(), dtype=torch.uint8, device=dev)
-            shard.write_blob_device(blob.data_ptr(), blob.numel())
-            flat, mx, sizes = allgather_blobs(blob, dist)
-            torch.cuda.synchronize()
-            g = pm.assemble(ctx, [flat.data_ptr() + i * mx for i in range(world)], sizes)
-            del flat, blob, shard
+            g, xt = exchange_graph(pm, ctx, shard, dist, dev)
+            del shard
+            if mk_auto is not None and not mk_auto:
+                mk_auto.update(xt)
+                mk_auto["mk_shard_s"] = t_mk
+            if record:
+                kt["exchange_s"] += xt["blob_s"] + xt["allgather_s"] + xt["assemble_s"]
+                kt["allgather_s"] += xt["allgather_s"]
+                kt["xbytes"] = xt["bytes"]
         else:
             g = shard
         if stepdepth:
@@ -260,9 +335,14 @@ def main():
             stats.update(st)
         return g
 
-    for _ in range(args.warmup):
+    for w in range(args.warmup):
         g = step(False)
         del g
+        if w == 0 and mk_auto is not None:
+            mk_mode, dec = choose_mk_mode(dist, dev, world, mk_auto["mk_shard_s"], mk_auto["blob_s"] +
+                                          mk_auto["allgather_s"] + mk_auto["assemble_s"], (e - b) / max(N, 1))
+            mk_auto.update(dec)
+            mk_auto["chosen"] = mk_mode
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -305,8 +385,41 @@ def main():
         dominant = second if vga_s >= mk_s else "makegraph_kernel"
         dom_bytes, dom_s = (vga_bytes, vga_s) if vga_s >= mk_s else (mk_bytes, mk_s)
         achieved = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
-        traffic = load_traffic(workload)
-        tr = traffic.get(dominant) if isinstance(traffic, dict) else None
+        pmc = load_pmc(workload) if world == 1 else {}
+        dpm = pmc.get(dominant, {})
+        roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                # HBM bytes per launch from the PMC passes of this workload and build: FETCH_SIZE + WRITE_SIZE as
+                # read (neither kernel streams 16 B/lane, where the guide's 2x FETCH correction applies); the
+                # corrected figure is an upper bound
+                "traffic": dpm.get("hbm_bytes_raw"), "traffic_corrected_2x_fetch": dpm.get("hbm_bytes_corrected"),
+                "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if dpm else None,
+                "algorithmic_bytes": dom_bytes,
+                "kernel_s_live": dom_s, "kernel_s_rocprof": dpm.get("duration_ns", 0) * 1e-9 if dpm else None}
+        if not stepdepth:
+            # SURVEY.md section 8(d) B_vga at batch size 1 = the reference's BFS work (every source reads every
+            # reached node's run records and touches N cells): the bytes a run-by-run BFS would move
+            b_vga = nsrc * (8 * int(g.info()["nruns"]) + 4 * N)
+            roof["b_vga_reference_work"] = b_vga
+            roof["b_vga_rate_GBs"] = b_vga / vga_s / 1e9 if vga_s else None
+            roof["work_model"] = ("8 B x run records tested + 16 B x tiles x sources (V/X reset) + 32 B x tiles x "
+                                  "levels + tile-visibility rows read (DESIGN.md section 3)")
+        # issue-rate roofline (VALU) for the two hot kernels, and makeGraph's FP64 rate
+        issue = {}
+        for kname in ("makegraph_kernel", "vga_tile_kernel", "stepdepth_kernel"):
+            e = pmc.get(kname)
+            if e and "valu_active_frac" in e:
+                issue[kname] = {"valu_busy_frac": e["valu_active_frac"], "valu_issue_frac": e.get("valu_issue_frac"),
+                                "wave_cycles_split": e.get("wave_cycles_split"), "clock_ghz": e.get("clock_ghz")}
+        if issue:
+            roof["issue"] = issue
+        mkp = pmc.get("makegraph_kernel", {})
+        if "per_step" in mkp and "fp64_flops" in mkp["per_step"] and mk_s:
+            f = mkp["per_step"]["fp64_flops"]
+            roof["makegraph_fp64"] = {"flops": f, "achieved": f / mk_s / 1e12, "peak": FP64_PEAK_TF,
+                                      "unit": "TFLOP/s", "frac": f / mk_s / 1e12 / FP64_PEAK_TF,
+                                      "note": "64 x (ADD+MUL+TRANS+2 FMA) F64 wave instructions (PMC), over the "
+                                              "live makeGraph time"}
         rec = {
             "metric": "grid cells/sec for VISPREP makeGraph + VGA global on N×N grid",
             "value": N * steps / elapsed,
@@ -336,9 +449,12 @@ def main():
                         "vga_levels_top_down": stats.get("vga_top_down_levels"),
                         "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc,
                         "makegraph_algorithmic_bytes": mk_bytes, "vga_algorithmic_bytes": vga_bytes},
-            "roofline": {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": tr},
+            "roofline": roof,
         }
+        if kt["exchange_s"] or mk_auto:
+            rec["kernels"]["graph_exchange"] = {
+                "s_per_step": kt["exchange_s"] / max(kt["n"], 1), "allgather_s": kt["allgather_s"] / max(kt["n"], 1),
+                "bytes": kt["xbytes"], "auto": mk_auto}
         if stepdepth:
             rec["metric"] = "grid cells/sec for VISPREP makeGraph + metric step depth on N×N grid"
             kk = rec["kernels"]
@@ -348,16 +464,14 @@ def main():
                        "stepdepth_cells_relaxed": stats.get("sd_cells_relaxed"),
                        "stepdepth_algorithmic_bytes": vga_bytes,
                        "stepdepth_reached_cells": int((sd_out[0][:, 0] >= 0).sum())})
-        if not args.no_cpu_baseline and world == 1 and stepdepth:
-            rec["cpu_baseline"] = cpu_baseline_mk(region, lines, 1.0, fill, N, args.cpu_budget)
-            rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
-        elif not args.no_cpu_baseline and world == 1:
-            rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, g, args.cpu_budget)
+        if not args.no_cpu_baseline and world == 1:
+            rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, g, args.cpu_budget, stepdepth=stepdepth,
+                                               N=N)
             rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
         print(json.dumps(rec), flush=True)
         if args.dump_out and out_full is not None:
             np.save(args.dump_out, out_full.cpu().numpy())
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -11,7 +11,9 @@ LIB_PATH = os.path.join(_HERE, "_lib", "libdmx.so")
 
 DMX_OK = 0
 STATUS_NAMES = {-1: "DMX_ERR_ARG", -2: "DMX_ERR_HIP", -3: "DMX_ERR_CAPACITY", -4: "DMX_ERR_STATE",
-                -5: "DMX_ERR_UNSUPPORTED", -6: "DMX_ERR_OUTSIDE"}
+                -5: "DMX_ERR_UNSUPPORTED", -6: "DMX_ERR_OUTSIDE", -7: "DMX_ERR_CANCELLED"}
+# int32_t (*dmx_progress_fn)(void* user, int32_t phase, int64_t done, int64_t total)
+PROGRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int32, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_int64)
 
 # every symbol include/dmx.h declares, with (restype, argtypes)
 _vp, _i64, _i32, _dbl, _cs = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_char_p
@@ -47,6 +49,8 @@ SIGNATURES = {
     "dmx_vga_angular": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp]),
     "dmx_angular_stepdepth": (_i32, [_vp, _vp, _vp, _i64, _vp]),
     "dmx_release_cached_memory": (_i32, []),
+    "dmx_ctx_set_progress": (_i32, [_vp, PROGRESS_FN, _vp, _dbl]),
+    "dmx_ctx_cancel": (_i32, [_vp]),
     "dmx_ctx_last_stepdepth": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_ctx_last_stepdepth_detail": (_i32, [_vp, _vp]),
     "dmx_ctx_last_phase_cycles": (_i32, [_vp, _vp]),

@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/dmx.h"
@@ -37,7 +38,10 @@ double now_s() {
 }
 bool verbose() {
     static int v = -1;
-    if (v < 0) v = getenv("DMX_VERBOSE") ? 1 : 0;
+    if (v < 0) {
+        const char* e = getenv("DMX_VERBOSE");
+        v = (e && *e && strcmp(e, "0") != 0) ? 1 : 0;
+    }
     return v == 1;
 }
 #define VLOG(...)                                      \
@@ -173,6 +177,13 @@ struct dmx_ctx {
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
     long long last_stats[32] = {};
+    // progress / cancel (dmx_ctx_set_progress, dmx_ctx_cancel): host-mapped block polled by the kernels
+    DmxCtl* h_ctl = nullptr;
+    DmxCtl* d_ctl = nullptr;
+    dmx_progress_fn progress = nullptr;
+    void* progress_user = nullptr;
+    double progress_interval = 0.5;
+    hipEvent_t ev_poll = nullptr;
 };
 
 struct dmx_pointmap {
@@ -345,9 +356,63 @@ int dmx_ctx_create(int device, dmx_ctx** out) {
     HIPCHK(hipEventCreate(&c->ev1));
     HIPCHK(c->counters.alloc(16));
     HIPCHK(c->stats.alloc(32));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_poll, hipEventDisableTiming));
+    HIPCHK(hipHostMalloc((void**)&c->h_ctl, sizeof(DmxCtl), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(c->h_ctl, 0, sizeof(DmxCtl));
+    HIPCHK(hipHostGetDevicePointer((void**)&c->d_ctl, c->h_ctl, 0));
     *out = c;
     return DMX_OK;
 }
+
+int dmx_ctx_set_progress(dmx_ctx* ctx, dmx_progress_fn fn, void* user, double interval_s) {
+    if (!ctx || !(interval_s >= 0.0)) return fail(DMX_ERR_ARG, "bad arguments");
+    ctx->progress = fn;
+    ctx->progress_user = user;
+    ctx->progress_interval = interval_s > 0.0 ? interval_s : 0.5;
+    return DMX_OK;
+}
+
+int dmx_ctx_cancel(dmx_ctx* ctx) {
+    if (!ctx || !ctx->h_ctl) return fail(DMX_ERR_ARG, "bad context");
+    __atomic_store_n(&ctx->h_ctl->cancel, 1, __ATOMIC_SEQ_CST);
+    return DMX_OK;
+}
+
+// Wait for the work queued on the context stream.  With a progress callback, poll it every interval
+// while the kernel runs: done = (work items taken, published by the kernel) x unit; a non-zero return
+// from the callback requests cancellation, as dmx_ctx_cancel does.
+static hipError_t wait_progress(dmx_ctx* ctx, int32_t phase, int64_t total, int64_t unit) {
+    if (!ctx->progress) return hipStreamSynchronize(ctx->stream);
+    hipError_t e = hipEventRecord(ctx->ev_poll, ctx->stream);
+    if (e != hipSuccess) return e;
+    double next = now_s() + ctx->progress_interval;
+    for (;;) {
+        e = hipEventQuery(ctx->ev_poll);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) return e;
+        if (now_s() >= next) {
+            const int64_t done = std::min<int64_t>(total, (int64_t)__atomic_load_n(&ctx->h_ctl->progress,
+                                                                                  __ATOMIC_RELAXED) * unit);
+            if (ctx->progress(ctx->progress_user, phase, done, total)) dmx_ctx_cancel(ctx);
+            next = now_s() + ctx->progress_interval;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(500));
+    }
+    if (!__atomic_load_n(&ctx->h_ctl->cancel, __ATOMIC_SEQ_CST) && ctx->progress(ctx->progress_user, phase, total, total))
+        dmx_ctx_cancel(ctx);
+    return hipSuccess;
+}
+
+// A raised cancel flag ends the running operation with DMX_ERR_CANCELLED and is consumed by it.
+static bool take_cancel(dmx_ctx* ctx) {
+    if (!__atomic_load_n(&ctx->h_ctl->cancel, __ATOMIC_SEQ_CST)) return false;
+    __atomic_store_n(&ctx->h_ctl->cancel, 0, __ATOMIC_SEQ_CST);
+    return true;
+}
+#define CANCEL_POINT(ctx)                                                        \
+    do {                                                                         \
+        if (take_cancel(ctx)) return fail(DMX_ERR_CANCELLED, "operation cancelled"); \
+    } while (0)
 
 int dmx_release_cached_memory(void) {
     BlockCache& c = block_cache();
@@ -363,6 +428,8 @@ int dmx_ctx_free(dmx_ctx* c) {
     c->stats.reset();
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->ev_poll) (void)hipEventDestroy(c->ev_poll);
+    if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return DMX_OK;
@@ -552,6 +619,8 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.cellw = pm->d_cellw.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
             P.node_begin = node_begin; P.node_end = node_end;
             P.work_counter = ctx->counters.p + 0;
+            P.ctl = ctx->d_ctl;
+            ctx->h_ctl->progress = 0;
             P.error = ctx->counters.p + 1;
             P.pool_cursor = (unsigned long long*)(ctx->counters.p + 2);
             P.pool_capacity = pool_cap; P.pool = g->pool.p;
@@ -574,7 +643,8 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
                 HIPCHK(hipGetLastError());
             }
             HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-            HIPCHK(hipStreamSynchronize(ctx->stream));
+            HIPCHK(wait_progress(ctx, DMX_PHASE_MAKEGRAPH, todo, 1));
+            CANCEL_POINT(ctx);
             float ms = 0;
             HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
             kernel_s += ms * 1e-3;
@@ -1154,9 +1224,11 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
     if (const char* c = getenv("DMX_VGA_CHUNK")) P.chunk = std::max(1, atoi(c));
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
+    P.ctl = ctx->d_ctl;
+    ctx->h_ctl->progress = 0;
     hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL, RBM>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(ctx->stream));   // hint freed on return
+    HIPCHK(wait_progress(ctx, DMX_PHASE_VGA, nsrc, P.chunk));   // hint freed on return
     *blocks_out = blocks;
     return DMX_OK;
 }
@@ -1242,6 +1314,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
             ntpb = 1024;
         }
         if (rc) return rc;
+        CANCEL_POINT(ctx);
         if (nseeds == 0) {
             hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsrc + 255) / 256)), dim3(256), 0, ctx->stream, sb,
                                se, d_hist.p, d_nlev.p, outp, levels ? d_lv.p : nullptr, ctx->stats.p, d_src_list);
@@ -1390,7 +1463,9 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->h_ctl->progress = 0;   // these kernels do not poll: a cancel takes effect when they finish
+    HIPCHK(wait_progress(ctx, DMX_PHASE_VGA, nsrc, 1));
+    CANCEL_POINT(ctx);
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     ctx->last_vga_s = ms * 1e-3;
@@ -1719,6 +1794,7 @@ static int stepdepth_batched(dmx_ctx* ctx, dmx_graph* g, const std::vector<uint8
         HIPCHK(hipMemcpyAsync(&hc, d_ctl.p, sizeof(hc), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));
         if (hc.done) break;
+        CANCEL_POINT(ctx);
         if (it > max_it) return fail(DMX_ERR_STATE, "batched step depth did not terminate");
     }
     HIPCHK(hipEventRecord(ctx->ev1, s));

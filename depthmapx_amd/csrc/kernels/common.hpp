@@ -35,4 +35,23 @@ struct alignas(8) Run {
     int16_t x0, y0, x1, y1;
 };
 
+// Host-mapped control block shared by the host and a running kernel (dmx_ctx_set_progress /
+// dmx_ctx_cancel): the host raises `cancel`, workers stop taking work items; workers publish the index
+// of the item they took in `progress`.  The reference's Communicator polls IsCancelled and posts the
+// record count every 500 ms (genlib/comm.h:59-142, salalib/pointdata.cpp:1301-1316).
+struct DmxCtl {
+    int cancel;
+    int progress;
+};
+constexpr int CTL_STOP = 1 << 29;   // work index handed out after a cancel: past every range
+
+// Poll at a work grab (one lane): publish the grabbed index every 8th grab, read the cancel word.
+// Both are vector memory operations at system scope on host-mapped memory.
+__device__ __forceinline__ int ctl_poll(DmxCtl* c, int w) {
+    if (!c) return w;
+    if ((w & 7) == 0) __hip_atomic_store(&c->progress, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (__hip_atomic_load(&c->cancel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) return CTL_STOP;
+    return w;
+}
+
 } // namespace dmx

@@ -30,6 +30,7 @@ struct MakeGraphParams {
     const int32_t* node_cell;  // [N] node -> x-major cell index
     int64_t node_begin, node_end;
     int* work_counter;         // dynamic source counter (zeroed by the host each launch)
+    DmxCtl* ctl;               // host-mapped progress / cancel block (nullptr: none)
     unsigned long long* pool_cursor;
     int64_t pool_capacity;     // in runs
     Run* pool;
@@ -182,9 +183,10 @@ __device__ __forceinline__ Run make_run(int q, int cx, int cy, int ind, int ds, 
     return r;
 }
 
-// per-wave counters in HBM scratch, read and written through L2 (a wave reads back its own stores)
-__device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ __forceinline__ void st_l2(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+// per-wave counters in HBM scratch (one wave per workgroup reads back its own stores: workgroup scope keeps
+// them in L1/L2; agent scope would write every store through to memory and miss L2 on every load)
+__device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+__device__ __forceinline__ void st_l2(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
 // open-run state per row: valid(1) | slot(2) | start(14) | last(14)
 __device__ __forceinline__ uint32_t pack_open(int slot, int s, int l) {
@@ -307,7 +309,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
     for (;;) {
         int s_idx = 0;
-        if (lane == 0) s_idx = atomicAdd(P.work_counter, 1);
+        if (lane == 0) s_idx = ctl_poll(P.ctl, atomicAdd(P.work_counter, 1));
         s_idx = __shfl(s_idx, 0);
         int64_t node;
         if (P.node_list) {

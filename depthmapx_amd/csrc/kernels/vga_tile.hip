@@ -59,6 +59,7 @@ struct VgaTileParams {
     int64_t uf_count;
     int alpha;
     int* work_counter;
+    DmxCtl* ctl;              // host-mapped progress / cancel block (nullptr: none)
     int chunk;                // consecutive sources per work grab (neighbouring sources share hints)
     uint16_t* hint;           // [nt*64] scan position of the run that last hit for a recent source (0xFFFF:
                               // none); shared by all workgroups: a stale value only costs one test
@@ -397,7 +398,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
         // through the same runs: the hint array carries that knowledge from one source to the next
         if (src + 1 >= chunk_end) {
             __syncthreads();
-            if (tid == 0) S.src = atomicAdd(P.work_counter, 1);
+            if (tid == 0) S.src = ctl_poll(P.ctl, atomicAdd(P.work_counter, 1));
             __syncthreads();
             src = P.src_begin + (int64_t)S.src * P.chunk;
             chunk_end = min(src + (int64_t)P.chunk, P.src_end);

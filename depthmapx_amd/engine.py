@@ -45,6 +45,26 @@ class Context:
 
     __del__ = close
 
+    def set_progress(self, fn, interval_s=0.5):
+        """fn(phase, done, total) -> truthy to cancel, called while makeGraph / VGA-global kernels run
+        (dmx_ctx_set_progress; the reference's Communicator, genlib/comm.h:59-142).  None removes it."""
+        if fn is None:
+            self._progress = None
+            N.check(N.lib().dmx_ctx_set_progress(self.h, N.PROGRESS_FN(), None, 0.0))
+            return
+
+        def tramp(_user, phase, done, total):
+            try:
+                return 1 if fn(int(phase), int(done), int(total)) else 0
+            except Exception:
+                return 1
+        self._progress = N.PROGRESS_FN(tramp)   # kept alive while registered
+        N.check(N.lib().dmx_ctx_set_progress(self.h, self._progress, None, float(interval_s)))
+
+    def cancel(self):
+        """Cancel the running (or next) makeGraph / VGA-global / step-depth call (any thread)."""
+        N.check(N.lib().dmx_ctx_cancel(self.h))
+
     def last_timing(self):
         mk, vg = ctypes.c_double(), ctypes.c_double()
         N.check(N.lib().dmx_ctx_last_timing(self.h, ctypes.byref(mk), ctypes.byref(vg)))

@@ -51,6 +51,60 @@ def allgather_blobs(blob, dist, device=None):
     return flat, mx, sizes
 
 
+def exchange_graph(pm, ctx, shard, dist, device):
+    """Step 2 on device memory: every rank's run-length shard blob is written straight into its padded
+    send buffer, all-gathered (RCCL all_gather_into_tensor over xGMI) and assembled into the whole graph.
+    Returns (graph, {"blob_s", "allgather_s", "assemble_s", "bytes"}); the phases are bracketed by device
+    synchronisations so that bench.py can size the exchange against replicated makeGraph."""
+    import time
+    world = dist.get_world_size()
+
+    def sync():
+        if device.type == "cuda":
+            torch.cuda.synchronize(device)
+    sync()
+    t0 = time.perf_counter()
+    n = shard.blob_size()
+    sz = torch.tensor([n], dtype=torch.int64, device=device)
+    sizes = [torch.zeros_like(sz) for _ in range(world)]
+    dist.all_gather(sizes, sz)
+    sizes = [int(v.item()) for v in sizes]
+    mx = max(sizes)
+    mine = torch.empty(mx, dtype=torch.uint8, device=device)
+    shard.write_blob_device(mine.data_ptr(), n)
+    sync()
+    t1 = time.perf_counter()
+    flat = torch.empty(world * mx, dtype=torch.uint8, device=device)
+    if _rccl(dist):
+        dist.all_gather_into_tensor(flat, mine)
+    else:
+        parts = list(flat.view(world, mx).unbind(0))
+        dist.all_gather(parts, mine)
+    sync()
+    t2 = time.perf_counter()
+    del mine
+    g = pm.assemble(ctx, [flat.data_ptr() + i * mx for i in range(world)], sizes)
+    sync()
+    t3 = time.perf_counter()
+    del flat
+    return g, {"blob_s": t1 - t0, "allgather_s": t2 - t1, "assemble_s": t3 - t2, "bytes": sum(sizes),
+               "padded_bytes": world * mx}
+
+
+def choose_mk_mode(dist, device, world, mk_shard_s, exchange_s, shard_frac):
+    """--mk-mode auto after a warm-up step run sharded: replicate (every rank builds the whole graph, no
+    data-path collective) when building it all costs less than building the shard and exchanging it.
+    Times are the max over ranks so that every rank takes the same branch."""
+    t = torch.tensor([mk_shard_s, exchange_s, shard_frac], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    mk, ex, frac = (float(v) for v in t.tolist())
+    replicate_s = mk / max(frac, 1e-9)
+    shard_s = mk + ex
+    return ("replicate" if replicate_s < shard_s else "shard"), {"predicted_replicate_s": replicate_s,
+                                                                 "predicted_shard_s": shard_s,
+                                                                 "mk_shard_s": mk, "exchange_s": ex}
+
+
 def allgather_rows(full, n, dist):
     """full: [n, k] tensor where this rank filled rows shard_range(n, rank, world); afterwards every
     rank holds all rows."""

@@ -27,7 +27,15 @@ enum {
     DMX_ERR_CAPACITY = -3,     /* a kernel capacity was exceeded even after retries */
     DMX_ERR_STATE = -4,        /* call sequence not allowed (e.g. makegraph on an unfilled map) */
     DMX_ERR_UNSUPPORTED = -5,  /* feature of the reference not (yet) implemented on this path */
-    DMX_ERR_OUTSIDE = -6       /* fill point outside the region ("Point outside of target region") */
+    DMX_ERR_OUTSIDE = -6,      /* fill point outside the region ("Point outside of target region") */
+    DMX_ERR_CANCELLED = -7     /* dmx_ctx_cancel / the progress callback stopped the operation
+                                  (the reference throws Communicator::CancelledException, genlib/comm.h:61-65) */
+};
+
+/* Phases reported to the progress callback. */
+enum {
+    DMX_PHASE_MAKEGRAPH = 1,   /* sources of PointMap::sparkGraph2 (pointdata.cpp:1293-1322) */
+    DMX_PHASE_VGA = 2          /* sources of VGAVisualGlobal::run (vgavisualglobal.cpp:195-202) */
 };
 
 typedef struct dmx_ctx dmx_ctx;
@@ -46,6 +54,21 @@ int dmx_ctx_free(dmx_ctx* ctx);
  * (run pool, scan order, visibility rows) to the HIP runtime.  Optional; allocation failures do it
  * automatically. */
 int dmx_release_cached_memory(void);
+
+/* Progress and cancellation, the Communicator contract (genlib/comm.h:59-142): the reference posts the
+ * record count and polls IsCancelled every 500 ms inside makeGraph (pointdata.cpp:1301-1316) and VGA
+ * (vgavisualglobal.cpp:195-202).  While a makegraph / VGA-global kernel runs, the calling thread
+ * calls fn(user, phase, done, total) every interval_s seconds (<= 0: 0.5 s) and once with
+ * done == total when the phase completes; a non-zero return requests cancellation.  fn NULL: no
+ * polling (the default).  The kernels read the cancel word between sources, so a cancelled call
+ * returns DMX_ERR_CANCELLED within one source's time; its outputs are not written (device outputs
+ * are undefined).  A context's callback runs on the thread that made the call. */
+typedef int32_t (*dmx_progress_fn)(void* user, int32_t phase, int64_t done, int64_t total);
+int dmx_ctx_set_progress(dmx_ctx* ctx, dmx_progress_fn fn, void* user, double interval_s);
+/* Request cancellation of the operation running on ctx (callable from any thread).  The request is
+ * consumed by the operation that observes it; one made while no operation runs cancels the next
+ * makegraph / VGA-global / step-depth call at its first poll. */
+int dmx_ctx_cancel(dmx_ctx* ctx);
 /* Wall time of the kernels of the last makegraph / vga call, measured with HIP events on the
  * context stream (seconds); kernel_ms receives per-kernel averages. */
 int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);

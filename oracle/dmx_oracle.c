@@ -157,6 +157,7 @@ struct dmxo_map {
     NodeG* nodes;
     float* attrs;        /* [N][3] */
     uint8_t* gridconn;
+    int runs_borrowed;   /* nodes[].runs point into a caller's array (dmxo_set_graph_view) */
 };
 
 static inline int64_t cidx(const dmxo_map* m, int x, int y) { return (int64_t)x * m->rows + y; }
@@ -206,11 +207,21 @@ dmxo_map* dmxo_create(const double region[4], double spacing, const double* line
     return m;
 }
 
+static void release_nodes(dmxo_map* m) {
+    if (m->nodes) {
+        if (!m->runs_borrowed)
+            for (int64_t i = 0; i < m->nnodes; i++) free(m->nodes[i].runs);
+        free(m->nodes);
+    }
+    m->nodes = NULL;
+    m->runs_borrowed = 0;
+}
+
 void dmxo_free(dmxo_map* m) {
     if (!m) return;
     free(m->state); free((void*)m->draw); free(m->cl_off); free(m->cl);
     free(m->node_of_cell); free(m->node_cell); free(m->attrs); free(m->gridconn);
-    if (m->nodes) { for (int64_t i = 0; i < m->nnodes; i++) free(m->nodes[i].runs); free(m->nodes); }
+    release_nodes(m);
     free(m);
 }
 
@@ -740,7 +751,7 @@ int dmxo_makegraph(dmxo_map* m, double maxdist, int boundary, int64_t nb, int64_
     }
     index_nodes(m);
     int64_t N = m->nnodes;
-    if (m->nodes) { for (int64_t i = 0; i < N; i++) free(m->nodes[i].runs); free(m->nodes); }
+    release_nodes(m);
     m->nodes = (NodeG*)calloc(N ? N : 1, sizeof(NodeG));
     free(m->attrs); m->attrs = (float*)calloc((N ? N : 1) * 3, sizeof(float));
     free(m->gridconn); m->gridconn = (uint8_t*)calloc(N ? N : 1, 1);
@@ -786,6 +797,7 @@ int dmxo_makegraph(dmxo_map* m, double maxdist, int boundary, int64_t nb, int64_
  * time in secs[i].  The graph arrays of the map are allocated on first use (no boundary graph). */
 int dmxo_makegraph_sample(dmxo_map* m, double maxdist, const int64_t* nodes, int64_t n, int nthreads, double* secs) {
     if (!m->blocked_lines) block_lines(m);
+    if (m->runs_borrowed) release_nodes(m);
     if (!m->nodes) {
         index_nodes(m);
         int64_t N = m->nnodes;
@@ -848,6 +860,7 @@ void dmxo_get_graph(const dmxo_map* m, float* attrs, int32_t* bins, int16_t* run
 int dmxo_set_graph(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_t nruns) {
     if (!m->node_of_cell) index_nodes(m);
     int64_t N = m->nnodes, ro = 0;
+    if (m->runs_borrowed) release_nodes(m);
     if (!m->nodes) m->nodes = (NodeG*)calloc(N ? N : 1, sizeof(NodeG));
     for (int64_t k = 0; k < N; k++) {
         NodeG* nd = &m->nodes[k];
@@ -863,6 +876,32 @@ int dmxo_set_graph(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_
         if (ro + t > nruns) return -1;
         nd->runs = (Run*)malloc((t ? t : 1) * sizeof(Run));
         memcpy(nd->runs, runs + 4 * ro, t * sizeof(Run));
+        nd->total_runs = t;
+        ro += t;
+    }
+    return 0;
+}
+
+/* As dmxo_set_graph, without copying the runs: nodes[].runs point into `runs`, which the caller keeps
+ * alive and unchanged until the next set_graph / makegraph / free (bench.py's CPU leg on a 36 GB graph). */
+int dmxo_set_graph_view(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_t nruns) {
+    if (!m->node_of_cell) index_nodes(m);
+    int64_t N = m->nnodes, ro = 0;
+    release_nodes(m);
+    m->nodes = (NodeG*)calloc(N ? N : 1, sizeof(NodeG));
+    m->runs_borrowed = 1;
+    for (int64_t k = 0; k < N; k++) {
+        NodeG* nd = &m->nodes[k];
+        int64_t t = 0;
+        for (int b = 0; b < 32; b++) {
+            const int32_t* o = bins + (k * 32 + b) * 4;
+            nd->dir[b] = (char)o[0]; nd->count[b] = (uint16_t)o[1];
+            memcpy(&nd->dist[b], &o[2], 4);
+            nd->nruns[b] = o[3];
+            t += o[3];
+        }
+        if (ro + t > nruns) { release_nodes(m); return -1; }
+        nd->runs = (Run*)(runs + 4 * ro);
         nd->total_runs = t;
         ro += t;
     }

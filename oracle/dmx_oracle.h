@@ -45,6 +45,8 @@ int64_t dmxo_num_runs(const dmxo_map* m);
 void dmxo_get_graph(const dmxo_map* m, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn);
 /* Replace the graph with externally supplied bins/runs (e.g. a reference dump), same layout. */
 int dmxo_set_graph(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_t nruns);
+/* same, borrowing `runs` (kept alive by the caller) instead of copying it */
+int dmxo_set_graph_view(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_t nruns);
 
 /* VGAVisualGlobal::run (vgamodules/vgavisualglobal.cpp:23-216) for source nodes
  * [node_begin, node_end).  out [N][7] in column order: Visual Entropy, Integration [HH],

@@ -58,6 +58,8 @@ def lib():
         L.dmxo_vga_local.argtypes = [vp, i32, i64, i64, i32, vp]
         L.dmxo_vga_global.restype = i32
         L.dmxo_vga_global.argtypes = [vp, dbl, i32, i64, i64, i32, vp, vp]
+        L.dmxo_set_graph_view.restype = i32
+        L.dmxo_set_graph_view.argtypes = [vp, vp, vp, i64]
         L.dmxo_makegraph_sample.restype = i32
         L.dmxo_makegraph_sample.argtypes = [vp, dbl, vp, i64, i32, vp]
         L.dmxo_vga_global_sample.restype = i32
@@ -127,6 +129,15 @@ class OracleMap:
         rc = lib().dmxo_set_graph(self.h, _p(bins), _p(runs), len(runs))
         if rc:
             raise ValueError("bins/runs inconsistent")
+        self._borrowed = None
+
+    def set_graph_view(self, bins, runs):
+        """set_graph without copying the runs: the map keeps a reference to `runs` and reads it in place."""
+        bins = np.ascontiguousarray(bins, dtype=np.int32)
+        runs = np.ascontiguousarray(runs, dtype=np.int16)
+        if lib().dmxo_set_graph_view(self.h, _p(bins), _p(runs), len(runs)):
+            raise ValueError("bins/runs inconsistent")
+        self._borrowed = runs
 
     def vga_global(self, radius=-1.0, gates_only=False, node_begin=0, node_end=-1, threads=1, levels=False):
         N = self.num_nodes

@@ -38,12 +38,36 @@ def _unpack(buf):
     return bins, runs
 
 
+class _HostShard:
+    """The Graph shard's blob interface (blob_size / write_blob_device) over a host byte array."""
+
+    def __init__(self, buf):
+        self.buf = buf
+
+    def blob_size(self):
+        return len(self.buf)
+
+    def write_blob_device(self, ptr, n):
+        import ctypes
+        assert n == len(self.buf)
+        ctypes.memmove(ptr, self.buf.ctypes.data, n)
+
+
+class _HostAssembler:
+    """PointMap.assemble over host pointers: unpack each rank's blob, concatenate in rank order."""
+
+    def assemble(self, ctx, ptrs, sizes):
+        import ctypes
+        parts = [_unpack(np.frombuffer(ctypes.string_at(p, n), dtype=np.uint8)) for p, n in zip(ptrs, sizes)]
+        return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+
+
 def _worker(rank, world, port, q):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     for p in (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle")):
         sys.path.insert(0, p)
-    from depthmapx_amd.sharded import allgather_blobs, allgather_rows_chunked, shard_range, vga_nodes
+    from depthmapx_amd.sharded import allgather_rows_chunked, choose_mk_mode, exchange_graph, shard_range, vga_nodes
     from pyoracle import OracleMap
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -57,12 +81,12 @@ def _worker(rank, world, port, q):
     full = om.graph()
     ro = int(full["bins"][:b, :, 3].sum())
     nr = int(full["bins"][b:e, :, 3].sum())
-    blob = torch.from_numpy(_pack(dict(bins=full["bins"][b:e], runs=full["runs"][ro:ro + nr]), e - b))
-    flat, mx, sizes = allgather_blobs(blob, dist, device=torch.device("cpu"))
-    parts = [_unpack(flat[i * mx:i * mx + sizes[i]].numpy()) for i in range(world)]
-    bins = np.concatenate([p[0] for p in parts])
-    runs = np.concatenate([p[1] for p in parts])
+    shard = _HostShard(_pack(dict(bins=full["bins"][b:e], runs=full["runs"][ro:ro + nr]), e - b))
+    (bins, runs), xt = exchange_graph(_HostAssembler(), None, shard, dist, torch.device("cpu"))
+    assert xt["bytes"] >= shard.blob_size() and xt["allgather_s"] >= 0
     om.set_graph(bins, runs)
+    # --mk-mode auto: ranks measure different times but must take the same branch
+    mode, dec = choose_mk_mode(dist, torch.device("cpu"), world, 1.0 + rank, 0.5 * rank, (e - b) / N)
     out = torch.full((N, 7), -1.0)
     # VGA sources: 16-node chunks dealt round-robin (bench.py uses 4096)
     mine = vga_nodes(N, rank, world, chunk=16)
@@ -70,7 +94,7 @@ def _worker(rank, world, port, q):
         cb, ce = int(mine[c0]), int(mine[min(c0 + 16, len(mine)) - 1]) + 1
         out[cb:ce] = torch.from_numpy(om.vga_global(node_begin=cb, node_end=ce)[cb:ce])
     allgather_rows_chunked(out, N, dist, chunk=16)
-    q.put((rank, bins, runs, out.numpy()))
+    q.put((rank, bins, runs, out.numpy(), mode, dec))
     dist.destroy_process_group()
 
 
@@ -93,7 +117,9 @@ def test_two_rank_gloo_matches_single_process():
     om.make_graph()
     g = om.graph()
     ref = om.vga_global()
-    for _, bins, runs, out in res:
+    assert len({r[4] for r in res}) == 1 and res[0][5]["mk_shard_s"] == 2.0 and res[0][5]["exchange_s"] == 0.5
+    assert res[0][4] == "shard"       # 2.0 + 0.5 < 2.0 / (1/2)
+    for _, bins, runs, out, _, _ in res:
         np.testing.assert_array_equal(bins, g["bins"])
         np.testing.assert_array_equal(runs, g["runs"])
         np.testing.assert_array_equal(out.view(np.uint32), ref.view(np.uint32))
