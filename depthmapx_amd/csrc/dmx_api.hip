@@ -220,6 +220,7 @@ struct dmx_graph {
     DevBuf<unsigned long long> uf_tiles;
     DevBuf<unsigned long long> notuf_tiles;
     int64_t uf_count = -1;
+    bool scan_ready = false;   // prepare_uf done (scan order; U_f from the symmetry pass or coverage counting)
     // bottom-up scan order: runs of each node longest-first, indexed by cell
     DevBuf<Run> scan_pool;
     DevBuf<int64_t> cell_scan_start;
@@ -252,6 +253,12 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     PointMapHost& h = *pm->host;
     if (!h.lines_blocked()) h.block_lines();
     if (pm->uploaded_version == pm->version && pm->uploaded_for == ctx->device) return DMX_OK;
+    if (pm->uploaded_for >= 0 && pm->uploaded_for != ctx->device) {
+        // another device's copies: release them (DevBuf::alloc would otherwise reuse the pointers)
+        pm->d_cellw.reset(); pm->d_segs.reset(); pm->d_node_cell.reset(); pm->d_cell_node.reset();
+        pm->d_node_flags.reset(); pm->d_seed_tiles.reset(); pm->d_nonexp_tiles.reset();
+        pm->uploaded_for = -1;
+    }
     const int64_t C = h.cells();
     std::vector<uint32_t> cellw((size_t)C);
     const auto& st = h.state();
@@ -409,6 +416,12 @@ static bool take_cancel(dmx_ctx* ctx) {
     __atomic_store_n(&ctx->h_ctl->cancel, 0, __ATOMIC_SEQ_CST);
     return true;
 }
+// a graph lives on the device of the context that built it
+#define SAME_DEVICE(ctx, g)                                                                          \
+    do {                                                                                             \
+        if ((ctx) && (g) && (g)->ctx && (g)->ctx->device != (ctx)->device)                           \
+            return fail(DMX_ERR_ARG, "graph was built on another device than the context's");        \
+    } while (0)
 #define CANCEL_POINT(ctx)                                                        \
     do {                                                                         \
         if (take_cancel(ctx)) return fail(DMX_ERR_CANCELLED, "operation cancelled"); \
@@ -937,8 +950,11 @@ static int prep_allreduce(dmx_graph* g, void* p, int64_t count, int dtype) {
 }
 // U_f (filled cells that appear in some run: the early-exit universe of every BFS) by range counts,
 // plus the longest-first scan pool.  O(runs) with a few line-prefix passes.
+static int prepare_symmetry(dmx_graph* g);
 static int prepare_uf(dmx_graph* g) {
-    if (g->uf_count >= 0) return DMX_OK;
+    if (g->scan_ready) return DMX_OK;
+    // the symmetry pass computes U_f from its in-set hashes; coverage counting only when it is skipped
+    if (int rc = prepare_symmetry(g)) return rc;
     dmx_ctx* ctx = g->ctx;
     hipStream_t s = ctx->stream;
     PointMapHost& h = *g->pm->host;
@@ -947,30 +963,33 @@ static int prepare_uf(dmx_graph* g) {
     const int64_t C = (int64_t)cols * rows, N = g->nnodes;
     DevBuf<int> cov;
     DevBuf<unsigned long long> cnt;
-    HIPCHK(cov.alloc((size_t)4 * C));
     HIPCHK(cnt.alloc(1));
-    HIPCHK(g->uf_tiles.alloc((size_t)tw * th));
-    HIPCHK(g->notuf_tiles.alloc((size_t)tw * th));
-    HIPCHK(hipMemsetAsync(cov.p, 0, (size_t)4 * C * 4, s));
     HIPCHK(hipMemsetAsync(cnt.p, 0, 8, s));
-    int64_t pb, pe;
-    prep_range(g, pb, pe);
-    if (pe > pb) {
-        hipLaunchKernelGGL(cov_scatter_kernel, dim3((unsigned)std::min<int64_t>(pe - pb, 4096)), dim3(256), 0, s, cols,
-                           rows, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb, g->pool.p, cov.p);
+    const bool have_uf = g->uf_count >= 0;
+    if (!have_uf) {
+        HIPCHK(cov.alloc((size_t)4 * C));
+        HIPCHK(g->uf_tiles.alloc((size_t)tw * th));
+        HIPCHK(g->notuf_tiles.alloc((size_t)tw * th));
+        HIPCHK(hipMemsetAsync(cov.p, 0, (size_t)4 * C * 4, s));
+        int64_t pb, pe;
+        prep_range(g, pb, pe);
+        if (pe > pb) {
+            hipLaunchKernelGGL(cov_scatter_kernel, dim3((unsigned)std::min<int64_t>(pe - pb, 4096)), dim3(256), 0, s,
+                               cols, rows, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb, g->pool.p, cov.p);
+            HIPCHK(hipGetLastError());
+        }
+        if (int rc = prep_allreduce(g, cov.p, (int64_t)4 * C, DMX_I32)) return rc;
+        hipLaunchKernelGGL(cov_lines_kernel, dim3((cols + rows + 127) / 128, 4), dim3(128), 0, s, cols, rows, cov.p);
+        HIPCHK(hipGetLastError());
+        hipLaunchKernelGGL(cov_tiles_kernel, dim3((tw * th + 255) / 256), dim3(256), 0, s, cols, rows, tw, th,
+                           g->pm->d_cell_node.p, cov.p, g->uf_tiles.p, g->notuf_tiles.p, cnt.p);
         HIPCHK(hipGetLastError());
     }
-    if (int rc = prep_allreduce(g, cov.p, (int64_t)4 * C, DMX_I32)) return rc;
-    hipLaunchKernelGGL(cov_lines_kernel, dim3((cols + rows + 127) / 128, 4), dim3(128), 0, s, cols, rows, cov.p);
-    HIPCHK(hipGetLastError());
-    hipLaunchKernelGGL(cov_tiles_kernel, dim3((tw * th + 255) / 256), dim3(256), 0, s, cols, rows, tw, th,
-                       g->pm->d_cell_node.p, cov.p, g->uf_tiles.p, g->notuf_tiles.p, cnt.p);
-    HIPCHK(hipGetLastError());
     // scan pool (node order, runs longest-first inside each node)
     std::vector<int32_t> nr((size_t)std::max<int64_t>(N, 1));
     if (N) HIPCHK(hipMemcpyAsync(nr.data(), g->node_nruns.p, N * 4, hipMemcpyDeviceToHost, s));
-    unsigned long long ufc = 0;
-    HIPCHK(hipMemcpyAsync(&ufc, cnt.p, 8, hipMemcpyDeviceToHost, s));
+    unsigned long long ufc = have_uf ? (unsigned long long)g->uf_count : 0ull;
+    if (!have_uf) HIPCHK(hipMemcpyAsync(&ufc, cnt.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     std::vector<int64_t> ss((size_t)std::max<int64_t>(N, 1));
     int64_t acc = 0;
@@ -990,6 +1009,7 @@ static int prepare_uf(dmx_graph* g) {
     }
     HIPCHK(hipStreamSynchronize(s));
     g->uf_count = (int64_t)ufc;
+    g->scan_ready = true;
     return DMX_OK;
 }
 
@@ -1037,9 +1057,22 @@ static int prepare_symmetry(dmx_graph* g) {
                            g->pm->d_node_cell.p, N, C, diff.p, ho.p, fcount.p, flist.p, kSpecLimit);
         HIPCHK(hipGetLastError());
     }
+    // U_f straight from the in-set hashes (uf_hi_tiles_kernel): no separate coverage pass
+    const int tw = (cols + 7) / 8, th = (rows + 7) / 8;
+    DevBuf<unsigned long long> ufcnt;
+    HIPCHK(ufcnt.alloc(1));
+    HIPCHK(hipMemsetAsync(ufcnt.p, 0, 8, s));
+    HIPCHK(g->uf_tiles.alloc((size_t)tw * th));
+    HIPCHK(g->notuf_tiles.alloc((size_t)tw * th));
+    hipLaunchKernelGGL(uf_hi_tiles_kernel, dim3((tw * th + 255) / 256), dim3(256), 0, s, cols, rows, tw, th,
+                       g->pm->d_cell_node.p, diff.p, g->uf_tiles.p, g->notuf_tiles.p, ufcnt.p);
+    HIPCHK(hipGetLastError());
     int nspec = 0;
+    unsigned long long ufc = 0;
     HIPCHK(hipMemcpyAsync(&nspec, fcount.p, 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(&ufc, ufcnt.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    g->uf_count = (int64_t)ufc;
     g->nspecial = nspec;
     if (nspec == 0) { g->symmetric = 1; return DMX_OK; }
     if (nspec > kSpecLimit) { g->symmetric = 0; return DMX_OK; }
@@ -1504,12 +1537,14 @@ static int refuse_merges(const dmx_graph* g) {
 
 int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
                    int64_t* levels) {
+    SAME_DEVICE(ctx, g);
     if (int rc = refuse_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out, false, levels);
 }
 
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se,
                           float* out_device) {
+    SAME_DEVICE(ctx, g);
     if (int rc = refuse_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out_device, true, nullptr);
 }
@@ -1518,6 +1553,7 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
 // every rank gets the same mix of cheap and expensive sources).  Tile-resolved BFS only.
 int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
                                int64_t n, float* out_device) {
+    SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out_device || (n > 0 && !nodes)) return fail(DMX_ERR_ARG, "bad arguments");
     if (int rc = refuse_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)
@@ -1591,57 +1627,90 @@ static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
     HIPCHK(d_srt.alloc((size_t)nb * std::max<int64_t>(N, 1)));
     HIPCHK(d_out.alloc((size_t)std::max<int64_t>(N, 1) * NO));
     HIPCHK(hipMemcpyAsync(d_flags.p, flags.data(), C, hipMemcpyHostToDevice, s));
+    // Per-workgroup overflow list.  A source whose search outgrows it stops, is listed, and only the
+    // listed sources run again with a 4x list on fewer workgroups (bounded by free device memory).
     int64_t cap = 8 * (nexp + 1) + SD_WIN + 1024;
     if (ANG) cap += 32 * N;   // cells reached at angle 0 are queued too (and re-queued on improvement)
-    for (int attempt = 0; attempt < 4; attempt++) {
-        HIPCHK(d_over.alloc((size_t)nb * cap));
-        HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), s));
-        HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), s));
+    if (const char* e = getenv("DMX_SD_CAP")) cap = std::max<int64_t>(64, atoll(e));   // test hook: retries
+    DevBuf<int64_t> d_list[2];
+    DevBuf<int> d_nfail;
+    HIPCHK(d_list[0].alloc(std::max<int64_t>(se - sb, 1)));
+    HIPCHK(d_list[1].alloc(std::max<int64_t>(se - sb, 1)));
+    HIPCHK(d_nfail.alloc(1));
+    HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), s));
+    double kernel_s = 0.0;
+    int64_t todo = se - sb, rerun = 0;
+    const int64_t* list = nullptr;   // first pass: the range; then the failed sources
+    int cur = 0;
+    for (int attempt = 0; todo > 0; attempt++) {
+        const int64_t nbl = std::max<int64_t>(1, std::min<int64_t>(nb, todo));
+        size_t free_b = 0, total_b = 0;
+        HIPCHK(hipMemGetInfo(&free_b, &total_b));
+        free_b += cached_bytes() + d_over.n * sizeof(unsigned long long);
+        const int64_t cap_max = (int64_t)(free_b * 0.8 / 8.0 / (double)nbl);
+        if (attempt > 0 && cap > cap_max) return fail(DMX_ERR_CAPACITY, "VGA metric/angular: search queue exceeds device memory");
+        if (attempt >= 10) return fail(DMX_ERR_CAPACITY, "VGA metric/angular: queue overflow after retries");
+        d_over.reset();
+        HIPCHK(d_over.alloc((size_t)nbl * std::min(cap, std::max<int64_t>(cap_max, 1))));
+        const int64_t cap_used = std::min(cap, std::max<int64_t>(cap_max, 1));
+        HIPCHK(hipMemsetAsync(d_nfail.p, 0, sizeof(int), s));
         StepDepthParams P;
         P.cols = cols; P.rows = rows; P.flags = d_flags.p; P.cell_node = g->pm->d_cell_node.p;
         P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
         P.key = d_key.p; P.mdist = d_mdist.p; P.cum = d_cum.p; P.lastpix = d_last.p;
-        P.over = d_over.p; P.over_cap = cap; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
+        P.over = d_over.p; P.over_cap = cap_used; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
         HIPCHK(hipEventRecord(ctx->ev0, s));
-        if (se > sb) {
-            hipLaunchKernelGGL(vga_metric_kernel<ANG>, dim3((unsigned)nb), dim3(SD_THREADS), 0, s, P, C, g->pm->d_node_cell.p,
-                               sb, se, gates_only, h.spacing(), radius < 0 ? -1.0 : radius, d_comp.p, d_srt.p,
-                               std::max<int64_t>(N, 1), d_out.p);
-            HIPCHK(hipGetLastError());
-        }
+        hipLaunchKernelGGL(vga_metric_kernel<ANG>, dim3((unsigned)nbl), dim3(SD_THREADS), 0, s, P, C, g->pm->d_node_cell.p,
+                           list ? 0 : sb, list ? todo : se, gates_only, h.spacing(), radius < 0 ? -1.0 : radius, d_comp.p,
+                           d_srt.p, std::max<int64_t>(N, 1), d_out.p, list, d_list[cur].p, d_nfail.p);
+        HIPCHK(hipGetLastError());
         HIPCHK(hipEventRecord(ctx->ev1, s));
         HIPCHK(hipStreamSynchronize(s));
-        int hc[2];
-        HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
-        if (hc[1] & KERR_FRONTIER) { cap *= 4; continue; }
-        if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA metric/angular search failed");
         float ms = 0;
         HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
-        ctx->last_vga_s = ms * 1e-3;
-        if (se > sb)
-            HIPCHK(copy_sync(ctx->stream, out + sb * NO, d_out.p + sb * NO, (size_t)(se - sb) * NO * 4, hipMemcpyDeviceToHost));
-        unsigned long long stv[3];
-        HIPCHK(copy_sync(ctx->stream, stv, ctx->stats.p, sizeof(stv), hipMemcpyDeviceToHost));
-        ctx->last_sd_stats[0] = (long long)stv[0];
-        ctx->last_sd_stats[1] = (long long)stv[1];
-        ctx->last_stats[7] = se - sb;
-        return DMX_OK;
+        kernel_s += ms * 1e-3;
+        int hc[2], nfail = 0;
+        HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+        HIPCHK(copy_sync(ctx->stream, &nfail, d_nfail.p, sizeof(int), hipMemcpyDeviceToHost));
+        if (hc[1] & ~KERR_FRONTIER) return fail(DMX_ERR_CAPACITY, "VGA metric/angular search failed");
+        VLOG("vga %s: attempt %d, %lld sources, list %lld per workgroup x %lld: %.3f s, %d to re-run\n",
+             ANG ? "angular" : "metric", attempt, (long long)todo, (long long)cap_used, (long long)nbl, ms * 1e-3, nfail);
+        if (nfail > 0 && cap_used < cap) return fail(DMX_ERR_CAPACITY, "VGA metric/angular: search queue exceeds device memory");
+        HIPCHK(hipMemsetAsync(ctx->counters.p + 1, 0, sizeof(int), s));
+        rerun += nfail;
+        todo = nfail;
+        list = d_list[cur].p;
+        cur ^= 1;
+        cap *= 4;
     }
-    return fail(DMX_ERR_CAPACITY, "VGA metric: queue overflow after retries");
+    ctx->last_vga_s = kernel_s;   // every attempt counted
+    if (se > sb)
+        HIPCHK(copy_sync(ctx->stream, out + sb * NO, d_out.p + sb * NO, (size_t)(se - sb) * NO * 4, hipMemcpyDeviceToHost));
+    unsigned long long stv[3];
+    HIPCHK(copy_sync(ctx->stream, stv, ctx->stats.p, sizeof(stv), hipMemcpyDeviceToHost));
+    ctx->last_sd_stats[0] = (long long)stv[0];
+    ctx->last_sd_stats[1] = (long long)stv[1];
+    ctx->last_stats[7] = se - sb;
+    ctx->last_stats[8] = rerun;   // sources re-run with a larger overflow list
+    return DMX_OK;
 }
 
 int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    SAME_DEVICE(ctx, g);
     if (int rc = refuse_merges(g)) return rc;
     return vga_search_all<false>(ctx, g, radius, gates_only, sb, se, out);
 }
 
 int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
+    SAME_DEVICE(ctx, g);
     if (int rc = refuse_merges(g)) return rc;
     return vga_search_all<true>(ctx, g, radius, gates_only, sb, se, out);
 }
 
 // ---------------------------------------------------------------- VGA visual local
 int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t sb, int64_t se, float* out) {
+    SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
@@ -1945,11 +2014,13 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
 }
 
 int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    SAME_DEVICE(ctx, g);
     if (int rc = refuse_merges(g)) return rc;
     return stepdepth_impl<false>(ctx, g, sel_cells, nsel, out);
 }
 
 int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    SAME_DEVICE(ctx, g);
     if (int rc = refuse_merges(g)) return rc;
     return stepdepth_impl<true>(ctx, g, sel_cells, nsel, out);
 }
@@ -1967,6 +2038,7 @@ int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {
 // extent short-cut only skips already-covered suffixes); contextfilled odd cells get their level but
 // are not expanded.  Runs on the tile-resolved BFS in seed mode (one workgroup).
 int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
+    SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
     if (int rc = refuse_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)

@@ -61,7 +61,7 @@ struct SdShared {
     unsigned long long red[SD_THREADS / 64];
     unsigned long long gmin;        // lower bound of the keys in the overflow list
     long long nover;                // entries in the overflow list
-    int nwin, nchunk, cut_ok, pad;
+    int nwin, nchunk, cut_ok, ovf;  // ovf: the overflow list overflowed (sticky for the search)
     unsigned long long cur;         // key being popped
     float cut_w;                    // refill window width (distance units)
     unsigned long long keep;
@@ -77,7 +77,7 @@ __device__ __forceinline__ void sd_push(SdShared& S, const StepDepthParams& P, u
     }
     const long long o = atomicAdd((unsigned long long*)&S.nover, 1ull);
     if (o < P.over_cap) P.over[o] = k;
-    else atomicOr(P.error, KERR_FRONTIER);
+    else { atomicOr(P.error, KERR_FRONTIER); S.ovf = 1; }
     atomicMin(&S.gmin, k);
 }
 
@@ -181,7 +181,7 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
     int& s_idx = S.idx;
     int& s_cnt = S.cnt;
     if (tid == 0) {
-        S.nwin = 0; S.nchunk = 0; S.gmin = SD_INF; S.nover = 0; S.cut_w = 4.0f;
+        S.nwin = 0; S.nchunk = 0; S.gmin = SD_INF; S.nover = 0; S.cut_w = 4.0f; S.ovf = 0;
     }
     __syncthreads();
     // the selected cells enter at distance 0 (vgametricdepth.cpp:45-47)
@@ -208,6 +208,7 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
         }
         __syncthreads();
         const unsigned long long ku = S.cur;
+        if (S.ovf) break;   // the overflow list overflowed: the caller re-runs this search
         if (ku == SD_INF || ku >= S.gmin) {
             if (S.nover == 0 && ku == SD_INF) break;
             // ---- refill: flush the window into the overflow list, then take back the smallest keys
@@ -215,7 +216,7 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
             for (int i = tid; i < nw; i += SD_THREADS) {
                 const long long o = atomicAdd((unsigned long long*)&S.nover, 1ull);
                 if (o < P.over_cap) P.over[o] = S.win[i];
-                else atomicOr(P.error, KERR_FRONTIER);
+                else { atomicOr(P.error, KERR_FRONTIER); S.ovf = 1; }
                 atomicMin(&S.gmin, S.win[i]);
             }
             __syncthreads();
@@ -653,7 +654,8 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
                                                                 int64_t sb, int64_t se, int gates_only, double spacing,
                                                                 double radius, unsigned long long* comp_all,
                                                                 unsigned long long* srt_all, int64_t nstride,
-                                                                float* out) {
+                                                                float* out, const int64_t* src_list,
+                                                                int64_t* fail_list, int* fail_count) {
     __shared__ SdShared S;
     __shared__ int hoff[VM_BUCKETS + 1];
     __shared__ int cur[VM_BUCKETS];
@@ -673,7 +675,10 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
     unsigned long long* srt = srt_all + b * nstride;
     unsigned long long popped = 0, refills = 0;
     unsigned relaxed = 0;
-    for (int64_t src = sb + blockIdx.x; src < se; src += gridDim.x) {
+    // sources sb + i, or src_list[i] on a re-run of the sources whose overflow list overflowed
+    const int64_t nwork = src_list ? se : se - sb;
+    for (int64_t i = blockIdx.x; i < nwork; i += gridDim.x) {
+        const int64_t src = src_list ? src_list[i] : sb + i;
         constexpr int NO = ANG ? 3 : 4;
         float* o = out + src * NO;
         if (gates_only) {
@@ -689,6 +694,11 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
         if (tid == 0) { s_src = node_cell[src]; s_n = 0; s_pos = 0; s_maxd = 0u; }
         __syncthreads();
         sd_run<ANG>(S, P, &s_src, 1, spacing, radius, popped, refills, relaxed);
+        __syncthreads();
+        if (S.ovf) {   // this source only: re-run by the host with a larger list
+            if (tid == 0) fail_list[atomicAdd(fail_count, 1)] = src;
+            continue;
+        }
         const int sx = s_src / P.rows, sy = s_src % P.rows;
         // reached cells within the radius: count and largest distance
         int n = 0;

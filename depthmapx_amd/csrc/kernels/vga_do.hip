@@ -571,6 +571,30 @@ __global__ void cov_tiles_kernel(int cols, int rows, int tw, int th, const int32
     if (w) atomicAdd(count, (unsigned long long)__popcll(w));
 }
 
+// U_f from the in-set hashes of the symmetry pass (hi4 = the four range-added weight arrays after
+// their line prefix sums): a filled cell lies on some run iff some node sees it, i.e. its in-set is
+// non-empty, i.e. HI = the sum of its in-neighbours' 64-bit weights is non-zero -- exact but for the
+// 2^-64 chance per cell on which the symmetry certificate already rests.  Replaces the coverage
+// counting pass (cov_scatter / cov_lines), one O(runs) scatter less per graph.
+__global__ void uf_hi_tiles_kernel(int cols, int rows, int tw, int th, const int32_t* cell_node,
+                                   const unsigned long long* hi4, unsigned long long* uf, unsigned long long* notuf,
+                                   unsigned long long* count) {
+    const int64_t C = (int64_t)cols * rows;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= tw * th) return;
+    const int tx = t % tw, ty = t / tw;
+    unsigned long long w = 0;
+    for (int b = 0; b < 64; b++) {
+        const int x = tx * 8 + (b & 7), y = ty * 8 + (b >> 3);
+        if (x >= cols || y >= rows) continue;
+        const int64_t c = (int64_t)x * rows + y;
+        if (cell_node[c] >= 0 && (hi4[c] + hi4[C + c] + hi4[2 * C + c] + hi4[3 * C + c]) != 0ull) w |= 1ull << b;
+    }
+    uf[t] = w;
+    notuf[t] = ~w;
+    if (w) atomicAdd(count, (unsigned long long)__popcll(w));
+}
+
 // Scan pool: each node's runs in bottom-up scan order.  Runs are split into the 8 angular groups of
 // 4 bins (bins 4g..4g+3), ordered longest-first inside a group (16 log2-length buckets), and the
 // groups are interleaved round-robin: the first 8 entries are the longest run of each direction, so

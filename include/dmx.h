@@ -181,7 +181,7 @@ int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
 int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t src_begin, int64_t src_end, float* out);
 /* Multi-GPU share of the VGA preparation (no reference counterpart: the reference prepares nothing;
  * this splits our own O(runs) pre-passes).  Every rank holds the whole graph; the per-node scatters
- * (covered-cell counts, in-set sums, tile-visibility rows) then run over nodes [node_begin, node_end)
+ * (in-set hash sums, tile-visibility rows) then run over nodes [node_begin, node_end)
  * only and each partial device buffer is handed to fn, which must sum it in place over all ranks
  * (an all-reduce SUM of `count` elements of dtype DMX_I32 / DMX_I64, returning 0 on success) before
  * returning.  Every rank must call this with the same fn semantics before its first VGA call on g;

@@ -119,6 +119,19 @@ def test_1000_vga_kernels_agree_at_size(big1000, ctx, monkeypatch):
     np.testing.assert_array_equal(a[b:e].view(np.uint32), c[b:e].view(np.uint32))
 
 
+def test_1000_vga_per_tile_summary_path_agrees(big1000, ctx, monkeypatch):
+    """The coarser per-tile frontier summary (what grids above ~1010^2 use when the line-resolved
+    summaries no longer fit the LDS), forced at 1000^2 with DMX_VGA_RB=0: bit-identical to the
+    default line-summary run on a block of 256 sources."""
+    pm, g, om = big1000
+    N = g.info()["nnodes"]
+    b, e = 2 * N // 3, 2 * N // 3 + 256
+    a = g.vga_visual_global(src_begin=b, src_end=e)
+    monkeypatch.setenv("DMX_VGA_RB", "0")
+    c = g.vga_visual_global(src_begin=b, src_end=e)
+    np.testing.assert_array_equal(a[b:e].view(np.uint32), c[b:e].view(np.uint32))
+
+
 @pytest.fixture(scope="module")
 def big2000(ctx):
     from pyoracle import OracleMap
@@ -166,3 +179,21 @@ def test_2000_metric_stepdepth_batched_equals_serial(big2000, ctx, monkeypatch):
     st = pm.state()
     k_sel = int(np.searchsorted(np.nonzero(st & FILLED)[0], cell))
     assert a[k_sel, 1] == 0.0 and a[k_sel, 2] == 0.0
+
+
+def test_2000_vga_sources_match_oracle(big2000, ctx):
+    """configs[4] grid (2000^2, above the tile kernel's 1024^2 limit: the direction-optimising kernel
+    with its bitmaps in HBM): 8 seeded sources of VGA global against the oracle's BFS over the same
+    graph (node count exact, floats within 1e-6)."""
+    pm, g, om = big2000
+    N = g.info()["nnodes"]
+    b = int(np.random.default_rng(2000).integers(0, N - 8))
+    out = g.vga_visual_global(src_begin=b, src_end=b + 8)
+    assert ctx.last_stats()["vga_kernel"] != "tile-resolved"
+    full = g.copy(runs=True)
+    om.set_graph_view(full["bins"], full["runs"])
+    ref = om.vga_global(node_begin=b, node_end=b + 8, threads=8)
+    got, want = out[b:b + 8].astype(np.float64), ref[b:b + 8].astype(np.float64)
+    np.testing.assert_array_equal(got[:, 5], want[:, 5])
+    assert (np.abs(got - want) <= 1e-6 * np.maximum(1.0, np.abs(want))).all()
+    assert (want[:, 5] > 0.5 * N).all()
