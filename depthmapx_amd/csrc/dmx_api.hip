@@ -579,11 +579,26 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     DevBuf<int64_t> fail_list, node_list;
     HIPCHK(fail_list.alloc(std::max<int64_t>(n, 1)));
     HIPCHK(node_list.alloc(std::max<int64_t>(n, 1)));
-    for (int restart = 0; restart < 3; restart++) {
+    // Run pool size.  The worst case above (6 runs per depth per source) is ~1.4x the real count at
+    // 1000^2 and, at 2000^2, would take the memory a following VGA needs for its scan order.  A first
+    // pass over an evenly spaced sample of sources measures the runs per source; the pool takes 1.25x
+    // that plus 64 per source.  An overflow still re-runs everything with a doubled pool.
+    const int64_t kSample = 4096;
+    bool sampling = n >= 16 * kSample && !getenv("DMX_MK_NOSAMPLE");
+    double mk_total_s = 0.0;
+    for (int restart = 0; restart < 4; restart++) {
         // one full pass, then re-runs of only the sources that overflowed an LDS / staging capacity
         double kernel_s = 0.0;
         int64_t list_n = -1;   // -1: the whole range
         bool pool_over = false;
+        const int64_t pool_cap_full = pool_cap;
+        if (sampling) {
+            std::vector<int64_t> sl((size_t)kSample);
+            for (int64_t i = 0; i < kSample; i++) sl[i] = node_begin + (i * n) / kSample + n / (2 * kSample);
+            HIPCHK(hipMemcpyAsync(node_list.p, sl.data(), kSample * 8, hipMemcpyHostToDevice, ctx->stream));
+            list_n = kSample;
+            pool_cap = kSample * std::max<int64_t>(64, 6 * (int64_t)D);
+        }
         HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 16 * sizeof(int), ctx->stream));
         HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), ctx->stream));
         size_t lds0 = makegraph_lds(gcap, bcap, D);
@@ -682,7 +697,19 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             list_n = nfail;
             if (attempt == 7) return fail(DMX_ERR_CAPACITY, "makegraph capacities exceeded after retries");
         }
-        if (pool_over) continue;
+        if (sampling) {
+            unsigned long long used = 0;
+            HIPCHK(copy_sync(ctx->stream, &used, ctx->counters.p + 2, 8, hipMemcpyDeviceToHost));
+            sampling = false;
+            mk_total_s += kernel_s;
+            if (pool_over) { pool_cap = pool_cap_full; continue; }   // no estimate: the worst-case pool
+            const double per_src = (double)used / (double)kSample;
+            pool_cap = std::min<int64_t>(pool_cap_full, (int64_t)(1.25 * per_src * (double)n) + 64 * n + 4096);
+            VLOG("makegraph: sample of %lld sources, %.1f runs each -> pool %.3f GB\n", (long long)kSample, per_src,
+                 pool_cap * 8.0 / 1e9);
+            continue;
+        }
+        if (pool_over) { mk_total_s += kernel_s; continue; }
         HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
         if (n > 0) {
             hipLaunchKernelGGL(gridconn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, h.rows(),
@@ -715,7 +742,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         ctx->last_stats[0] = (long long)st[0];
         ctx->last_stats[1] = (long long)st[1];
         ctx->last_stats[2] = (long long)used;
-        ctx->last_mk_s = kernel_s;
+        ctx->last_mk_s = mk_total_s + kernel_s;   // every pass counted (sample, overflow re-runs)
         g->nruns = (int64_t)used;
         VLOG("makegraph: kernels %.3f s, total %.3f s\n", kernel_s, now_s() - t_start);
         *out = g.release();
@@ -784,16 +811,29 @@ int dmx_graph_copy_range(dmx_graph* g, int64_t kb, int64_t ke, float* attrs, int
     if (nruns_out) *nruns_out = acc;
     if (runs) {
         if (runs_cap >= 0 && acc > runs_cap) return fail(DMX_ERR_ARG, "runs buffer too small for the node range");
-        // node-ordered copy (the pool is in completion order)
+        // node-ordered copy (the pool is in completion order), gathered in node batches of at most
+        // kChunk runs so that the staging buffer stays small next to a 90 GB graph
+        const int64_t kChunk = (int64_t)1 << 29;   // 4 GiB of runs
         DevBuf<int64_t> d_dst;
         DevBuf<Run> d_runs;
         HIPCHK(d_dst.alloc(n));
-        HIPCHK(d_runs.alloc(std::max<int64_t>(acc, 1)));
-        HIPCHK(copy_sync(st, d_dst.p, dst.data(), n * 8, hipMemcpyHostToDevice));
-        hipLaunchKernelGGL(gather_runs_kernel, dim3((unsigned)n), dim3(256), 0, st, g->pool.p,
-                           g->node_run_start.p + kb, g->node_nruns.p + kb, d_dst.p, n, d_runs.p);
-        HIPCHK(hipGetLastError());
-        if (acc) HIPCHK(copy_sync(st, runs, d_runs.p, acc * sizeof(Run), hipMemcpyDeviceToHost));
+        HIPCHK(d_runs.alloc(std::max<int64_t>(std::min(acc, kChunk), 1)));
+        int64_t k0 = 0;
+        while (k0 < n) {
+            int64_t k1 = k0;
+            const int64_t base = dst[k0];
+            while (k1 < n && (k1 == k0 || (k1 + 1 < n ? dst[k1 + 1] : acc) - base <= kChunk)) k1++;
+            const int64_t cnt = (k1 < n ? dst[k1] : acc) - base;
+            std::vector<int64_t> rel((size_t)(k1 - k0));
+            for (int64_t k = k0; k < k1; k++) rel[k - k0] = dst[k] - base;
+            if (cnt > (int64_t)d_runs.n) HIPCHK(d_runs.alloc(cnt));   // one node above the chunk size
+            HIPCHK(copy_sync(st, d_dst.p, rel.data(), (k1 - k0) * 8, hipMemcpyHostToDevice));
+            hipLaunchKernelGGL(gather_runs_kernel, dim3((unsigned)(k1 - k0)), dim3(256), 0, st, g->pool.p,
+                               g->node_run_start.p + kb + k0, g->node_nruns.p + kb + k0, d_dst.p, k1 - k0, d_runs.p);
+            HIPCHK(hipGetLastError());
+            if (cnt) HIPCHK(copy_sync(st, runs + base * 4, d_runs.p, cnt * sizeof(Run), hipMemcpyDeviceToHost));
+            k0 = k1;
+        }
     }
     return DMX_OK;
 }

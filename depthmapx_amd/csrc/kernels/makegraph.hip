@@ -183,6 +183,15 @@ __device__ __forceinline__ Run make_run(int q, int cx, int cy, int ind, int ds, 
     return r;
 }
 
+// One wave per workgroup: lanes exchanging data through LDS need only an ordering point (the wave's LDS
+// instructions execute in order); __syncthreads would also drain every outstanding global load and
+// store (vmcnt(0)) several times per depth.  Exchanges through global memory keep __syncthreads.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // per-wave counters in HBM scratch (one wave per workgroup reads back its own stores: workgroup scope keeps
 // them in L1/L2; agent scope would write every store through to memory and miss L2 on every load)
 __device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
@@ -416,7 +425,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     if (valid && first) L.bsorted[rank] = make_double2(bx, by);
                     double gx = 0.0, gy = 0.0;
                     if (lane < ng) { const double2 v = L.gaps[lane]; gx = v.x; gy = v.y; }
-                    __syncthreads();
+                    wave_sync();
                     double sx = 0.0, sy = 0.0;
                     if (lane < nu) { const double2 v = L.bsorted[lane]; sx = v.x; sy = v.y; }
                     // sparkSieve2::collectgarbage (sparksieve2.cpp:89-132), wave-uniform
@@ -453,12 +462,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         no += ng - gi - 1;
                     }
                     if (no > gcap) { if (lane == 0) atomicOr(P.error, KERR_GAP_CAPACITY); failed = true; break; }
-                    __syncthreads();
+                    wave_sync();
                     ng = no;
                     for (int i = lane; i < ng; i += 64) L.gaps[i] = L.gaps2[i];
                     if (lane == 0) L.misc[1] = 0;
-                    __syncthreads();
+                    wave_sync();
                 } else if (nb > 0) {
+                    __syncthreads();   // spilled blocks written by other lanes live in HBM: drain the stores
                     // std::sort (start asc, end desc) + std::unique: first-occurrence flags, then
                     // each distinct block lands at its rank among the distinct blocks.  Blocks past
                     // the LDS capacity live in this wave's HBM spill area (rare: long walls across
@@ -585,7 +595,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     carryF = max(carryF, __shfl(incl, 63));
                 }
                 if (lane == 0) L.gpre[ng] = carryT;
-                __syncthreads();
+                wave_sync();
                 const int T = carryT;
                 examined += (unsigned long long)T;
                 MK_T(1);
@@ -666,8 +676,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             }
                             const double dx = (double)(hx - cx), dy = (double)(hy - cy);
                             this_dist = sqrt(dx * dx + dy * dy) * sp;
-                            atomicAdd(&L.binc[bin], 1u);
-                            atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
+                        }
+                        // per-bin node count and farthest distance (Bin::m_node_count / m_distance): the
+                        // lanes run in increasing ind and at one depth the distance grows with ind, so a
+                        // bin's farthest cell is its highest lane -- one ballot per bin class of the
+                        // octant, updated by lane 0, instead of same-address LDS atomics from every lane
+                        // (a bin outside the 5 classes is flagged KERR_BIN_MISMATCH below)
+                        {
+                            const unsigned fb = __float_as_uint((float)this_dist);
+#pragma unroll
+                            for (int kk = 0; kk < 5; kk++) {
+                                const unsigned long long mb = ballot(add && bin == obin[kk]);
+                                if (mb) {
+                                    const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)fb, 63 - __clzll((long long)mb));
+                                    if (lane == 0) {
+                                        L.binc[obin[kk]] += (unsigned)__popcll(mb);
+                                        L.bfar[obin[kk]] = max(L.bfar[obin[kk]], v);
+                                    }
+                                }
+                            }
                         }
                         MK_T(3);
                         if (P.exact_moments) {
@@ -758,7 +785,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     }
                     pf_ok = true;
                 }
-                __syncthreads();
+                wave_sync();
             }
             if (failed) break;
             // ---------------- flush open rows, then place this octant's runs canonically
