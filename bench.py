@@ -369,7 +369,7 @@ def main():
         tw, th = (info["cols"] + 7) // 8, (info["rows"] + 7) // 8
         levels = stats.get("vga_bottom_up_levels", 0) + stats.get("vga_top_down_levels", 0)
         # run records tested + V/X reset and per-level read/write + the tile-visibility rows read by
-        # phase C (tvis and ftvis) and phase B1 (tile-to-tile rows)
+        # phase C (tvis and ftvis) and phase B (tile-to-tile rows)
         tvw = th * ((tw + 63) // 64)
         vga_bytes = (8 * stats.get("vga_runs_expanded", 0) + 16 * tw * th * nsrc + 32 * tw * th * levels +
                      2 * stats.get("vga_tvis_bytes", 0) + 8 * tvw * stats.get("vga_b_tiles", 0))

@@ -176,7 +176,7 @@ struct dmx_ctx {
     long long phase_cycles[5] = {0, 0, 0, 0, 0};   // tile BFS: level 1, A, B, C, bookkeeping (sum over workgroups)
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
-    long long last_stats[32] = {};
+    long long last_stats[40] = {};
     // progress / cancel (dmx_ctx_set_progress, dmx_ctx_cancel): host-mapped block polled by the kernels
     DmxCtl* h_ctl = nullptr;
     DmxCtl* d_ctl = nullptr;
@@ -450,7 +450,7 @@ int dmx_ctx_free(dmx_ctx* c) {
 
 int dmx_ctx_last_stats(dmx_ctx* c, int64_t* out, int n) {
     if (!c || !out) return fail(DMX_ERR_ARG, "bad arguments");
-    for (int i = 0; i < n && i < 32; i++) out[i] = c->last_stats[i];
+    for (int i = 0; i < n && i < 40; i++) out[i] = c->last_stats[i];
     return DMX_OK;
 }
 
@@ -580,11 +580,15 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     HIPCHK(fail_list.alloc(std::max<int64_t>(n, 1)));
     HIPCHK(node_list.alloc(std::max<int64_t>(n, 1)));
     // Run pool size.  The worst case above (6 runs per depth per source) is ~1.4x the real count at
-    // 1000^2 and, at 2000^2, would take the memory a following VGA needs for its scan order.  A first
-    // pass over an evenly spaced sample of sources measures the runs per source; the pool takes 1.25x
-    // that plus 64 per source.  An overflow still re-runs everything with a doubled pool.
+    // 1000^2; at 2000^2 it exceeds the device, and clamping it to the free memory would leave nothing
+    // for the scan order a following VGA needs.  When the worst case takes more than 40 % of the free
+    // memory, a first pass over an evenly spaced sample of sources measures the runs per source and
+    // the pool takes 1.25x that plus 64 per source (0.08 s at 1000^2, so skipped there).  An overflow
+    // still re-runs everything with a doubled pool.
     const int64_t kSample = 4096;
-    bool sampling = n >= 16 * kSample && !getenv("DMX_MK_NOSAMPLE");
+    const bool big_pool = (double)pool_cap * sizeof(Run) > 0.4 * (double)(free_b + cached_bytes());
+    bool sampling = !getenv("DMX_MK_NOSAMPLE") &&
+                    ((n >= 16 * kSample && big_pool) || (n >= kSample && getenv("DMX_MK_SAMPLE")));   // test hook
     double mk_total_s = 0.0;
     for (int restart = 0; restart < 4; restart++) {
         // one full pass, then re-runs of only the sources that overflowed an LDS / staging capacity

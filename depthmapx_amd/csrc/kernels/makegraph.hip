@@ -676,25 +676,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             }
                             const double dx = (double)(hx - cx), dy = (double)(hy - cy);
                             this_dist = sqrt(dx * dx + dy * dy) * sp;
-                        }
-                        // per-bin node count and farthest distance (Bin::m_node_count / m_distance): the
-                        // lanes run in increasing ind and at one depth the distance grows with ind, so a
-                        // bin's farthest cell is its highest lane -- one ballot per bin class of the
-                        // octant, updated by lane 0, instead of same-address LDS atomics from every lane
-                        // (a bin outside the 5 classes is flagged KERR_BIN_MISMATCH below)
-                        {
-                            const unsigned fb = __float_as_uint((float)this_dist);
-#pragma unroll
-                            for (int kk = 0; kk < 5; kk++) {
-                                const unsigned long long mb = ballot(add && bin == obin[kk]);
-                                if (mb) {
-                                    const unsigned v = (unsigned)__builtin_amdgcn_readlane((int)fb, 63 - __clzll((long long)mb));
-                                    if (lane == 0) {
-                                        L.binc[obin[kk]] += (unsigned)__popcll(mb);
-                                        L.bfar[obin[kk]] = max(L.bfar[obin[kk]], v);
-                                    }
-                                }
-                            }
+                            atomicAdd(&L.binc[bin], 1u);
+                            atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
                         }
                         MK_T(3);
                         if (P.exact_moments) {

@@ -85,8 +85,8 @@ class Context:
         return dict(zip(["level1", "tile_common", "heads", "hard", "bookkeeping"], (int(v) for v in out)))
 
     def last_stats(self):
-        out = np.zeros(32, dtype=np.int64)
-        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 32))
+        out = np.zeros(40, dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 40))
         keys = ["mk_cells_examined", "mk_visible_pairs", "mk_runs", "vga_kernel", "vga_runs_expanded", "vga_levels",
                 "vga_cells_reached", "vga_sources", "vga_fail_cells", "vga_fail_runs", "vga_hbm_bitmaps",
                 "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",

@@ -72,7 +72,7 @@ int dmx_ctx_cancel(dmx_ctx* ctx);
 /* Wall time of the kernels of the last makegraph / vga call, measured with HIP events on the
  * context stream (seconds); kernel_ms receives per-kernel averages. */
 int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
-/* Work counters of the last calls (for roofline accounting), up to 24 entries:
+/* Work counters of the last calls (for roofline accounting), up to 40 entries (engine.py names them):
  * [0] sieve cells examined, [1] visible (source,target) pairs, [2] runs written,
  * [3] VGA kernel used (0 top-down v1, 1 direction-optimising restricted to top-down,
  *     2 direction-optimising, 3 tile-resolved) | nodes needing exact in-set corrections << 8,

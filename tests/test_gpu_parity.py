@@ -373,6 +373,16 @@ def test_makegraph_capacity_retries_are_exact(ctx, monkeypatch, gcap, bcap, spil
     _assert_graph_equal(g.copy(runs=True), A, True)
 
 
+def test_makegraph_sampled_pool_is_exact(ctx, monkeypatch):
+    """Run-pool sizing from a sample pass (forced with DMX_MK_SAMPLE; automatic when the worst-case pool
+    would take over 40 % of the device, e.g. 2000^2): the graph is bit-identical to the reference's."""
+    meta, A = load_case("syn256mk")
+    monkeypatch.setenv("DMX_MK_SAMPLE", "1")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    _assert_graph_equal(g.copy(runs=True), A, meta["full_runs"])
+
+
 def test_makegraph_certified_moments_equal_serial_chains(ctx, monkeypatch):
     """The first makeGraph pass sums the moments in parallel (double-double) and keeps a float only
     when the reference's serial FP64 chain provably rounds to it; the rest are re-run with the
