@@ -144,6 +144,7 @@ def cpu_baseline(region, lines, spacing, fill, g, budget_s, seed=2026, stepdepth
     mk_nodes = np.sort(rng.choice(N, size=min(200, N), replace=False))
     bfs_nodes = np.sort(rng.choice(N, size=min(20, N), replace=False))
     T = cpu_threads()
+    print("[bench] CPU baseline: makeGraph sample", file=sys.stderr, flush=True)
     t0 = time.perf_counter()
     mk_secs = om.make_graph_sample(mk_nodes, threads=1)
     mk1_wall = time.perf_counter() - t0
@@ -163,6 +164,7 @@ def cpu_baseline(region, lines, spacing, fill, g, budget_s, seed=2026, stepdepth
                          "%.2f s; metric step depth not sampled (CPU rate overstated)" % (len(mk_nodes), mk1_wall, T,
                                                                                           mkT_wall))
     else:
+        print("[bench] CPU baseline: graph copy + BFS sample", file=sys.stderr, flush=True)
         gn = g.copy(runs=True)
         om.set_graph_view(gn["bins"], gn["runs"])
         # all S sources on T threads (each source's own time recorded on its thread), then the first of
@@ -334,9 +336,16 @@ def main():
             stats.update(st)
         return g
 
+    def progress(what):
+        # one stderr line per step (stdout carries only the JSON result line)
+        if rank == 0:
+            print("[bench] %s %.1f s" % (what, time.perf_counter() - t_start), file=sys.stderr, flush=True)
+
+    t_start = time.perf_counter()
     for w in range(args.warmup):
         g = step(False)
         del g
+        progress("warm-up step %d/%d" % (w + 1, args.warmup))
         if w == 0 and mk_auto is not None:
             mk_mode, dec = choose_mk_mode(dist, dev, world, mk_auto["mk_shard_s"], mk_auto["blob_s"] +
                                           mk_auto["allgather_s"] + mk_auto["assemble_s"], (e - b) / max(N, 1))
@@ -350,6 +359,7 @@ def main():
         g = step(True)
         if i != args.steps - 1:
             del g
+        progress("step %d/%d" % (i + 1, args.steps))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
