@@ -520,7 +520,7 @@ int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, i
 // makeGraph kernel variant: VGPR budget (waves per SIMD) chosen at launch (DMX_MK_WPE, default 5).
 // The kernel is latency-bound (one wave walks one source's sieve depth by depth), so waves beat
 // registers: at 1000^2, 3 waves/SIMD 6.9 s, 4: 5.7 s, 5: 5.3 s (96 VGPRs, some spills), 6: 5.4 s.
-typedef void (*mk_kernel_t)(MakeGraphParams);
+typedef void (*mk_kernel_t)(const MakeGraphParams*);
 static mk_kernel_t mk_kernel() {
     const char* e = getenv("DMX_MK_WPE");
     const int w = e ? atoi(e) : 5;
@@ -577,6 +577,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     int64_t pool_cap = std::max<int64_t>(n * std::max<int64_t>(64, 6 * (int64_t)D), 1024);
     ctx->last_mk_s = 0;
     DevBuf<int64_t> fail_list, node_list;
+    DevBuf<MakeGraphParams> dP;   // kernel parameters in device memory (see makegraph_kernel)
     HIPCHK(fail_list.alloc(std::max<int64_t>(n, 1)));
     HIPCHK(node_list.alloc(std::max<int64_t>(n, 1)));
     // Run pool size.  The worst case above (6 runs per depth per source) is ~1.4x the real count at
@@ -671,7 +672,10 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.exact_moments = (list_n >= 0 || getenv("DMX_MK_EXACT")) ? 1 : 0;
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
-                hipLaunchKernelGGL(mk_kernel(), dim3((unsigned)waves), dim3(64), lds, ctx->stream, P);
+                HIPCHK(dP.alloc(1));
+                HIPCHK(hipMemcpyAsync(dP.p, &P, sizeof(P), hipMemcpyHostToDevice, ctx->stream));
+                hipLaunchKernelGGL(mk_kernel(), dim3((unsigned)waves), dim3(64), lds, ctx->stream,
+                                   (const MakeGraphParams*)dP.p);
                 HIPCHK(hipGetLastError());
             }
             HIPCHK(hipEventRecord(ctx->ev1, ctx->stream));
@@ -1303,7 +1307,11 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     P.ctl = ctx->d_ctl;
     ctx->h_ctl->progress = 0;
-    hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL, RBM>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream, P);
+    DevBuf<VgaTileParams> dP;
+    HIPCHK(dP.alloc(1));
+    HIPCHK(hipMemcpyAsync(dP.p, &P, sizeof(P), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL, RBM>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream,
+                       (const VgaTileParams*)dP.p);
     HIPCHK(hipGetLastError());
     HIPCHK(wait_progress(ctx, DMX_PHASE_VGA, nsrc, P.chunk));   // hint freed on return
     *blocks_out = blocks;

@@ -262,7 +262,11 @@ struct Lds {
 // WPE: waves per SIMD the register allocation targets; PROF: per-phase clocks (DMX_VERBOSE builds of
 // a run) -- a template flag so that the 8 clock counters cost no registers otherwise
 template <int WPE, bool PROF>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) makegraph_kernel(MakeGraphParams P) {
+// The parameters are read through a pointer to device memory rather than passed by value: the compiler
+// then reloads cold fields with scalar loads instead of keeping ~50 pointers live in SGPRs and
+// spilling them (VGA tile kernel: 210 -> 105 SGPR spills).
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) makegraph_kernel(const MakeGraphParams* __restrict__ PP) {
+    const MakeGraphParams& P = *PP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int gcap = P.gcap, bcap = P.bcap, D = P.dmax;
@@ -397,6 +401,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             // when that adds no block (nb == 0: the gap list is unchanged)
             uint32_t pf_w = 0;
             bool pf_ok = false;
+            int pf_T = 0;   // candidates of the prefetched depth (its ranges are in L.ga / gpre / gc)
             for (;;) {
                 // ---------------- collectgarbage (sparksieve2.cpp:89-132) for the previous depth
                 int nb = L.misc[1];
@@ -549,7 +554,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 // ---------------- sieve2 for this depth (pointdata.cpp:1512-1565)
                 // per-gap visit ranges with the monotone firstind rule
                 int carryF = 0, carryT = 0;
-                if (ng <= 8) {
+                if (ng <= 8 && pf_ok) {
+                    // the previous depth's prefetch already laid out this depth's ranges (same gap list)
+                    carryT = pf_T;
+                } else if (ng <= 8) {
                     // few gaps (the common case): a wave-uniform loop over the gaps in order -- no
                     // cross-lane scans.  F = the largest b of the earlier visited gaps (at least 0).
                     int F = 0, T = 0;
@@ -758,9 +766,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         const int a = max(lo, F1);
                         const int c = (b >= a) ? (b - a + 1) : 0;
                         if (lane >= T1 && lane < T1 + c) pind = a + (lane - T1);
+                        if (lane == 0) {   // depth d1's visit ranges, reused if no block changes the gaps
+                            L.ga[g] = a;
+                            L.gpre[g] = T1;
+                            L.gc[g] = make_int2((int)ceil(z.x * d1), (int)floor(z.y * d1));
+                        }
                         T1 += c;
                         if (b >= lo) F1 = max(F1, b);
                     }
+                    pf_T = T1;
                     if (pind >= 0) {
                         int px, py;
                         octant_cell(q, cx, cy, d1, pind, px, py);

@@ -358,7 +358,8 @@ __device__ __forceinline__ bool special_hit(const VgaTileParams& P, const FView&
 // SPECIAL = false: the graph has no asymmetric nodes (every U_f cell is regular), no exact path.
 // RBM: line-resolved summaries RB / CB in LDS (replace Fsc; need ~32 KB more LDS, grids <= ~1010^2).
 template <int NT, bool SPECIAL, bool RBM>
-__global__ void __launch_bounds__(NT) vga_tile_kernel(VgaTileParams P) {
+__global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __restrict__ PP) {
+    const VgaTileParams& P = *PP;
     extern __shared__ __attribute__((aligned(16))) unsigned long long F[];
     __shared__ TileShared S;
     constexpr int NW = NT / 64;
