@@ -27,6 +27,8 @@ SIGNATURES = {
     "dmx_pointmap_create": (_i32, [_vp, _dbl, _vp, _i64, _vp]),
     "dmx_pointmap_free": (_i32, [_vp]),
     "dmx_pointmap_fill": (_i32, [_vp, _dbl, _dbl, _vp]),
+    "dmx_pointmap_fill_device": (_i32, [_vp, _vp, _dbl, _dbl, _vp]),
+    "dmx_ctx_last_fill": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_pointmap_info": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "dmx_pointmap_state": (_i32, [_vp, _vp]),
     "dmx_pointmap_cell_lines": (_i32, [_vp, _vp, _vp, _vp]),

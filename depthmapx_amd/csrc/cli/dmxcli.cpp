@@ -467,22 +467,27 @@ struct VisPrep : Mode {
             std::cout << " ok" << std::endl;
             return;
         }
+        std::unique_ptr<Context> C;   // the GPU: makeGraph, and the fill with DMX_FILL=device
         if (!fills.empty()) {
+            // DMX_FILL=device: blockLines + the flood fill on the GPU (dmx_pointmap_fill_device)
+            const char* fe = getenv("DMX_FILL");
+            const bool on_device = fe && std::string(fe) == "device";
+            if (on_device) C.reset(new Context());
             std::cout << "ok\nFilling grid... " << std::flush;
             timed(perf, "Filling grid", [&] {
                 for (auto& p : fills) {
                     int made = 0;
                     // fillGraph (runmethods.cpp:269-277)
-                    check(dmx_pointmap_fill(pm, p.first, p.second, &made));
+                    if (on_device) check(dmx_pointmap_fill_device(C->ctx, pm, p.first, p.second, &made));
+                    else check(dmx_pointmap_fill(pm, p.first, p.second, &made));
                 }
             });
         }
         dmx_graph* g = nullptr;
-        std::unique_ptr<Context> C;   // the GPU is only needed to make the graph
         if (make) {
             std::cout << "ok\nMaking graph... " << std::flush;
             d.state |= MG_ANGULARGRAPH;   // MetaGraph::makeGraph (mgraph.cpp:264-284)
-            C.reset(new Context());
+            if (!C) C.reset(new Context());
             timed(perf, "Making graph", [&] { check(dmx_makegraph(C->ctx, pm, maxvis, boundary ? 1 : 0, 0, -1, &g)); });
             d.view = dmx_view_vga_top(d.view);
         }

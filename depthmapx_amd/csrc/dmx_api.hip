@@ -28,6 +28,8 @@
 #include "kernels/vga_tile.hip"
 #include "kernels/stepdepth.hip"
 #include "kernels/vga_local.hip"
+#include "kernels/fill.hip"
+#include "kernels/vstep.hip"
 
 using namespace dmx;
 
@@ -184,6 +186,8 @@ struct dmx_ctx {
     void* progress_user = nullptr;
     double progress_interval = 0.5;
     hipEvent_t ev_poll = nullptr;
+    double last_fill_s[2] = {0, 0};   // GPU fill: blockLines, flood fill
+    long long last_fill_levels = 0;
 };
 
 struct dmx_pointmap {
@@ -486,6 +490,180 @@ int dmx_pointmap_fill(dmx_pointmap* pm, double x, double y, int* made) {
     pm->version++;
     if (made) *made = (r == 0);
     if (r == 1) return fail(DMX_ERR_OUTSIDE, "Point outside of target region");
+    return DMX_OK;
+}
+
+namespace {
+// scratch for scan_excl: per level, the tile sums and the tile offsets (+ total)
+int64_t scan_scratch_size(int64_t n) {
+    int64_t s = 1;
+    for (;;) {
+        const int64_t t = (n + SCAN_TILE - 1) / SCAN_TILE;
+        s += 2 * t + 1;
+        if (t <= 1) break;
+        n = t;
+    }
+    return s;
+}
+// out[0..n) = exclusive prefix of in, out[n] = total; out must not alias in.
+void scan_excl(hipStream_t st, const int64_t* in, int64_t n, int64_t* out, int64_t* scratch) {
+    if (n <= 0) {
+        (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
+        return;
+    }
+    const int64_t t = (n + SCAN_TILE - 1) / SCAN_TILE;
+    int64_t* tsum = scratch;
+    int64_t* toff = scratch + t;
+    hipLaunchKernelGGL(scan_tile_kernel, dim3((unsigned)t), dim3(SCAN_THREADS), 0, st, in, n, out, tsum);
+    if (t == 1) {
+        hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, st, out, n, (const int64_t*)tsum);
+        return;
+    }
+    scan_excl(st, tsum, t, toff, scratch + 2 * t + 1);
+    hipLaunchKernelGGL(scan_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, n, (const int64_t*)toff);
+    hipLaunchKernelGGL(scan_total_kernel, dim3(1), dim3(1), 0, st, out, n, (const int64_t*)(toff + t));
+}
+unsigned fill_blocks(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + FILL_THREADS - 1) / FILL_THREADS); }
+} // namespace
+
+// PointMap::makePoints on the GPU (kernels/fill.hip): blockLines on the first fill, then the ordered
+// level-synchronous flood fill.  The host model stays the owner of the results (cell states,
+// cropped pieces), so makeGraph and the .graph writer see exactly what the host fill would leave.
+int dmx_pointmap_fill_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y, int* made) {
+    if (!ctx || !pm) return fail(DMX_ERR_ARG, "bad arguments");
+    PointMapHost& h = *pm->host;
+    if (made) *made = 0;
+    int sx = 0, sy = 0;
+    const int r = h.fill_seed(x, y, &sx, &sy);
+    if (r == 1) return fail(DMX_ERR_OUTSIDE, "Point outside of target region");
+    if (r) return DMX_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = ctx->stream;
+    const double t0 = now_s();
+    const int64_t C = h.cells();
+    FillGrid G;
+    G.cols = h.cols();
+    G.rows = h.rows();
+    G.spacing = h.spacing();
+    G.blx = h.bottom_left().x;
+    G.bly = h.bottom_left().y;
+    G.region = h.grid_region();
+    DevBuf<int32_t> d_state, d_segoff;
+    DevBuf<double> d_segs;
+    DevBuf<int64_t> cnt, off, scratch;
+    HIPCHK(d_state.alloc(C));
+    HIPCHK(d_segoff.alloc(C + 1));
+    HIPCHK(cnt.alloc(C + 1));
+    HIPCHK(off.alloc(C + 1));
+    HIPCHK(scratch.alloc(scan_scratch_size(C + 1)));
+    HIPCHK(hipMemcpyAsync(d_state.p, h.state().data(), C * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    int64_t npieces = 0;
+    if (!h.lines_blocked()) {
+        // blockLines: count / scan / emit per line, place / sort / crop per cell
+        const std::vector<double>& draw = h.drawing();
+        const int64_t L = (int64_t)draw.size() / 4;
+        DevBuf<double> d_draw;
+        DevBuf<int64_t> line_off, cursor;
+        DevBuf<int32_t> em_cell, cell_lines;
+        HIPCHK(d_draw.alloc(std::max<int64_t>(4 * L, 1)));
+        HIPCHK(line_off.alloc(L + 1));
+        if (L) HIPCHK(hipMemcpyAsync(d_draw.p, draw.data(), 4 * L * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(cnt.p, 0, (C + 1) * sizeof(int64_t), st));
+        DevBuf<int64_t> lcnt, lscratch;
+        HIPCHK(lcnt.alloc(std::max<int64_t>(L, 1)));
+        HIPCHK(lscratch.alloc(scan_scratch_size(L)));
+        if (L) hipLaunchKernelGGL(rast_count_kernel, dim3(fill_blocks(L)), dim3(FILL_THREADS), 0, st, G, (const double*)d_draw.p, L, lcnt.p);
+        scan_excl(st, lcnt.p, L, line_off.p, lscratch.p);
+        int64_t E = 0;
+        HIPCHK(copy_sync(st, &E, line_off.p + L, sizeof(int64_t), hipMemcpyDeviceToHost));
+        HIPCHK(em_cell.alloc(std::max<int64_t>(E, 1)));
+        HIPCHK(cell_lines.alloc(std::max<int64_t>(E, 1)));
+        HIPCHK(cursor.alloc(C + 1));
+        HIPCHK(hipMemsetAsync(cursor.p, 0, C * sizeof(int64_t), st));
+        if (L) hipLaunchKernelGGL(rast_emit_kernel, dim3(fill_blocks(L)), dim3(FILL_THREADS), 0, st, G, (const double*)d_draw.p, L,
+                                  (const int64_t*)line_off.p, em_cell.p, cnt.p);
+        scan_excl(st, cnt.p, C, off.p, scratch.p);   // off = per-cell line lists
+        if (E) hipLaunchKernelGGL(rast_place_kernel, dim3(fill_blocks(E)), dim3(FILL_THREADS), 0, st, (const int64_t*)line_off.p, L,
+                                  (const int32_t*)em_cell.p, E, (const int64_t*)off.p, cursor.p, cell_lines.p);
+        // cnt is reused for the surviving pieces per cell; cursor (int64) holds their offsets
+        hipLaunchKernelGGL(rast_crop_count_kernel, dim3(fill_blocks(C)), dim3(FILL_THREADS), 0, st, G, (const double*)d_draw.p, C,
+                           (const int64_t*)off.p, cell_lines.p, d_state.p, cnt.p);
+        scan_excl(st, cnt.p, C, cursor.p, scratch.p);
+        HIPCHK(copy_sync(st, &npieces, cursor.p + C, sizeof(int64_t), hipMemcpyDeviceToHost));
+        if (npieces >= (int64_t)INT32_MAX / 4) return fail(DMX_ERR_UNSUPPORTED, "too many occluder pieces");
+        HIPCHK(d_segs.alloc(std::max<int64_t>(4 * npieces, 1)));
+        hipLaunchKernelGGL(rast_crop_write_kernel, dim3(fill_blocks(C)), dim3(FILL_THREADS), 0, st, G, (const double*)d_draw.p, C,
+                           (const int64_t*)off.p, (const int32_t*)cell_lines.p, (const int64_t*)cursor.p, d_segs.p);
+        std::vector<int64_t> off64((size_t)C + 1);
+        std::vector<int32_t> seg_off((size_t)C + 1);
+        std::vector<double> segs((size_t)(4 * npieces));
+        HIPCHK(hipMemcpyAsync(off64.data(), cursor.p, (C + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
+        if (npieces) HIPCHK(hipMemcpyAsync(segs.data(), d_segs.p, 4 * npieces * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        for (int64_t c = 0; c <= C; c++) seg_off[c] = (int32_t)off64[c];
+        HIPCHK(hipMemcpyAsync(d_segoff.p, seg_off.data(), (C + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        h.adopt_blocked(std::move(seg_off), std::move(segs));
+        VLOG("fill: blockLines on the GPU (%lld lines, %lld cell touches, %lld pieces) %.3f s\n", (long long)L, (long long)E,
+             (long long)npieces, now_s() - t0);
+    } else {
+        npieces = (int64_t)h.segs().size() / 4;
+        HIPCHK(d_segs.alloc(std::max<int64_t>(4 * npieces, 1)));
+        HIPCHK(hipMemcpyAsync(d_segoff.p, h.seg_off().data(), (C + 1) * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        if (npieces) HIPCHK(hipMemcpyAsync(d_segs.p, h.segs().data(), 4 * npieces * sizeof(double), hipMemcpyHostToDevice, st));
+    }
+    // the ordered flood fill, one level per round
+    const double t1 = now_s();
+    DevBuf<int32_t> layer[2];
+    DevBuf<uint32_t> owner;
+    DevBuf<uint8_t> blocked, children;
+    HIPCHK(layer[0].alloc(C));
+    HIPCHK(layer[1].alloc(C));
+    HIPCHK(owner.alloc(C));
+    HIPCHK(blocked.alloc(C));
+    HIPCHK(children.alloc(C));
+    HIPCHK(hipMemsetAsync(owner.p, 0xFF, C * sizeof(uint32_t), st));
+    const int64_t c0 = h.index(sx, sy);
+    const int32_t seed_state = CELL_FILLED | (h.state()[c0] & CELL_BLOCKED);
+    const int32_t seed_cell = (int32_t)c0;
+    HIPCHK(hipMemcpyAsync(d_state.p + c0, &seed_state, sizeof(int32_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(layer[0].p, &seed_cell, sizeof(int32_t), hipMemcpyHostToDevice, st));
+    int64_t n = 1, levels = 0;
+    int cur = 0;
+    while (n > 0) {
+        hipLaunchKernelGGL(fill_claim_kernel, dim3(fill_blocks(n)), dim3(FILL_THREADS), 0, st, G, (const int32_t*)d_segoff.p,
+                           (const double*)d_segs.p, (const int32_t*)d_state.p, (const int32_t*)layer[cur].p, n, owner.p, blocked.p);
+        hipLaunchKernelGGL(fill_resolve_kernel, dim3(fill_blocks(n)), dim3(FILL_THREADS), 0, st, G, d_state.p,
+                           (const int32_t*)layer[cur].p, n, (const uint32_t*)owner.p, (const uint8_t*)blocked.p, children.p, cnt.p);
+        scan_excl(st, cnt.p, n, off.p, scratch.p);
+        int64_t n_next = 0;
+        HIPCHK(copy_sync(st, &n_next, off.p + n, sizeof(int64_t), hipMemcpyDeviceToHost));
+        if (n_next)
+            hipLaunchKernelGGL(fill_push_kernel, dim3(fill_blocks(n)), dim3(FILL_THREADS), 0, st, G, d_state.p,
+                               (const int32_t*)layer[cur].p, n, (const uint8_t*)children.p, (const int64_t*)off.p, n_next,
+                               layer[cur ^ 1].p);
+        HIPCHK(hipGetLastError());
+        cur ^= 1;
+        n = n_next;
+        levels++;
+    }
+    std::vector<int32_t> state((size_t)C);
+    HIPCHK(copy_sync(st, state.data(), d_state.p, C * sizeof(int32_t), hipMemcpyDeviceToHost));
+    h.adopt_state(std::move(state));
+    pm->version++;
+    ctx->last_fill_s[0] = t1 - t0;
+    ctx->last_fill_s[1] = now_s() - t1;
+    ctx->last_fill_levels = levels;
+    VLOG("fill: flood fill on the GPU, %lld levels, %lld filled, %.3f s\n", (long long)levels, (long long)h.filled_count(),
+         now_s() - t1);
+    if (made) *made = 1;
+    return DMX_OK;
+}
+
+int dmx_ctx_last_fill(dmx_ctx* ctx, double* block_s, double* fill_s, int64_t* levels) {
+    if (!ctx) return fail(DMX_ERR_ARG, "ctx is NULL");
+    if (block_s) *block_s = ctx->last_fill_s[0];
+    if (fill_s) *fill_s = ctx->last_fill_s[1];
+    if (levels) *levels = ctx->last_fill_levels;
     return DMX_OK;
 }
 
@@ -1773,12 +1951,13 @@ int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t sb, int64_
     PointMapHost& h = *g->pm->host;
     const int cols = h.cols(), rows = h.rows();
     const int tw = (cols + 7) / 8, th = (rows + 7) / 8, nt = tw * th;
-    const size_t lds = (size_t)2 * nt * 8;
-    if (lds > 150 * 1024)
-        return fail(DMX_ERR_UNSUPPORTED, "grid too large for VGA visual local (two tile bitmaps must fit the LDS)");
+    const size_t bm_bytes = (size_t)2 * nt * 8;
+    const bool gbm = bm_bytes > 150 * 1024 || getenv("DMX_VL_GBM");   // the env forces the HBM variant (tests)
+    const size_t lds = gbm ? 0 : bm_bytes;
     hipStream_t s = ctx->stream;
     DevBuf<int32_t> nsz;
     DevBuf<float> d_out;
+    DevBuf<unsigned long long> d_bm;
     HIPCHK(nsz.alloc(std::max<int64_t>(N, 1)));
     HIPCHK(d_out.alloc((size_t)std::max<int64_t>(N, 1) * 3));
     HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * 8, s));
@@ -1788,11 +1967,19 @@ int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t sb, int64_
                            g->node_nruns.p, g->pool.p, nsz.p);
         HIPCHK(hipGetLastError());
         int occ = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_local_kernel, VL_THREADS, lds));
-        const int64_t nb = std::min<int64_t>(se - sb, (int64_t)ctx->num_cu * std::max(occ, 1));
-        hipLaunchKernelGGL(vga_local_kernel, dim3((unsigned)nb), dim3(VL_THREADS), lds, s, cols, rows, tw, th,
+        auto kern = gbm ? vga_local_kernel<true> : vga_local_kernel<false>;
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, VL_THREADS, lds));
+        int64_t nb = std::min<int64_t>(se - sb, (int64_t)ctx->num_cu * std::max(occ, 1));
+        if (gbm) {
+            // bitmap slices within a quarter of the free memory
+            size_t fr = 0, tot = 0;
+            HIPCHK(hipMemGetInfo(&fr, &tot));
+            nb = std::max<int64_t>(1, std::min<int64_t>(nb, (int64_t)((fr + cached_bytes()) / 4 / bm_bytes)));
+            HIPCHK(d_bm.alloc((size_t)nb * 2 * nt));
+        }
+        hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(VL_THREADS), lds, s, cols, rows, tw, th,
                            g->pm->d_node_cell.p, g->pm->d_cell_node.p, g->pm->d_node_flags.p, g->node_run_start.p,
-                           g->node_nruns.p, g->pool.p, nsz.p, sb, se, gates_only, d_out.p, ctx->stats.p);
+                           g->node_nruns.p, g->pool.p, nsz.p, sb, se, gates_only, d_out.p, ctx->stats.p, d_bm.p);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ctx->ev1, s));
@@ -2089,6 +2276,60 @@ int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {
 // discovered through run membership (Bin::extractUnseen, ngraph.cpp:308-326: set semantics, the
 // extent short-cut only skips already-covered suffixes); contextfilled odd cells get their level but
 // are not expanded.  Runs on the tile-resolved BFS in seed mode (one workgroup).
+// Visual step depth for grids above 1024^2 or asymmetric graphs: the level-synchronous top-down
+// search of kernels/vstep.hip over the whole GPU.
+static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vector<int32_t>& seeds, int tw, int th,
+                                    float* out) {
+    PointMapHost& h = *g->pm->host;
+    const int rows = h.rows();
+    const int64_t C = h.cells(), N = g->nnodes, nt = (int64_t)tw * th;
+    hipStream_t s = ctx->stream;
+    DevBuf<unsigned long long> vis, cnt;
+    DevBuf<int32_t> level, fr[2];
+    HIPCHK(vis.alloc(nt));
+    HIPCHK(cnt.alloc(1));
+    HIPCHK(level.alloc(C));
+    HIPCHK(fr[0].alloc(std::max<int64_t>(N, 1)));
+    HIPCHK(fr[1].alloc(std::max<int64_t>(N, 1)));
+    std::vector<unsigned long long> v0((size_t)nt, 0ull);
+    std::vector<int32_t> lv((size_t)C, -1);
+    for (int32_t k : seeds) {
+        const int c = g->pm->node_cell[k], x = c / rows, y = c % rows;
+        v0[(size_t)(y >> 3) * tw + (x >> 3)] |= 1ull << ((y & 7) * 8 + (x & 7));
+        lv[c] = 0;
+    }
+    HIPCHK(hipMemcpyAsync(vis.p, v0.data(), nt * 8, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(level.p, lv.data(), C * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(fr[0].p, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, s));
+    HIPCHK(hipEventRecord(ctx->ev0, s));
+    int64_t nf = (int64_t)seeds.size();
+    int cur = 0, L = 0;
+    while (nf > 0) {
+        HIPCHK(hipMemsetAsync(cnt.p, 0, 8, s));
+        const int64_t blocks = std::min<int64_t>((nf + 3) / 4, (int64_t)ctx->num_cu * 16);
+        hipLaunchKernelGGL(vsd_level_kernel, dim3((unsigned)blocks), dim3(VSD_THREADS), 0, s, rows, tw,
+                           (const int32_t*)fr[cur].p, nf, g->node_run_start.p, g->node_nruns.p, g->pool.p,
+                           g->pm->d_cell_node.p, g->pm->d_node_flags.p, L + 1, vis.p, level.p, fr[cur ^ 1].p, cnt.p);
+        HIPCHK(hipGetLastError());
+        unsigned long long n_next = 0;
+        HIPCHK(copy_sync(s, &n_next, cnt.p, 8, hipMemcpyDeviceToHost));
+        cur ^= 1;
+        nf = (int64_t)n_next;
+        L++;
+    }
+    HIPCHK(hipEventRecord(ctx->ev1, s));
+    HIPCHK(copy_sync(s, lv.data(), level.p, C * 4, hipMemcpyDeviceToHost));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    ctx->last_vga_s = ms * 1e-3;
+    for (int64_t k = 0; k < N; k++) {
+        const int v = lv[g->pm->node_cell[k]];
+        out[k] = v >= 0 ? (float)v : -1.0f;
+    }
+    VLOG("visual step depth: top-down, %d levels, %.3f s\n", L, ms * 1e-3);
+    return DMX_OK;
+}
+
 int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
@@ -2118,13 +2359,17 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
         }
     }
     if (seeds.empty()) return fail(DMX_ERR_STATE, "no filled cell selected");
-    int rc = prepare_uf(g);
-    if (rc) return rc;
-    rc = prepare_symmetry(g);
-    if (rc) return rc;
     const int tw = (cols + 7) / 8, th = (rows + 7) / 8, nt = tw * th;
-    if (g->symmetric != 1 || nt > 16 * 1024)
-        return fail(DMX_ERR_UNSUPPORTED, "visual step depth needs the tile-resolved BFS (grid <= 1024^2, symmetric graph)");
+    bool tile = nt <= 16 * 1024 && !getenv("DMX_VSD_TOPDOWN");
+    int rc = DMX_OK;
+    if (tile) {
+        rc = prepare_uf(g);
+        if (rc) return rc;
+        rc = prepare_symmetry(g);
+        if (rc) return rc;
+        tile = g->symmetric == 1;
+    }
+    if (!tile) return visual_stepdepth_topdown(ctx, g, seeds, tw, th, out);
     DevBuf<int32_t> d_seeds, d_level;
     HIPCHK(d_seeds.alloc(seeds.size()));
     HIPCHK(d_level.alloc((size_t)nt * 64));

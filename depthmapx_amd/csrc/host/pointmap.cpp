@@ -154,7 +154,7 @@ int PointMapHost::expand(int x1, int y1, int x2, int y2, std::vector<int32_t>& n
     return 8;
 }
 
-int PointMapHost::fill(double px, double py) {
+int PointMapHost::fill_seed(double px, double py, int* psx, int* psy) const {
     // fillGraph: graph.getRegion().contains(point) -- strict (p2dpoly.h:338-340)
     if (!(px > parent_.blx && px < parent_.trx && py > parent_.bly && py < parent_.tr_y)) return 1;
     // PointMap::pixelate(p, false) (pointdata.cpp:283-305) into PixelRef(short, short)
@@ -167,6 +167,27 @@ int PointMapHost::fill(double px, double py) {
         for (int32_t k = seg_off_[c]; k < seg_off_[c + 1]; k++)
             if (segs_cross_strict(seg_at(k), ls, 0.0)) return 2;
     }
+    *psx = sx;
+    *psy = sy;
+    return 0;
+}
+
+void PointMapHost::adopt_blocked(std::vector<int32_t>&& seg_off, std::vector<double>&& segs) {
+    seg_off_ = std::move(seg_off);
+    segs_ = std::move(segs);
+    blocked_ = true;
+}
+
+void PointMapHost::adopt_state(std::vector<int32_t>&& state) {
+    state_ = std::move(state);
+    filled_ = 0;
+    for (int32_t s : state_) filled_ += (s & CELL_FILLED) ? 1 : 0;
+}
+
+int PointMapHost::fill(double px, double py) {
+    int sx = 0, sy = 0;
+    const int r = fill_seed(px, py, &sx, &sy);
+    if (r) return r;
     block_lines();
     int64_t c0 = index(sx, sy);
     state_[c0] = CELL_FILLED | (state_[c0] & CELL_BLOCKED);

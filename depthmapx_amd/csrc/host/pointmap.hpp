@@ -39,6 +39,14 @@ class PointMapHost {
     // Returns 0 = filled, 1 = point outside region, 2 = makePoints refused (off-grid, already
     // filled, or seed hidden from its cell centre).
     int fill(double x, double y);
+    // fill's checks on the seed alone (region, pixelate, already filled, seed hidden from its cell
+    // centre once lines are blocked): 0 = a fill may start at cell (*sx, *sy), else fill's code.
+    int fill_seed(double x, double y, int* sx, int* sy) const;
+    // Results of a fill computed elsewhere (the GPU path): lines blocked into these per-cell pieces,
+    // and/or the cell states after the fill.
+    void adopt_blocked(std::vector<int32_t>&& seg_off, std::vector<double>&& segs);
+    void adopt_state(std::vector<int32_t>&& state);
+    const std::vector<double>& drawing() const { return draw_; }
     // A map restored from a .graph PointMap chunk: grid geometry and cell states as stored
     // (PointMap::read, pointdata.cpp:1073-1156).  No occluder pieces: such a map can run VGA and
     // step depth on its graph but not makeGraph.

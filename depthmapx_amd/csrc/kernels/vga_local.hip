@@ -6,7 +6,8 @@
 //   total    = |union of cells(n)|
 // and the three columns cluster/(k(k-1)), control, k/total with k = |V(s)| (-1 for k <= 1).
 //
-// One workgroup per source.  V(s) and the union live in LDS as 8x8-cell tile bitmaps (the layout of
+// One workgroup per source.  V(s) and the union live in LDS (above ~780^2 cells: in a per-workgroup
+// slice of HBM) as 8x8-cell tile bitmaps (the layout of
 // vga_tile.hip), so a neighbour's run costs one LDS word per tile it crosses: AND + popcount for the
 // intersection, a test-then-OR for the union.  The control sum is a sequential float chain in x-major
 // cell order (the reference sorts the neighbourhood): wave 0 walks the columns 64 cells at a time and
@@ -63,17 +64,21 @@ __global__ void node_size_kernel(int64_t n, const int64_t* node_run_start, const
     if (lane == 0) node_size[k] = acc;
 }
 
+// GBM = false: both bitmaps in LDS (grids up to ~780^2 cells); true: a per-workgroup slice of HBM
+// scratch (2*tw*th words at gbm + blockIdx.x * 2*nt), L2-resident, for larger grids.
+template <bool GBM>
 __global__ void __launch_bounds__(VL_THREADS) vga_local_kernel(int cols, int rows, int tw, int th,
                                                                const int32_t* node_cell, const int32_t* cell_node,
                                                                const uint8_t* node_flags, const int64_t* node_run_start,
                                                                const int32_t* node_nruns, const Run* pool,
                                                                const int32_t* node_size, int64_t sb, int64_t se,
                                                                int gates_only, float* out,
-                                                               unsigned long long* stats) {
+                                                               unsigned long long* stats, unsigned long long* gbm) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long vl_lds[];
     const int nt = tw * th;
-    unsigned long long* S = vl_lds;        // V(s)
-    unsigned long long* U = vl_lds + nt;   // union of the neighbours' cells
+    unsigned long long* const bm = GBM ? gbm + (size_t)blockIdx.x * 2 * nt : vl_lds;
+    unsigned long long* S = bm;        // V(s)
+    unsigned long long* U = bm + nt;   // union of the neighbours' cells
     __shared__ long long red_cl[VL_THREADS / 64];
     __shared__ int red_k[VL_THREADS / 64], red_t[VL_THREADS / 64];
     __shared__ float s_control;
@@ -88,7 +93,7 @@ __global__ void __launch_bounds__(VL_THREADS) vga_local_kernel(int cols, int row
             if (threadIdx.x < 3) o[threadIdx.x] = -1.0f;   // skipped (count only)
             continue;
         }
-        for (int t = threadIdx.x; t < 2 * nt; t += VL_THREADS) vl_lds[t] = 0ull;
+        for (int t = threadIdx.x; t < 2 * nt; t += VL_THREADS) bm[t] = 0ull;
         __syncthreads();
         {
             const int64_t rs = node_run_start[src];

@@ -1,0 +1,52 @@
+// vstep.hip -- visual step depth over the whole GPU, for the maps the tile-resolved BFS does not take
+// (grids above 1024^2 cells, or graphs too asymmetric for its bottom-up levels).
+//
+// VGAVisualGlobalDepth::run (salalib/vgamodules/vgavisualglobaldepth.cpp:23-77) is a multi-source
+// BFS: the selected cells are level 0 and always expand; a cell popped at level L > 0 takes the
+// value L and expands unless it is context-filled at an odd PixelRef (:53); expanding walks the
+// node's runs (Node::extractUnseen) and queues every cell not yet seen.  Without merge links (they
+// are refused before this runs) the value of a filled cell is its BFS level, whatever the order
+// inside a level, so the search is level-synchronous and top-down:
+//   - one wave per frontier node, lanes over its runs;
+//   - a run is walked tile word by tile word (8x8-cell words, the layout of vga_tile.hip) against
+//     the visited bitmap: atomicOr claims the unseen cells of the word, each newly seen cell takes
+//     level L+1, and the expandable filled ones join the next frontier.
+// Cost: 8 B per run plus one bitmap word per 8 cells of run length, per expanded node.
+#pragma once
+
+namespace dmx {
+
+constexpr int VSD_THREADS = 256;
+
+__global__ void __launch_bounds__(VSD_THREADS) vsd_level_kernel(int rows, int tw, const int32_t* frontier, int64_t nf,
+                                                                const int64_t* node_run_start, const int32_t* node_nruns,
+                                                                const Run* pool, const int32_t* cell_node,
+                                                                const uint8_t* node_flags, int next_level,
+                                                                unsigned long long* vis, int32_t* level, int32_t* next,
+                                                                unsigned long long* next_n) {
+    const int lane = threadIdx.x & 63;
+    const int64_t waves = (int64_t)gridDim.x * (VSD_THREADS / 64);
+    for (int64_t f = (int64_t)blockIdx.x * (VSD_THREADS / 64) + (threadIdx.x >> 6); f < nf; f += waves) {
+        const int32_t node = frontier[f];
+        const int64_t rs = node_run_start[node];
+        const int nr = node_nruns[node];
+        for (int r = lane; r < nr; r += 64)
+            run_tile_words(tw, pool[rs + r], [&](int w, unsigned long long m) {
+                if ((vis[w] & m) == m) return;   // all seen (a stale read only costs the atomic below)
+                unsigned long long fresh = m & ~atomicOr(&vis[w], m);
+                while (fresh) {
+                    const int b = __builtin_ctzll(fresh);
+                    fresh &= fresh - 1;
+                    const int x = (w % tw) * 8 + (b & 7), y = (w / tw) * 8 + (b >> 3);
+                    const int64_t c = (int64_t)x * rows + y;
+                    level[c] = next_level;
+                    const int32_t nn = cell_node[c];
+                    // PixelRef::iseven: both coordinates even
+                    if (nn >= 0 && (!(node_flags[nn] & 1) || ((x % 2) == 0 && (y % 2) == 0)))
+                        next[atomicAdd(next_n, 1ull)] = nn;
+                }
+            });
+    }
+}
+
+} // namespace dmx

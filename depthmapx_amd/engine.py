@@ -65,6 +65,12 @@ class Context:
         """Cancel the running (or next) makeGraph / VGA-global / step-depth call (any thread)."""
         N.check(N.lib().dmx_ctx_cancel(self.h))
 
+    def last_fill(self):
+        """(blockLines s, flood fill s, levels) of the last GPU fill."""
+        b, f, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        N.check(N.lib().dmx_ctx_last_fill(self.h, ctypes.byref(b), ctypes.byref(f), ctypes.byref(n)))
+        return b.value, f.value, n.value
+
     def last_timing(self):
         mk, vg = ctypes.c_double(), ctypes.c_double()
         N.check(N.lib().dmx_ctx_last_timing(self.h, ctypes.byref(mk), ctypes.byref(vg)))
@@ -135,11 +141,15 @@ class PointMap:
     def rows(self):
         return self.info()["rows"]
 
-    def make_points(self, x, y):
+    def make_points(self, x, y, ctx=None):
         """runmethods fillGraph + PointMap::makePoints; raises DmxError(DMX_ERR_OUTSIDE) like the CLI's
-        'Point outside of target region'; returns False where makePoints returns false."""
+        'Point outside of target region'; returns False where makePoints returns false.  With a
+        Context the rasterisation and the flood fill run on its GPU (dmx_pointmap_fill_device)."""
         made = ctypes.c_int()
-        N.check(N.lib().dmx_pointmap_fill(self.h, float(x), float(y), ctypes.byref(made)))
+        if ctx is None:
+            N.check(N.lib().dmx_pointmap_fill(self.h, float(x), float(y), ctypes.byref(made)))
+        else:
+            N.check(N.lib().dmx_pointmap_fill_device(ctx.h, self.h, float(x), float(y), ctypes.byref(made)))
         return bool(made.value)
 
     def state(self):

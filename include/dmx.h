@@ -99,6 +99,14 @@ int dmx_pointmap_free(dmx_pointmap* pm);
  * salalib/pointdata.cpp:402-481).  DMX_ERR_OUTSIDE if the point is outside the region;
  * *made = 0 where makePoints returns false. */
 int dmx_pointmap_fill(dmx_pointmap* pm, double x, double y, int* made);
+/* The same fill computed on the context's GPU (kernels/fill.hip): PointMap::blockLines
+ * (pointdata.cpp:296-357, spacepix.cpp:144-214, p2dpoly.cpp:626-667) on the first fill, then the
+ * makePoints/expand flood fill (pointdata.cpp:402-514) in the reference's exact expand order, so
+ * the FILLED and order-dependent EDGE bits equal the host fill's.  Same return codes and *made. */
+int dmx_pointmap_fill_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y, int* made);
+/* Seconds of the last dmx_pointmap_fill_device: blockLines (0 when lines were already blocked),
+ * flood fill, and the number of fill levels. */
+int dmx_ctx_last_fill(dmx_ctx* ctx, double* block_s, double* fill_s, int64_t* levels);
 /* Restore the FILLED / EDGE / CONTEXTFILLED cell states of a map saved earlier (e.g. the state
  * array of a PointMap chunk of the same grid), as PointMap::read does before makeGraph. */
 int dmx_pointmap_set_state(dmx_pointmap* pm, const int32_t* state);
@@ -177,7 +185,8 @@ int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
  * (salalib/mgraph.cpp:349-353, vgamodules/vgavisuallocal.cpp:23-117) for source nodes
  * [src_begin, src_end) (src_end < 0: all).  out: host [N][3] in node order, rows outside the range
  * untouched: Visual Clustering Coefficient, Visual Control, Visual Controllability (-1 for skipped
- * sources and neighbourhoods of <= 1 cell).  DMX_ERR_UNSUPPORTED for grids above ~780^2 cells. */
+ * sources and neighbourhoods of <= 1 cell).  The two tile bitmaps per source live in LDS up to ~780^2
+ * cells and in per-workgroup HBM slices above that (no grid-size limit). */
 int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t src_begin, int64_t src_end, float* out);
 /* Multi-GPU share of the VGA preparation (no reference counterpart: the reference prepares nothing;
  * this splits our own O(runs) pre-passes).  Every rank holds the whole graph; the per-node scatters
@@ -212,7 +221,8 @@ int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
  * -> VGAVisualGlobalDepth::run (depthmapXcli/runmethods.cpp:767-769, salalib/mgraph.cpp:312-314,
  * vgamodules/vgavisualglobaldepth.cpp:23-77).  sel_cells as for dmx_metric_stepdepth.  out: host
  * [N] "Visual Step Depth" in node order (unreached cells -1).  DMX_ERR_STATE if no filled cell is
- * selected; DMX_ERR_UNSUPPORTED for grids above 1024^2 or graphs too asymmetric for the tile BFS. */
+ * selected.  Grids up to 1024^2 with a symmetric graph take the tile-resolved BFS; others the
+ * level-synchronous top-down search (kernels/vstep.hip). */
 int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out);
 /* Kernel time of the last step-depth call, expanders popped, cells relaxed. */
 int dmx_ctx_last_stepdepth(dmx_ctx* ctx, double* seconds, int64_t* expanders_popped, int64_t* cells_relaxed);

@@ -1,0 +1,135 @@
+"""GPU VISPREP preparation: occluder rasterisation and the flood fill on the
+GPU (dmx_pointmap_fill_device, kernels/fill.hip) against the reference.
+
+  * PointMap::blockLines / PixelBase::pixelateLineTouching / Line::crop (salalib/pointdata.cpp:296-357,
+    spacepix.cpp:144-214, genlib/p2dpoly.cpp:626-667): the per-cell cropped pieces, bit-exact;
+  * PointMap::makePoints / expand (pointdata.cpp:402-514): the cell states, including the EDGE bit
+    that depends on the reference's expand order, bit-exact.
+
+The reference fixtures (tests/golden/*.npz: `state`, `celllines_n`, `celllines`, written by the
+reference built from source) pin the small cases; at the benchmark sizes the GPU fill is compared
+with the host model, itself pinned to those fixtures (test_host_model.py) and to the oracle at size
+(test_gpu_scale.py).  The .graph VISPREP regression cases run through dmxcli with DMX_FILL=device.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import depthmapx_amd as dmx
+from golden_io import GOLDEN, case_input_lines, load_case, read_csv_lines
+
+pytestmark = pytest.mark.gpu
+
+FILLED, BLOCKED, EDGE = 2, 4, 32
+
+
+def _both(region, lines, spacing, fills, ctx):
+    a = dmx.PointMap(region, lines, spacing)
+    b = dmx.PointMap(region, lines, spacing)
+    made = []
+    for f in fills:
+        ma = a.make_points(*f)
+        mb = b.make_points(*f, ctx=ctx)
+        assert ma == mb, f
+        made.append(ma)
+    return a, b, made
+
+
+def _assert_same(a, b):
+    np.testing.assert_array_equal(b.state(), a.state())
+    ca, pa = a.cell_lines()
+    cb, pb = b.cell_lines()
+    np.testing.assert_array_equal(cb, ca)
+    np.testing.assert_array_equal(pb.view(np.uint64), pa.view(np.uint64))
+    assert a.info()["filled"] == b.info()["filled"]
+
+
+@pytest.mark.parametrize("name", ["kat", "syn16", "syn32", "gallery", "syn64", "barnsbury", "syn256mk"])
+def test_gpu_fill_matches_reference(ctx, name):
+    meta, A = load_case(name)
+    pm = dmx.PointMap(meta["region"], case_input_lines(meta), meta["spacing"])
+    for f in meta["fills"]:
+        assert pm.make_points(*f, ctx=ctx)
+    counts, pieces = pm.cell_lines()
+    np.testing.assert_array_equal(counts, A["celllines_n"])
+    np.testing.assert_array_equal(pieces, A["celllines"])
+    np.testing.assert_array_equal(pm.state(), A["state"])
+    assert pm.info()["filled"] == meta["nodes"]
+
+
+@pytest.mark.parametrize("cfg", ["syn1000", "syn2000_5000"])
+def test_gpu_fill_at_benchmark_size(ctx, cfg):
+    """configs[2] (1001^2, 50 occluders) and configs[4] (2000^2, 5000 occluders): GPU == host."""
+    W = 1000.0 if cfg == "syn1000" else 1999.0
+    lines = read_csv_lines(os.path.join(GOLDEN, "inputs", cfg + ".csv"))
+    a, b, made = _both([0.0, 0.0, W, W], lines, 1.0, [(0.5, 0.5)], ctx)
+    assert made == [True]
+    _assert_same(a, b)
+    st = b.state()
+    assert (st & EDGE).any() and (st & BLOCKED).any()
+    blk, fl, levels = ctx.last_fill()
+    assert levels > 100 and blk > 0 and fl > 0
+
+
+def test_gpu_fill_order_dependent_edges(ctx):
+    """Many short occluders crossing cell steps at odd angles: the EDGE bit depends on which
+    neighbour the reference's expand order fills first.  Seeded, several fills (rooms), GPU == host."""
+    rng = np.random.default_rng(11)
+    W = 96.0
+    n = 400
+    c = rng.uniform(2, W - 2, size=(n, 2))
+    ang = rng.uniform(0, np.pi, size=n)
+    ln = rng.uniform(0.6, 4.0, size=n)
+    d = np.stack([np.cos(ang), np.sin(ang)], 1) * (ln / 2)[:, None]
+    segs = np.concatenate([c - d, c + d], 1)
+    walls = np.array([[0, 0, W, 0], [W, 0, W, W], [W, W, 0, W], [0, W, 0, 0],
+                      [W / 2, 0, W / 2, W * 0.45], [W / 2, W * 0.55, W / 2, W]], dtype=np.float64)
+    lines = np.concatenate([walls, segs]).astype(np.float64)
+    fills = [(1.5, 1.5), (W - 1.5, W - 1.5), (1.5, 1.5), (W / 4 + 0.3, W * 0.8 + 0.2)]
+    for spacing in (1.0, 0.7):
+        a, b, made = _both([0.0, 0.0, W, W], lines, spacing, fills, ctx)
+        assert made[2] is False                       # already filled: makePoints false
+        _assert_same(a, b)
+        st = a.state()
+        assert ((st & EDGE) != 0).sum() > 100
+
+
+def test_gpu_fill_errors_like_the_host(ctx):
+    meta, _ = load_case("syn16")
+    pm = dmx.PointMap(meta["region"], case_input_lines(meta), meta["spacing"])
+    with pytest.raises(dmx.DmxError) as e:                 # runmethods.cpp:271-275
+        pm.make_points(-5.0, 3.0, ctx=ctx)
+    assert e.value.status == -6
+    assert pm.make_points(0.5, 0.5, ctx=ctx)
+    assert not pm.make_points(0.5, 0.5, ctx=ctx)
+    # a device-filled map makes the same graph as the fixture's
+    meta, A = load_case("syn32")
+    pm = dmx.PointMap(meta["region"], case_input_lines(meta), meta["spacing"])
+    for f in meta["fills"]:
+        assert pm.make_points(*f, ctx=ctx)
+    g = pm.make_graph(ctx)
+    got = g.copy()
+    np.testing.assert_array_equal(got["bins"], A["bins"])
+    np.testing.assert_array_equal(got["attrs"].view(np.uint32), A["attrs"].view(np.uint32))
+    g.close()
+
+
+def _fill_cases():
+    import json
+    gf = os.path.join(GOLDEN, "graphfiles")
+    cases = json.load(open(os.path.join(gf, "cases.json")))
+    return [n for n, m in cases.items() if not m.get("refused") and ("-pp" in m["args"] or "-pf" in m["args"])]
+
+
+@pytest.mark.parametrize("name", _fill_cases())
+def test_graph_visprep_device_fill_matches_reference(tmp_path, monkeypatch, name):
+    """The .graph regression cases that fill a grid, with the fill on the GPU (dmxcli DMX_FILL=device):
+    the same outputs as the reference's (byte-identical where the host run is)."""
+    import test_graphfile as tg
+    monkeypatch.setenv("DMX_FILL", "device")
+    how = tg._check_case(tmp_path, name)
+    assert how in ("identical", "within tolerance")
+    if not tg.CASES[name]["columns"]:
+        assert how == "identical"
