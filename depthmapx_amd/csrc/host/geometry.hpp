@@ -117,6 +117,11 @@ DMX_HD bool clip_seg(Seg& l, const Rect& c) {
     return true;
 }
 
+// int(floor(v)) as the reference's x86-64 build evaluates it (cvttsd2si): NaN and out-of-range values
+// give INT_MIN.  pixelateLineTouching meets NaN on zero-length lines (0/0 gradient); C++ leaves the
+// conversion undefined and the GPU's own conversion gives 0, so both paths spell it out.
+DMX_HD int cvt_i32_x86(double v) { return (v >= -2147483648.0 && v < 2147483648.0) ? (int)v : (int)(-2147483647 - 1); }
+
 // Point::m_state bits (salalib/point.h:32-38).
 enum CellState : int32_t {
     CELL_EMPTY = 0x0001, CELL_FILLED = 0x0002, CELL_BLOCKED = 0x0004, CELL_CONTEXTFILLED = 0x0008,

@@ -86,7 +86,8 @@ bool read_layer(Rd& r, GfLayer& L) {
     L.obj_ref = r.get<int32_t>();
     r.get<int32_t>();   // largest shape ref (recomputed on write)
     const int32_t ns = r.get<int32_t>();
-    if (!r.ok || ns < 0) return false;
+    // a stored shape takes >= 81 bytes: counts beyond what is left are damage, not an allocation
+    if (!r.ok || ns < 0 || (size_t)ns * 81 > r.n - r.o) return false;
     L.shapes.resize((size_t)ns);
     for (auto& s : L.shapes) {
         s.key = r.get<int32_t>();
@@ -271,13 +272,13 @@ int read_graphfile(const uint8_t* buf, size_t size, GraphFile& gf, std::string& 
         gf.name = r.str();
         for (int i = 0; i < 4; i++) gf.region[i] = r.get<double>();
         const int32_t nf = r.get<int32_t>();
-        if (!r.ok || nf < 0) { err = "damaged drawing section"; return -1; }
+        if (!r.ok || nf < 0 || (size_t)nf * 40 > r.n - r.o) { err = "damaged drawing section"; return -1; }
         gf.drawing.resize((size_t)nf);
         for (auto& f : gf.drawing) {
             f.name = r.str();
             for (int i = 0; i < 4; i++) f.region[i] = r.get<double>();
             const int32_t nl = r.get<int32_t>();
-            if (!r.ok || nl < 0) { err = "damaged drawing file"; return -1; }
+            if (!r.ok || nl < 0 || (size_t)nl * 8 > r.n - r.o) { err = "damaged drawing file"; return -1; }
             f.layers.resize((size_t)nl);
             for (auto& L : f.layers)
                 if (!read_layer(r, L)) { err = "damaged drawing layer"; return -1; }

@@ -392,7 +392,8 @@ int read_pointmap_chunk(const uint8_t* buf, size_t size, ParsedChunk& pc, std::s
         pc.columns[phys[i]] = sorted[i];
     }
     const int32_t nrows = r.get<int32_t>();
-    if (!r.ok || nrows < 0) { err = "truncated attribute table"; return -1; }
+    // a row takes >= 16 bytes: a count beyond what is left is damage, not an allocation
+    if (!r.ok || nrows < 0 || (size_t)nrows * 16 > size - r.o) { err = "truncated attribute table"; return -1; }
     for (auto& c : pc.columns) c.values.assign(nrows, -1.0f);
     pc.row_keys.resize(nrows);
     pc.row_layers.resize(nrows);
@@ -408,6 +409,8 @@ int read_pointmap_chunk(const uint8_t* buf, size_t size, ParsedChunk& pc, std::s
     if (r.o + 12 <= size) std::memcpy(pc.table_display, buf + r.o, 12);
     r.o += 12;
     const int64_t C = (int64_t)pc.cols * pc.rows;
+    // Point::write takes >= 30 bytes per cell
+    if (r.o > size || (uint64_t)C * 30 > (uint64_t)(size - r.o)) { err = "truncated point records"; return -1; }
     pc.state.resize(C);
     pc.gridconn.clear();
     pc.bins.clear();

@@ -80,11 +80,11 @@ void PointMapHost::rasterise(const Seg& in, std::vector<int32_t>& out) const {
     const double grad = along_x ? l.sign() * l.r.height() / l.r.width() : l.sign() * l.r.width() / l.r.height();
     const double constant = along_x ? l.ay() - grad * l.ax() : l.ax() - grad * l.ay();
     const double lo = along_x ? l.ax() : l.r.bly, hi = along_x ? l.bx() : l.r.tr_y;
-    int first = (int)floor(lo - tol), last = (int)floor(hi + tol);
+    int first = cvt_i32_x86(floor(lo - tol)), last = cvt_i32_x86(floor(hi + tol));
     for (int i = first; i <= last; i++) {
-        int j1 = (int)floor((first == i ? lo : double(i)) * grad + constant - l.sign() * tol);
-        int j2 = (int)floor((last == i ? hi : double(i + 1)) * grad + constant + l.sign() * tol);
-        int js[3] = {j1, j2, (j1 + j2) / 2};
+        int j1 = cvt_i32_x86(floor((first == i ? lo : double(i)) * grad + constant - l.sign() * tol));
+        int j2 = cvt_i32_x86(floor((last == i ? hi : double(i + 1)) * grad + constant + l.sign() * tol));
+        int js[3] = {j1, j2, (int)(((long long)j1 + j2) / 2)};
         int nj = (j1 != j2) ? (std::abs(j2 - j1) == 2 ? 3 : 2) : 1;
         for (int k = 0; k < nj; k++) {
             if (along_x) emit(i, js[k]);

@@ -64,13 +64,13 @@ __device__ void rasterise_line(const FillGrid& G, Seg l, Emit&& emit) {
     const double grad = along_x ? l.sign() * l.r.height() / l.r.width() : l.sign() * l.r.width() / l.r.height();
     const double constant = along_x ? l.ay() - grad * l.ax() : l.ax() - grad * l.ay();
     const double lo = along_x ? l.ax() : l.r.bly, hi = along_x ? l.bx() : l.r.tr_y;
-    const int first = (int)floor(lo - tol), last = (int)floor(hi + tol);
+    const int first = cvt_i32_x86(floor(lo - tol)), last = cvt_i32_x86(floor(hi + tol));
     const int lim = along_x ? G.cols : G.rows, olim = along_x ? G.rows : G.cols;
     const int ib = max(first, 0), ie = min(last, lim - 1);
     for (int i = ib; i <= ie; i++) {
-        const int j1 = (int)floor((first == i ? lo : double(i)) * grad + constant - l.sign() * tol);
-        const int j2 = (int)floor((last == i ? hi : double(i + 1)) * grad + constant + l.sign() * tol);
-        const int js[3] = {j1, j2, (j1 + j2) / 2};
+        const int j1 = cvt_i32_x86(floor((first == i ? lo : double(i)) * grad + constant - l.sign() * tol));
+        const int j2 = cvt_i32_x86(floor((last == i ? hi : double(i + 1)) * grad + constant + l.sign() * tol));
+        const int js[3] = {j1, j2, (int)(((long long)j1 + j2) / 2)};
         const int nj = (j1 != j2) ? (abs(j2 - j1) == 2 ? 3 : 2) : 1;
         for (int k = 0; k < nj; k++) {
             const int j = (short)js[k];
