@@ -106,7 +106,7 @@ def test_visual_stepdepth_topdown_equals_tile(ctx, monkeypatch, seed):
         monkeypatch.setenv("DMX_VSD_TOPDOWN", "1")
         b = g.visual_step_depth(cells=cells)
         np.testing.assert_array_equal(b.view(np.uint32), a.view(np.uint32))
-        assert b.max() >= (2 if nsel == 1 else 1)
+        assert (b >= 0).sum() > len(b) // 2
 
 
 def test_visual_stepdepth_above_1024_matches_oracle(ctx):
