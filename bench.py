@@ -396,15 +396,20 @@ def main():
         achieved = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
         pmc = load_pmc(workload) if world == 1 else {}
         dpm = pmc.get(dominant, {})
+        dps = dpm.get("per_step", {})
         roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 # HBM bytes per launch from the PMC passes of this workload and build: FETCH_SIZE + WRITE_SIZE as
                 # read (neither kernel streams 16 B/lane, where the guide's 2x FETCH correction applies); the
                 # corrected figure is an upper bound
-                "traffic": dpm.get("hbm_bytes_raw"), "traffic_corrected_2x_fetch": dpm.get("hbm_bytes_corrected"),
+                # per step: a kernel launched more than once per step (makeGraph: the sample pass, the main
+                # launch and the capacity retry) is counted over all its launches, like the live time
+                "traffic": dps.get("hbm_bytes_raw", dpm.get("hbm_bytes_raw")),
+                "traffic_corrected_2x_fetch": dps.get("hbm_bytes_corrected", dpm.get("hbm_bytes_corrected")),
                 "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if dpm else None,
-                "algorithmic_bytes": dom_bytes,
-                "kernel_s_live": dom_s, "kernel_s_rocprof": dpm.get("duration_ns", 0) * 1e-9 if dpm else None}
+                "algorithmic_bytes": dom_bytes, "launches_per_step": dpm.get("calls"),
+                "kernel_s_live": dom_s,
+                "kernel_s_rocprof": dps.get("duration_ns", dpm.get("duration_ns", 0)) * 1e-9 if dpm else None}
         if not stepdepth:
             # SURVEY.md section 8(d) B_vga at batch size 1 = the reference's BFS work (every source reads every
             # reached node's run records and touches N cells): the bytes a run-by-run BFS would move

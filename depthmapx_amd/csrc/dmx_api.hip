@@ -1482,6 +1482,16 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     // chunks of consecutive sources per workgroup, small enough to balance the tail
     P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
     if (const char* c = getenv("DMX_VGA_CHUNK")) P.chunk = std::max(1, atoi(c));
+    P.nwork = (int)((P.src_end - P.src_begin + P.chunk - 1) / P.chunk);
+    P.xcd_ctr = nullptr;
+    DevBuf<int> xcd;
+    if (const char* xe = getenv("DMX_VGA_XCD")) {
+        if (atoi(xe) > 0) {
+            HIPCHK(xcd.alloc(8));
+            HIPCHK(hipMemsetAsync(xcd.p, 0, 8 * sizeof(int), ctx->stream));
+            P.xcd_ctr = xcd.p;
+        }
+    }
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     P.ctl = ctx->d_ctl;
     ctx->h_ctl->progress = 0;

@@ -59,6 +59,8 @@ struct VgaTileParams {
     int64_t uf_count;
     int alpha;
     int* work_counter;
+    int* xcd_ctr;             // optional: 8 group counters (grab_work); nwork = work items (chunks)
+    int nwork;
     DmxCtl* ctl;              // host-mapped progress / cancel block (nullptr: none)
     int chunk;                // consecutive sources per work grab (neighbouring sources share hints)
     uint16_t* hint;           // [nt*64] scan position of the run that last hit for a recent source (0xFFFF:
@@ -269,8 +271,28 @@ __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
 
 struct TileShared {
     int src, qn, hn, item, bn;
+    int grp, grp_tries;   // XCD-grouped work: the group being drained, groups found empty
     unsigned long long cnt, mass;
 };
+
+// Next work item.  xcd_ctr == nullptr: one counter for the whole grid.  Otherwise the items are split
+// into 8 contiguous ranges, one per group of blocks sharing an XCD (blockIdx % 8: a label, not an XCD
+// id; placement only changes speed), so the ~32 workgroups of an XCD work on neighbouring sources and
+// share its L2; a group whose range is drained moves on to the next group's range.  The grid counter
+// still counts grabs, for progress.
+__device__ __forceinline__ int grab_work(DmxCtl* ctl, int* work_counter, int* xcd_ctr, int nwork, TileShared& S) {
+    const int w = ctl_poll(ctl, atomicAdd(work_counter, 1));   // progress and cancel on the grab count
+    if (!xcd_ctr || w == CTL_STOP) return w;
+    while (S.grp_tries < 8) {
+        const int g = S.grp;
+        const int b = (int)((long long)nwork * g / 8), e = (int)((long long)nwork * (g + 1) / 8);
+        const int i = atomicAdd(&xcd_ctr[g], 1);
+        if (b + i < e) return b + i;
+        S.grp = (g + 1) & 7;
+        S.grp_tries++;
+    }
+    return nwork;   // past the end: the workgroup leaves
+}
 
 // Frontier cells on run `ru` (rare path: exact count for the asymmetric nodes).
 __device__ __forceinline__ int run_count_f(const unsigned long long* F, int tw, Run ru) {
@@ -391,7 +413,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
     for (int i = tid; i < 32; i += NT) SC[i] = 0ull;
 
     uint16_t* Hn = P.hint;
-    if (tid == 0) { S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.cnt = 0; S.mass = 0; S.src = -1; }
+    if (tid == 0) {
+        S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.cnt = 0; S.mass = 0; S.src = -1;
+        S.grp = blockIdx.x & 7; S.grp_tries = 0;
+    }
     int64_t chunk_end = 0;
     int64_t src = -1;
     for (;;) {
@@ -399,7 +424,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
         // through the same runs: the hint array carries that knowledge from one source to the next
         if (src + 1 >= chunk_end) {
             __syncthreads();
-            if (tid == 0) S.src = ctl_poll(P.ctl, atomicAdd(P.work_counter, 1));
+            if (tid == 0) S.src = grab_work(P.ctl, P.work_counter, P.xcd_ctr, P.nwork, S);
             __syncthreads();
             src = P.src_begin + (int64_t)S.src * P.chunk;
             chunk_end = min(src + (int64_t)P.chunk, P.src_end);
