@@ -629,7 +629,23 @@ int dmx_pointmap_fill_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y,
     HIPCHK(hipMemcpyAsync(layer[0].p, &seed_cell, sizeof(int32_t), hipMemcpyHostToDevice, st));
     int64_t n = 1, levels = 0;
     int cur = 0;
+    DevBuf<long long> io;
+    HIPCHK(io.alloc(3));
+    const bool wg_on = !getenv("DMX_FILL_GRID");   // test hook: every level grid-wide
     while (n > 0) {
+        if (wg_on && n <= FILL_WG_CAP) {
+            // small layers: one workgroup runs levels until the fill ends or a layer outgrows the cap
+            long long h_io[3] = {(long long)n, (long long)cur, 0};
+            HIPCHK(hipMemcpyAsync(io.p, h_io, sizeof(h_io), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(fill_levels_wg_kernel, dim3(1), dim3(FILL_WG_THREADS), 0, st, G, (const int32_t*)d_segoff.p,
+                               (const double*)d_segs.p, d_state.p, layer[0].p, layer[1].p, owner.p, io.p);
+            HIPCHK(hipGetLastError());
+            HIPCHK(copy_sync(st, h_io, io.p, sizeof(h_io), hipMemcpyDeviceToHost));
+            n = h_io[0];
+            cur = (int)h_io[1];
+            levels += h_io[2];
+            if (n == 0) break;
+        }
         hipLaunchKernelGGL(fill_claim_kernel, dim3(fill_blocks(n)), dim3(FILL_THREADS), 0, st, G, (const int32_t*)d_segoff.p,
                            (const double*)d_segs.p, (const int32_t*)d_state.p, (const int32_t*)layer[cur].p, n, owner.p, blocked.p);
         hipLaunchKernelGGL(fill_resolve_kernel, dim3(fill_blocks(n)), dim3(FILL_THREADS), 0, st, G, d_state.p,

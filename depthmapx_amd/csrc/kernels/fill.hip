@@ -190,11 +190,8 @@ __device__ bool fill_step_blocked(const FillGrid& G, const int32_t* seg_off, con
 
 // Claim: every unblocked expand of layer cell p onto a cell unfilled at the start of the layer bids
 // its call index p*8+k; blocked calls are remembered for the edge test.
-__global__ void fill_claim_kernel(FillGrid G, const int32_t* seg_off, const double* segs, const int32_t* state,
-                                  const int32_t* layer, int64_t n, uint32_t* owner, uint8_t* blocked) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const int32_t c = layer[p];
+__device__ __forceinline__ uint32_t fill_claim_one(const FillGrid& G, const int32_t* seg_off, const double* segs,
+                                                   const int32_t* state, int32_t c, int64_t p, uint32_t* owner) {
     const int x = c / G.rows, y = c % G.rows;
     uint32_t bm = 0;
     for (int k = 0; k < 8; k++) {
@@ -205,15 +202,13 @@ __global__ void fill_claim_kernel(FillGrid G, const int32_t* seg_off, const doub
         if (fill_step_blocked(G, seg_off, segs, x, y, x2, y2)) bm |= 1u << k;
         else atomicMin(&owner[c2], (uint32_t)(p * 8 + k));
     }
-    blocked[p] = (uint8_t)bm;
+    return bm;
 }
 
-// Resolve: the edge bit of layer cell p and the neighbours it fills.
-__global__ void fill_resolve_kernel(FillGrid G, int32_t* state, const int32_t* layer, int64_t n, const uint32_t* owner,
-                                    const uint8_t* blocked, uint8_t* children, int64_t* child_cnt) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const int32_t c = layer[p];
+// Resolve: the edge bit of layer cell p and the neighbours it fills (returned as a direction mask).
+// owner is read at agent scope: the bids are atomics, served by L2, never by a stale L1 line.
+__device__ __forceinline__ uint32_t fill_resolve_one(const FillGrid& G, int32_t* state, int32_t c, int64_t p,
+                                                     const uint32_t* owner, uint32_t blocked) {
     const int x = c / G.rows, y = c % G.rows;
     bool edge = (state[c] & CELL_BLOCKED) != 0;
     uint32_t ch = 0;
@@ -223,28 +218,22 @@ __global__ void fill_resolve_kernel(FillGrid G, int32_t* state, const int32_t* l
         const int64_t c2 = (int64_t)x2 * G.rows + y2;
         if (state[c2] & CELL_FILLED) continue;
         const uint32_t me = (uint32_t)(p * 8 + k);
-        if ((blocked[p] >> k) & 1) {
-            if (!(owner[c2] < me)) edge = true;   // expand returned 4
-        } else if (owner[c2] == me) {
-            ch |= 1u << k;                        // expand returned 8
+        const uint32_t ow = __hip_atomic_load(&owner[c2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((blocked >> k) & 1) {
+            if (!(ow < me)) edge = true;   // expand returned 4
+        } else if (ow == me) {
+            ch |= 1u << k;                 // expand returned 8
         }
     }
     if (edge) atomicOr(&state[c], (int32_t)CELL_EDGE);
-    children[p] = (uint8_t)ch;
-    child_cnt[p] = __popc(ch);
+    return ch;
 }
 
-// Push: the owned neighbours in direction order at consecutive push positions; the next layer is
-// processed from the back, so push position q lands at index n_next - 1 - q.
-__global__ void fill_push_kernel(const FillGrid G, int32_t* state, const int32_t* layer, int64_t n,
-                                 const uint8_t* children, const int64_t* child_off, int64_t n_next, int32_t* next) {
-    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= n) return;
-    const uint32_t ch = children[p];
-    if (!ch) return;
-    const int32_t c = layer[p];
+// Push: the owned neighbours in direction order at consecutive push positions from q; the next layer
+// is processed from the back, so push position q lands at index n_next - 1 - q.
+__device__ __forceinline__ void fill_push_one(const FillGrid& G, int32_t* state, int32_t c, uint32_t ch, int64_t q,
+                                              int64_t n_next, int32_t* next) {
     const int x = c / G.rows, y = c % G.rows;
-    int64_t q = child_off[p];
     for (int k = 0; k < 8; k++) {
         if (!((ch >> k) & 1)) continue;
         const int64_t c2 = (int64_t)(x + c_fill_dx[k]) * G.rows + (y + c_fill_dy[k]);
@@ -252,6 +241,85 @@ __global__ void fill_push_kernel(const FillGrid G, int32_t* state, const int32_t
         next[n_next - 1 - q] = (int32_t)c2;
         q++;
     }
+}
+
+__global__ void fill_claim_kernel(FillGrid G, const int32_t* seg_off, const double* segs, const int32_t* state,
+                                  const int32_t* layer, int64_t n, uint32_t* owner, uint8_t* blocked) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    blocked[p] = (uint8_t)fill_claim_one(G, seg_off, segs, state, layer[p], p, owner);
+}
+
+__global__ void fill_resolve_kernel(FillGrid G, int32_t* state, const int32_t* layer, int64_t n, const uint32_t* owner,
+                                    const uint8_t* blocked, uint8_t* children, int64_t* child_cnt) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t ch = fill_resolve_one(G, state, layer[p], p, owner, blocked[p]);
+    children[p] = (uint8_t)ch;
+    child_cnt[p] = __popc(ch);
+}
+
+__global__ void fill_push_kernel(const FillGrid G, int32_t* state, const int32_t* layer, int64_t n,
+                                 const uint8_t* children, const int64_t* child_off, int64_t n_next, int32_t* next) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t ch = children[p];
+    if (ch) fill_push_one(G, state, layer[p], ch, child_off[p], n_next, next);
+}
+
+// Small layers: one workgroup runs level after level with no host round trip (a launch and an 8-byte
+// readback per level cost ~47 us; a workgroup barrier a few hundred ns).  It stops when the fill is
+// done or a layer outgrows FILL_WG_CAP cells, leaving {n, cur} in io for the host, which continues with
+// the grid-wide kernels above.  Same claim / resolve / push bodies, separated by barriers; the per-cell
+// masks live in LDS, and each thread owns a contiguous slice of the layer so that its push positions
+// follow from one exclusive scan of the slice counts.
+constexpr int FILL_WG_THREADS = 1024, FILL_WG_CAP = 16384;
+__global__ void __launch_bounds__(FILL_WG_THREADS) fill_levels_wg_kernel(FillGrid G, const int32_t* seg_off,
+                                                                         const double* segs, int32_t* state,
+                                                                         int32_t* layer0, int32_t* layer1,
+                                                                         uint32_t* owner, long long* io) {
+    __shared__ uint8_t blk[FILL_WG_CAP], chm[FILL_WG_CAP];
+    __shared__ int part[FILL_WG_THREADS];
+    const int tid = threadIdx.x;
+    int64_t n = io[0];
+    int cur = (int)io[1];
+    long long levels = 0;
+    while (n > 0 && n <= FILL_WG_CAP) {
+        const int32_t* layer = cur ? layer1 : layer0;
+        int32_t* next = cur ? layer0 : layer1;
+        for (int p = tid; p < n; p += FILL_WG_THREADS) blk[p] = (uint8_t)fill_claim_one(G, seg_off, segs, state, layer[p], p, owner);
+        __builtin_amdgcn_s_waitcnt(0);   // the bids (atomics) have reached L2 before anyone resolves
+        __syncthreads();
+        const int per = (int)((n + FILL_WG_THREADS - 1) / FILL_WG_THREADS);
+        const int pb = min((int64_t)tid * per, n), pe = min((int64_t)(tid + 1) * per, n);
+        int cnt = 0;
+        for (int p = pb; p < pe; p++) {
+            const uint32_t ch = fill_resolve_one(G, state, layer[p], p, owner, blk[p]);
+            chm[p] = (uint8_t)ch;
+            cnt += __popc(ch);
+        }
+        part[tid] = cnt;
+        __syncthreads();
+        for (int d = 1; d < FILL_WG_THREADS; d <<= 1) {   // inclusive scan of the slice counts
+            const int v = tid >= d ? part[tid - d] : 0;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        const int64_t n_next = part[FILL_WG_THREADS - 1];
+        int64_t q = part[tid] - cnt;
+        for (int p = pb; p < pe; p++) {
+            const uint32_t ch = chm[p];
+            if (ch) fill_push_one(G, state, layer[p], ch, q, n_next, next);
+            q += __popc(ch);
+        }
+        __builtin_amdgcn_s_waitcnt(0);   // the pushed cells and states are stored before the next claim
+        __syncthreads();
+        n = n_next;
+        cur ^= 1;
+        levels++;
+    }
+    if (tid == 0) { io[0] = n; io[1] = cur; io[2] = levels; }
 }
 
 // ---- exclusive scan of int64 counts (out[0..n) = prefix, out[n] = total) ----

@@ -73,6 +73,25 @@ def test_gpu_fill_at_benchmark_size(ctx, cfg):
     assert levels > 100 and blk > 0 and fl > 0
 
 
+@pytest.mark.parametrize("grid_only", [False, True])
+def test_gpu_fill_layers_past_the_workgroup_cap(ctx, monkeypatch, grid_only):
+    """4201^2 cells seeded at the centre: the rings grow past FILL_WG_CAP (16384 cells), so the fill
+    moves from the one-workgroup kernel to the grid-wide levels and back as the rings hit the walls.
+    DMX_FILL_GRID=1 runs every level grid-wide.  Both equal the host fill."""
+    if grid_only:
+        monkeypatch.setenv("DMX_FILL_GRID", "1")
+    W = 4200.0
+    rng = np.random.default_rng(4)
+    c = rng.uniform(50, W - 50, size=(300, 2))
+    ang = rng.uniform(0, np.pi, size=300)
+    d = np.stack([np.cos(ang), np.sin(ang)], 1) * rng.uniform(2, 40, size=300)[:, None]
+    lines = np.concatenate([c - d, c + d], 1)
+    a, b, made = _both([0.0, 0.0, W, W], lines, 1.0, [(W / 2 + 0.3, W / 2 + 0.2)], ctx)
+    assert made == [True]
+    _assert_same(a, b)
+    assert ctx.last_fill()[2] > 2000
+
+
 def test_gpu_fill_order_dependent_edges(ctx):
     """Many short occluders crossing cell steps at odd angles: the EDGE bit depends on which
     neighbour the reference's expand order fills first.  Seeded, several fills (rooms), GPU == host."""
@@ -88,8 +107,13 @@ def test_gpu_fill_order_dependent_edges(ctx):
                       [W / 2, 0, W / 2, W * 0.45], [W / 2, W * 0.55, W / 2, W]], dtype=np.float64)
     lines = np.concatenate([walls, segs]).astype(np.float64)
     fills = [(1.5, 1.5), (W - 1.5, W - 1.5), (1.5, 1.5), (W / 4 + 0.3, W * 0.8 + 0.2)]
-    for spacing in (1.0, 0.7):
-        a, b, made = _both([0.0, 0.0, W, W], lines, spacing, fills, ctx)
+    for spacing, grid_only in ((1.0, False), (0.7, False), (0.7, True)):
+        if grid_only:
+            os.environ["DMX_FILL_GRID"] = "1"
+        try:
+            a, b, made = _both([0.0, 0.0, W, W], lines, spacing, fills, ctx)
+        finally:
+            os.environ.pop("DMX_FILL_GRID", None)
         assert made[2] is False                       # already filled: makePoints false
         _assert_same(a, b)
         st = a.state()
