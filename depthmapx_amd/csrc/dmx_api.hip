@@ -1806,7 +1806,8 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
 }
 
 // VGA global for an arbitrary set of source nodes (multi-GPU shards interleaved over the grid so that
-// every rank gets the same mix of cheap and expensive sources).  Tile-resolved BFS only.
+// every rank gets the same mix of cheap and expensive sources).  The tile-resolved BFS takes the list
+// in one launch; otherwise runs of consecutive nodes go through vga_impl one by one.
 int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
                                int64_t n, float* out_device) {
     SAME_DEVICE(ctx, g);
@@ -1827,12 +1828,32 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
     if (rc) return rc;
     PointMapHost& h = *g->pm->host;
     const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
-    if (g->symmetric != 1 || tw * th > 16 * 1024 || ctx->tile_disabled)
-        return fail(DMX_ERR_UNSUPPORTED, "source lists need the tile-resolved BFS (grid <= 1024^2, symmetric graph)");
-    DevBuf<int32_t> d_list;
-    HIPCHK(d_list.alloc(lst.size()));
-    HIPCHK(hipMemcpyAsync(d_list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    return vga_tile_impl(ctx, g, radius, gates_only, 0, n, out_device, true, nullptr, tw, th, nullptr, 0, nullptr, d_list.p);
+    if (g->symmetric == 1 && tw * th <= 16 * 1024 && !ctx->tile_disabled) {
+        DevBuf<int32_t> d_list;
+        HIPCHK(d_list.alloc(lst.size()));
+        HIPCHK(hipMemcpyAsync(d_list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        rc = vga_tile_impl(ctx, g, radius, gates_only, 0, n, out_device, true, nullptr, tw, th, nullptr, 0, nullptr, d_list.p);
+        if (rc != DMX_ERR_CAPACITY) return rc;
+    }
+    // Grids above 1024^2, asymmetric graphs or a capacity retry: the other BFS kernels take contiguous
+    // source ranges, so each maximal run of consecutive listed nodes is one call (the preparation, and
+    // with it every collective of a sharded preparation, is already done: the ranks may differ in the
+    // number of calls from here on).  Kernel times add up; the work counters are the last call's.
+    const bool was_disabled = ctx->tile_disabled;
+    ctx->tile_disabled = true;
+    double total = 0.0;
+    for (int64_t i = 0; i < n;) {
+        int64_t j = i + 1;
+        while (j < n && lst[j] == lst[j - 1] + 1) j++;
+        rc = vga_impl(ctx, g, radius, gates_only, lst[i], (int64_t)lst[j - 1] + 1, out_device, true, nullptr);
+        if (rc) break;
+        total += ctx->last_vga_s;
+        i = j;
+    }
+    ctx->tile_disabled = was_disabled;
+    if (rc) return rc;
+    ctx->last_vga_s = total;
+    return DMX_OK;
 }
 
 // ---------------------------------------------------------------- VGA metric (all sources)

@@ -127,3 +127,32 @@ def test_visual_stepdepth_above_1024_matches_oracle(ctx):
         want = om.visual_stepdepth(cells)
         np.testing.assert_array_equal(got.view(np.uint32), want.view(np.uint32))
         assert got.max() >= 2
+
+
+def test_vga_source_list_above_1024_matches_full_run(ctx):
+    """dmx_vga_global_device_list past the tile BFS (1100^2): runs of consecutive listed nodes go
+    through the direction-optimising kernel; listed rows equal the full run's, the others are
+    untouched, and a block of them equals the restatement's BFS."""
+    import torch
+    from pyoracle import OracleMap
+    region, lines, sp = _room_map(1100.0, 64.0, 60, seed=9)
+    pm = dmx.PointMap(region, lines, 1.0)
+    assert pm.make_points(*sp)
+    g = pm.make_graph(ctx)
+    full = g.vga_visual_global()
+    n = full.shape[0]
+    rng = np.random.default_rng(3)
+    nodes = np.unique(np.concatenate([rng.choice(n, n // 4, replace=False), np.arange(100, 164)]))
+    out = torch.full((n, 7), -7.0, dtype=torch.float32, device="cuda")
+    g.vga_visual_global_device_list(out.data_ptr(), nodes)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(got[nodes].view(np.uint32), full[nodes].view(np.uint32))
+    assert (got[np.setdiff1d(np.arange(n), nodes)] == -7.0).all()
+    om = OracleMap(region, 1.0, lines)
+    assert om.fill(*sp)
+    om.make_graph(threads=8)
+    ref = om.vga_global(node_begin=100, node_end=164, threads=8)[100:164].astype(np.float64)
+    a = got[100:164].astype(np.float64)
+    np.testing.assert_array_equal(a[:, 5], ref[:, 5])
+    assert (np.abs(a - ref) <= 1e-6 * np.maximum(1.0, np.abs(ref))).all()
