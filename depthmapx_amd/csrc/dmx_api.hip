@@ -1447,12 +1447,12 @@ static int prepare_tiles(dmx_graph* g) {
             HIPCHK(hipMemsetAsync(g->ftvis.p, 0, tv_bytes, s));
         }
         const int ncw = (nt + 3) / 4;
-        const size_t tv_lds = ((size_t)(ncw + 1) / 2 + (size_t)TV_WAVES * (tvw + (ncw + 1) / 2)) * 8;
+        const size_t tv_lds = ((size_t)(ncw + 1) / 2 + (size_t)(tvw + (ncw + 1) / 2)) * 8;   // one node per workgroup
         if (tv_lds > 150 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the tile-visibility pass");
         int64_t pb, pe;
         prep_range(g, pb, pe);
         if (pe > pb) {
-            const int64_t nb = std::min<int64_t>((pe - pb + TV_WAVES - 1) / TV_WAVES, (int64_t)ctx->num_cu * 16);
+            const int64_t nb = std::min<int64_t>(pe - pb, (int64_t)ctx->num_cu * 16);
             hipLaunchKernelGGL(tile_vis_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), tv_lds, s, rows, tw, th,
                                g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb,
                                g->pool.p, g->notuf_tiles.p, g->tvis.p, ftv_on ? g->ftvis.p : nullptr);

@@ -915,8 +915,11 @@ __global__ void tile_heads_kernel(int rows, int tw, const int32_t* node_cell, in
 // tells whether any frontier tile is in view.  The full-visibility row (ftvis) sets the bit only
 // when the cell sees EVERY discoverable (non-seed) cell of the tile: a frontier tile under such a
 // bit is a certain hit for a regular cell (in-set == out-set), so phase C resolves it without a run
-// scan.  One wave per node; the rows and the per-tile covered-cell counts (bytes) are built in LDS.
-constexpr int TV_WAVES = 4;
+// scan.  One workgroup (TV_WAVES waves, threads over the runs) per node; the rows and the per-tile
+// covered-cell counts (bytes) are built in LDS with atomics.  A node per workgroup rather than per
+// wave keeps the LDS per CU small enough for 4 workgroups (32 waves): the run walks are latency
+// bound (divergent per-tile LDS atomics), so occupancy is what pays (1000^2: 0.33 s at 4 waves/CU).
+constexpr int TV_WAVES = 8;
 __device__ __forceinline__ void tv_count(uint32_t* cnt, int t, int c) {
     atomicAdd(&cnt[t >> 2], (uint32_t)c << (8 * (t & 3)));
 }
@@ -928,22 +931,22 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int t
     extern __shared__ __attribute__((aligned(16))) unsigned long long tvlds[];
     const int nt = tw * th, ncw = (nt + 3) / 4;
     const int wr = (tw + 63) / 64, tvw = th * wr;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int TB = 64 * TV_WAVES;
+    const int tid = threadIdx.x;
     uint8_t* nsc = (uint8_t*)tvlds;                                   // [nt] non-seed cells per tile
-    unsigned long long* row = tvlds + (ncw + 1) / 2 + (size_t)wave * (tvw + (ncw + 1) / 2);
+    unsigned long long* row = tvlds + (ncw + 1) / 2;                  // [tvw]
     uint32_t* cnt = (uint32_t*)(row + tvw);                            // [nt] covered non-seed cells (bytes)
     if (ftvis)
-        for (int t = threadIdx.x; t < nt; t += 64 * TV_WAVES) nsc[t] = (uint8_t)__popcll(~seed_tiles[t]);
-    __syncthreads();
-    for (int64_t k = (int64_t)blockIdx.x * TV_WAVES + wave; k < n; k += (int64_t)gridDim.x * TV_WAVES) {
-        for (int w = lane; w < tvw; w += 64) row[w] = 0ull;
+        for (int t = tid; t < nt; t += TB) nsc[t] = (uint8_t)__popcll(~seed_tiles[t]);
+    for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
+        __syncthreads();   // the previous node's rows are written out
+        for (int w = tid; w < tvw; w += TB) row[w] = 0ull;
         if (ftvis)
-            for (int w = lane; w < ncw; w += 64) cnt[w] = 0u;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            for (int w = tid; w < ncw; w += TB) cnt[w] = 0u;
+        __syncthreads();
         const int64_t rs = node_run_start[k];
         const int nr = node_nruns[k];
-        for (int r = lane; r < nr; r += 64) {
+        for (int r = tid; r < nr; r += TB) {
             const Run ru = pool[rs + r];
             if (ru.y0 == ru.y1) {
                 const int y = ru.y0, ty = y >> 3, t0 = ru.x0 >> 3, t1 = ru.x1 >> 3;
@@ -990,17 +993,16 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int t
                 }
             }
         }
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __syncthreads();
         const int c = node_cell[k];
         const int id = tile_id_of(c / rows, c % rows, tw);
         unsigned long long* out = tvis + (size_t)id * tvw;
-        for (int w = lane; w < tvw; w += 64) out[w] = row[w];
+        for (int w = tid; w < tvw; w += TB) out[w] = row[w];
         if (ftvis) {
             // a tile is fully seen when the covered count reaches its non-seed count (a node's runs
             // are disjoint, so no cell is counted twice)
             unsigned long long* fout = ftvis + (size_t)id * tvw;
-            for (int w = lane; w < tvw; w += 64) {
+            for (int w = tid; w < tvw; w += TB) {
                 unsigned long long m = row[w], f = 0ull;
                 const int tyw = w / wr, tx0 = (w % wr) * 64;
                 while (m) {
@@ -1013,7 +1015,6 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int t
                 fout[w] = f;
             }
         }
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
