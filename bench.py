@@ -421,10 +421,10 @@ def main():
         # issue-rate roofline (VALU) for the two hot kernels, and makeGraph's FP64 rate
         issue = {}
         for kname in ("makegraph_kernel", "vga_tile_kernel", "stepdepth_kernel"):
-            e = pmc.get(kname)
-            if e and "valu_active_frac" in e:
-                issue[kname] = {"valu_busy_frac": e["valu_active_frac"], "valu_issue_frac": e.get("valu_issue_frac"),
-                                "wave_cycles_split": e.get("wave_cycles_split"), "clock_ghz": e.get("clock_ghz")}
+            kp = pmc.get(kname)   # (not `e`: b, e is this rank's makeGraph shard, used below)
+            if kp and "valu_active_frac" in kp:
+                issue[kname] = {"valu_busy_frac": kp["valu_active_frac"], "valu_issue_frac": kp.get("valu_issue_frac"),
+                                "wave_cycles_split": kp.get("wave_cycles_split"), "clock_ghz": kp.get("clock_ghz")}
         if issue:
             roof["issue"] = issue
         mkp = pmc.get("makegraph_kernel", {})
