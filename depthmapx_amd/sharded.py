@@ -78,8 +78,10 @@ def exchange_graph(pm, ctx, shard, dist, device):
     if _rccl(dist):
         dist.all_gather_into_tensor(flat, mine)
     else:
-        parts = list(flat.view(world, mx).unbind(0))
-        dist.all_gather(parts, mine)
+        # other backends (gloo rehearsals): gather through host tensors staged explicitly, one per rank
+        parts = [torch.empty(mx, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, mine.cpu())
+        flat.copy_(torch.cat(parts))
     sync()
     t2 = time.perf_counter()
     del mine

@@ -6,8 +6,8 @@ OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/${TAG:-multi}
 mkdir -p $OUT
 W=${W:-256}
 timeout -k 10 300 python bench.py --grid $W --steps 1 --warmup 0 --no-cpu-baseline --dump-out $OUT/one.npy > $OUT/one.log 2>&1 && \
-DMX_DIST_BACKEND=gloo DMX_FORCE_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --grid $W --steps 1 --warmup 1 --no-cpu-baseline \
+DMX_DIST_BACKEND=gloo DMX_FORCE_DEVICE=0 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node ${NPROC:-2} \
+  --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus ${NPROC:-2} --grid $W --steps 1 --warmup 1 --no-cpu-baseline \
   --dump-out $OUT/two.npy ${EXTRA:-} > $OUT/two.log 2>&1 && \
 python -c "
 import numpy as np
