@@ -24,6 +24,14 @@ def _rccl(dist):
         return False
 
 
+def _gather_host(dist, t):
+    """all_gather of equal-shaped tensors on a non-RCCL backend, staged through host memory (gloo
+    rehearsals: its collectives on CUDA tensors are avoided); returns the concatenation on t's device."""
+    parts = [torch.empty(t.shape, dtype=t.dtype) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t.cpu())
+    return torch.cat(parts).to(t.device)
+
+
 def shard_range(n, rank, world):
     """Contiguous, balanced split of n units over `world` ranks."""
     return (n * rank) // world, (n * (rank + 1)) // world
@@ -66,9 +74,12 @@ def exchange_graph(pm, ctx, shard, dist, device):
     t0 = time.perf_counter()
     n = shard.blob_size()
     sz = torch.tensor([n], dtype=torch.int64, device=device)
-    sizes = [torch.zeros_like(sz) for _ in range(world)]
-    dist.all_gather(sizes, sz)
-    sizes = [int(v.item()) for v in sizes]
+    if _rccl(dist):
+        sizes = [torch.zeros_like(sz) for _ in range(world)]
+        dist.all_gather(sizes, sz)
+        sizes = [int(v.item()) for v in sizes]
+    else:
+        sizes = [int(v) for v in _gather_host(dist, sz).tolist()]
     mx = max(sizes)
     mine = torch.empty(mx, dtype=torch.uint8, device=device)
     shard.write_blob_device(mine.data_ptr(), n)
@@ -79,9 +90,7 @@ def exchange_graph(pm, ctx, shard, dist, device):
         dist.all_gather_into_tensor(flat, mine)
     else:
         # other backends (gloo rehearsals): gather through host tensors staged explicitly, one per rank
-        parts = [torch.empty(mx, dtype=torch.uint8) for _ in range(world)]
-        dist.all_gather(parts, mine.cpu())
-        flat.copy_(torch.cat(parts))
+        flat.copy_(_gather_host(dist, mine))
     sync()
     t2 = time.perf_counter()
     del mine
@@ -97,7 +106,8 @@ def choose_mk_mode(dist, device, world, mk_shard_s, exchange_s, shard_frac):
     """--mk-mode auto after a warm-up step run sharded: replicate (every rank builds the whole graph, no
     data-path collective) when building it all costs less than building the shard and exchanging it.
     Times are the max over ranks so that every rank takes the same branch."""
-    t = torch.tensor([mk_shard_s, exchange_s, shard_frac], dtype=torch.float64, device=device)
+    t = torch.tensor([mk_shard_s, exchange_s, shard_frac], dtype=torch.float64,
+                     device=device if _rccl(dist) else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     mk, ex, frac = (float(v) for v in t.tolist())
     replicate_s = mk / max(frac, 1e-9)
@@ -180,9 +190,7 @@ def allgather_rows_chunked(full, n, dist, chunk=4096):
         gathered = torch.empty((world * per, k), dtype=full.dtype, device=full.device)
         dist.all_gather_into_tensor(gathered, mine)
     else:
-        parts = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(parts, mine)
-        gathered = torch.cat(parts)
+        gathered = _gather_host(dist, mine)
     for r in range(world):
         idx = lists[r].to(full.device)
         full[idx] = gathered[r * per: r * per + len(idx)]
