@@ -66,6 +66,8 @@ SIGNATURES = {
     "dmx_chunk_load": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_graph_from_runs": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
     "dmx_graph_set_merges": (_i32, [_vp, _vp, _i64]),
+    "dmx_pointmap_set_merges": (_i32, [_vp, _vp, _i64]),
+    "dmx_chunk_merges": (_i32, [_vp, _vp, _vp]),
     "dmx_chunk_flags": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_chunk_set_column": (_i32, [_vp, _cs, _vp, _vp, _i32, _i32]),
     "dmx_chunk_set_displayed": (_i32, [_vp, _i32]),

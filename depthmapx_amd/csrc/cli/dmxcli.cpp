@@ -438,14 +438,25 @@ struct VisPrep : Mode {
             char nm[512];
             (void)nm;
             int processed = 0;
-            int64_t merges = 0;
-            check(dmx_chunk_flags(ch, &processed, nullptr, &merges, nullptr));
+            check(dmx_chunk_flags(ch, &processed, nullptr, nullptr, nullptr));
             if (unmake) {
                 if (!processed)
                     throw RuntimeException("Current map has not had its graph made so there's nothing to unmake");
-            } else if (merges || (processed && (!fills.empty() || make))) {
-                throw RuntimeException("Filling or making a point map that already has a graph or merge links is not "
-                                       "part of the accelerated path");
+            } else if (processed && (!fills.empty() || make)) {
+                // the reference re-runs sparkGraph2 / makePoints on a map whose attribute rows exist:
+                // AttributeTable::addRow throws a pointer (`throw new std::invalid_argument("Duplicate key")`,
+                // salalib/attributetable.cpp:278) that main's catch (std::exception&) does not catch, so
+                // depthmapXcli aborts; here it is an error with the CLI's exit code
+                throw RuntimeException("The point map already has a graph: unmake it first (-pu)");
+            }
+            // merge links stay on the points (PointMap::read keeps m_merge, pointdata.cpp:1133-1137) and
+            // are written back with them
+            int64_t nlinks = 0;
+            check(dmx_chunk_merges(ch, nullptr, &nlinks));
+            if (nlinks) {
+                std::vector<int32_t> links((size_t)nlinks * 2);
+                check(dmx_chunk_merges(ch, links.data(), &nlinks));
+                check(dmx_pointmap_set_merges(pm, links.data(), nlinks));
             }
             // the map keeps its name: read it back from the chunk header (dXstring: u32 length + bytes)
             uint32_t len = 0;

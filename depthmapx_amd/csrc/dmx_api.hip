@@ -84,16 +84,26 @@ struct BlockCache {
         free_blocks.clear();
         cached = 0;
     }
+    // blocks cached on one device: what an allocation failure there can get back
+    size_t cached_on(int dev) const {
+        size_t b = 0;
+        for (auto it = free_blocks.lower_bound({dev, 0}); it != free_blocks.end() && it->first.first == dev; ++it)
+            b += it->first.second;
+        return b;
+    }
 };
 BlockCache& block_cache() {
     static BlockCache* c = new BlockCache();   // never destroyed: frees at exit would race the runtime
     return *c;
 }
-// free device memory plus the blocks the cache would release on an allocation failure
+// the blocks the cache holds for the current device (added to hipMemGetInfo's free memory: an
+// allocation failure releases them)
 size_t cached_bytes() {
     BlockCache& c = block_cache();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
     std::lock_guard<std::mutex> g(c.m);
-    return c.cached;
+    return c.cached_on(dev);
 }
 hipError_t cached_malloc(void** p, size_t bytes) {
     BlockCache& c = block_cache();
@@ -209,7 +219,13 @@ struct dmx_pointmap {
 struct dmx_graph {
     dmx_ctx* ctx = nullptr;
     dmx_pointmap* pm = nullptr;
-    std::vector<int32_t> merges;   // [m][2] merge links (cell, partner cell), x-major (Point::m_merge)
+    // merge links (Point::m_merge): unique pairs (a < b) of x-major cells; device copies built by
+    // prepare_merges for the searches that follow them
+    std::vector<int32_t> merges;
+    bool merges_ready = false;
+    bool merge_ctxfill = false;      // a merge cell is CONTEXTFILLED
+    DevBuf<int2> d_mpairs;           // [m] (a, b) cells
+    DevBuf<int32_t> d_merge_cell;    // [C] partner cell or -1
     int64_t nnodes = 0, node_begin = 0, node_end = 0;
     int64_t nruns = 0;
     DevBuf<Run> pool;
@@ -252,6 +268,57 @@ struct dmx_graph {
 };
 
 namespace {
+
+// A graph made from a point map follows the map's merge links (Point::m_merge of its points).
+void inherit_merges(dmx_graph* g) {
+    const std::vector<int32_t>& pc = g->pm->host->merge();
+    g->merges.clear();
+    for (size_t c = 0; c < pc.size(); c++)
+        if (pc[c] > (int32_t)c) { g->merges.push_back((int32_t)c); g->merges.push_back(pc[c]); }
+    g->merges_ready = false;
+}
+
+// Device copies of the merge links for the searches; every linked cell must hold a node (the reference
+// calls getNode() on the partner, vgavisualglobal.cpp:116-118).
+int prepare_merges(dmx_graph* g) {
+    if (!g || g->merges_ready || g->merges.empty()) return DMX_OK;   // (a NULL graph fails in the caller)
+    HIPCHK(hipSetDevice(g->ctx->device));
+    const PointMapHost& h = *g->pm->host;
+    const int64_t C = h.cells(), m = (int64_t)g->merges.size() / 2;
+    const auto& st = h.state();
+    std::vector<int32_t> per_cell((size_t)C, -1);
+    std::vector<int2> pairs((size_t)m);
+    g->merge_ctxfill = false;
+    for (int64_t i = 0; i < m; i++) {
+        const int32_t a = g->merges[2 * i], b = g->merges[2 * i + 1];
+        if (!(st[a] & CELL_FILLED) || !(st[b] & CELL_FILLED)) return fail(DMX_ERR_ARG, "merge link to a cell without a node");
+        if ((st[a] | st[b]) & CELL_CONTEXTFILLED) g->merge_ctxfill = true;
+        per_cell[a] = b;
+        per_cell[b] = a;
+        pairs[i] = make_int2(a, b);
+    }
+    HIPCHK(g->d_mpairs.alloc(m));
+    HIPCHK(g->d_merge_cell.alloc(C));
+    HIPCHK(hipMemcpyAsync(g->d_mpairs.p, pairs.data(), m * sizeof(int2), hipMemcpyHostToDevice, g->ctx->stream));
+    HIPCHK(hipMemcpyAsync(g->d_merge_cell.p, per_cell.data(), C * 4, hipMemcpyHostToDevice, g->ctx->stream));
+    HIPCHK(hipStreamSynchronize(g->ctx->stream));
+    g->merges_ready = true;
+    return DMX_OK;
+}
+
+// Merge links whose outcome depends on the reference's pop order within a BFS level: a partner that is
+// CONTEXTFILLED at an odd PixelRef is counted/extracted or not depending on which end is popped first
+// when the analysis does not expand such cells (VGA global with a radius, visual step depth:
+// vgavisualglobal.cpp:104-122, vgavisualglobaldepth.cpp:52-63).  Only SEMIFILL (the GUI's context fill)
+// makes such cells; these maps are refused rather than analysed with a guessed order.
+int refuse_ordered_merges(dmx_graph* g, bool contextfill_limits_expansion) {
+    if (!g || g->merges.empty() || !contextfill_limits_expansion) return DMX_OK;
+    if (int rc = prepare_merges(g)) return rc;
+    if (g->merge_ctxfill)
+        return fail(DMX_ERR_UNSUPPORTED, "merge links on context-filled cells make this analysis depend on the "
+                                         "reference's pop order");
+    return DMX_OK;
+}
 
 int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     PointMapHost& h = *pm->host;
@@ -332,6 +399,25 @@ __global__ void gather_runs_kernel(const Run* pool, const int64_t* start, const 
     if (k >= n) return;
     const int64_t s = start[k], d = dst_off[k];
     for (int i = threadIdx.x; i < nruns[k]; i += blockDim.x) dst[d + i] = pool[s + i];
+}
+
+// Merge links as unique pairs (a < b): both directions of a pair may be listed (PointMap::write stores
+// m_merge on both points), every cell belongs to at most one pair (PointMap::mergePixels,
+// pointdata.cpp:1653-1680, unlinks a cell's previous partner).  per_cell[c] = partner or -1.
+int normalize_merges(int64_t C, const int32_t* pairs, int64_t n, std::vector<int32_t>& per_cell,
+                     std::vector<int32_t>& uniq) {
+    per_cell.assign(n ? (size_t)C : 0, -1);
+    uniq.clear();
+    for (int64_t i = 0; i < n; i++) {
+        const int32_t a = pairs[2 * i], b = pairs[2 * i + 1];
+        if (a < 0 || b < 0 || a >= C || b >= C || a == b) return fail(DMX_ERR_ARG, "merge link outside the grid");
+        if ((per_cell[a] >= 0 && per_cell[a] != b) || (per_cell[b] >= 0 && per_cell[b] != a))
+            return fail(DMX_ERR_ARG, "a cell with two merge links");
+        if (per_cell[a] < 0) { uniq.push_back(std::min(a, b)); uniq.push_back(std::max(a, b)); }
+        per_cell[a] = b;
+        per_cell[b] = a;
+    }
+    return DMX_OK;
 }
 
 size_t makegraph_lds(int gcap, int bcap, int D) {
@@ -747,6 +833,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     g->nnodes = N;
     g->node_begin = node_begin;
     g->node_end = node_end;
+    inherit_merges(g.get());
     const int D = std::max(h.cols(), h.rows());
     HIPCHK(g->node_run_start.alloc(std::max<int64_t>(n, 1)));
     HIPCHK(g->node_nruns.alloc(std::max<int64_t>(n, 1)));
@@ -1118,6 +1205,7 @@ int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const*
     }
     std::unique_ptr<dmx_graph> g(new dmx_graph());
     g->ctx = ctx; g->pm = pm; g->nnodes = N; g->node_begin = 0; g->node_end = N; g->nruns = total_runs;
+    inherit_merges(g.get());
     HIPCHK(g->node_run_start.alloc(std::max<int64_t>(N, 1)));
     HIPCHK(g->node_nruns.alloc(std::max<int64_t>(N, 1)));
     HIPCHK(g->bin_nruns.alloc(std::max<int64_t>(N, 1) * 32));
@@ -1561,6 +1649,8 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.src_begin = sb; Q.src_end = se; Q.radius = (int)radius; Q.gates_only = gates_only;
     Q.uf_count = g->uf_count;
     Q.seeds = d_seeds; Q.nseeds = nseeds; Q.cell_level = d_cell_level;
+    Q.nmp = (int)(g->merges.size() / 2);
+    Q.mpairs = Q.nmp ? g->d_mpairs.p : nullptr;
     Q.src_list = d_src_list;   // [sb, se) index this list of source nodes (out must be on the device)
     // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
     Q.alpha = 60;   // top-down costs a frontier cell its whole run list (~R/N runs): keep it rare
@@ -1744,6 +1834,9 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     Q.work_counter = P.work_counter; Q.scratch = frontier.p; Q.nnodes = N; Q.maxlev = maxlev;
     Q.out = outp; Q.levels_out = P.levels_out; Q.error = P.error; Q.stats = P.stats;
     Q.gbm = gbm ? gbm_buf.p : nullptr;
+    Q.nmp = (int)(g->merges.size() / 2);
+    Q.mpairs = Q.nmp ? g->d_mpairs.p : nullptr;
+    if (!use_do && Q.nmp) return fail(DMX_ERR_UNSUPPORTED, "the top-down v1 kernel does not follow merge links");
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (nsrc > 0) {
         if (gbm) hipLaunchKernelGGL(vga_do_kernel<true>, dim3((unsigned)blocks), dim3(DO_THREADS), lds, ctx->stream, Q);
@@ -1779,29 +1872,19 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     return DMX_OK;
 }
 
-// getMergePixel (vgavisualglobal.cpp:113-122, vgavisualglobaldepth.cpp:55-64, vgametric.cpp:97-104,
-// vgaangular.cpp:95-102, vgametricdepth.cpp:68-82, vgaangulardepth.cpp:57-66): a merge link joins two
-// cells' neighbourhoods, with per-analysis bookkeeping of the partner.  The GPU searches do not follow
-// merge links; maps that have them are refused rather than analysed differently (VGA visual local
-// has no merge logic and runs).
-static int refuse_merges(const dmx_graph* g) {
-    if (g && !g->merges.empty())
-        return fail(DMX_ERR_UNSUPPORTED, "point maps with merge links (LINK mode) are not on the accelerated path of "
-                                         "this analysis");
-    return DMX_OK;
-}
-
 int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
                    int64_t* levels) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = refuse_ordered_merges(g, radius != -1.0)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out, false, levels);
 }
 
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se,
                           float* out_device) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = refuse_ordered_merges(g, radius != -1.0)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out_device, true, nullptr);
 }
 
@@ -1812,7 +1895,8 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
                                int64_t n, float* out_device) {
     SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out_device || (n > 0 && !nodes)) return fail(DMX_ERR_ARG, "bad arguments");
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = refuse_ordered_merges(g, radius != -1.0)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
     HIPCHK(hipSetDevice(ctx->device));
@@ -1887,6 +1971,7 @@ static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
             if (ex) { f |= SDF_EXPAND; nexp++; }
             flags[c] = f;
         }
+    for (size_t i = 0; i < g->merges.size(); i++) { flags[g->merges[i]] |= SDF_MERGE; nexp++; }
     hipStream_t s = ctx->stream;
     int occ = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_metric_kernel<ANG>, SD_THREADS, 0));
@@ -1937,6 +2022,7 @@ static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
         P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
         P.key = d_key.p; P.mdist = d_mdist.p; P.cum = d_cum.p; P.lastpix = d_last.p;
         P.over = d_over.p; P.over_cap = cap_used; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
+        P.merge = g->merges.empty() ? nullptr : g->d_merge_cell.p;
         HIPCHK(hipEventRecord(ctx->ev0, s));
         hipLaunchKernelGGL(vga_metric_kernel<ANG>, dim3((unsigned)nbl), dim3(SD_THREADS), 0, s, P, C, g->pm->d_node_cell.p,
                            list ? 0 : sb, list ? todo : se, gates_only, h.spacing(), radius < 0 ? -1.0 : radius, d_comp.p,
@@ -1975,13 +2061,13 @@ static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
 
 int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     return vga_search_all<false>(ctx, g, radius, gates_only, sb, se, out);
 }
 
 int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     return vga_search_all<true>(ctx, g, radius, gates_only, sb, se, out);
 }
 
@@ -2206,6 +2292,7 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
             flags[c] = f;
         }
     for (int32_t c : sel) flags[c] |= SDF_EXPAND;
+    for (size_t i = 0; i < g->merges.size(); i++) { flags[g->merges[i]] |= SDF_MERGE; nexp++; }
     hipStream_t s = ctx->stream;
     DevBuf<uint8_t> d_flags;
     DevBuf<unsigned long long> d_key, d_over;
@@ -2223,7 +2310,8 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
     int64_t cap = 8 * (nexp + (int64_t)sel.size()) + SD_WIN + 1024 + (ANG ? 8 * N : 0);
     // metric: the batched search over the whole GPU (stepdepth.hip, "batched metric step depth");
     // DMX_SD_KERNEL=serial forces the one-workgroup kernel, which is also the fallback
-    bool batched = !ANG;
+    // (merge links: the serial kernel, which extracts a partner at its link's pop)
+    bool batched = !ANG && g->merges.empty();
     if (const char* e = getenv("DMX_SD_KERNEL")) batched = batched && strcmp(e, "serial") != 0;
     ctx->last_sd_mode = 0;
     if (batched) {
@@ -2260,6 +2348,7 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
         P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
         P.key = d_key.p; P.mdist = d_mdist.p; P.cum = d_cum.p; P.lastpix = d_last.p;
         P.over = d_over.p; P.over_cap = cap; P.error = ctx->counters.p + 1; P.stats = ctx->stats.p;
+        P.merge = g->merges.empty() ? nullptr : g->d_merge_cell.p;
         HIPCHK(hipEventRecord(ctx->ev0, s));
         hipLaunchKernelGGL(stepdepth_kernel<ANG>, dim3(1), dim3(SD_THREADS), 0, s, P, d_sel.p, (int)sel.size());
         HIPCHK(hipGetLastError());
@@ -2301,13 +2390,13 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
 
 int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     return stepdepth_impl<false>(ctx, g, sel_cells, nsel, out);
 }
 
 int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     return stepdepth_impl<true>(ctx, g, sel_cells, nsel, out);
 }
 
@@ -2358,6 +2447,13 @@ static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vecto
                            (const int32_t*)fr[cur].p, nf, g->node_run_start.p, g->node_nruns.p, g->pool.p,
                            g->pm->d_cell_node.p, g->pm->d_node_flags.p, L + 1, vis.p, level.p, fr[cur ^ 1].p, cnt.p);
         HIPCHK(hipGetLastError());
+        if (!g->merges.empty()) {
+            const int nmp = (int)(g->merges.size() / 2);
+            hipLaunchKernelGGL(vsd_merge_kernel, dim3((unsigned)((nmp + 255) / 256)), dim3(256), 0, s, rows, tw,
+                               (const int2*)g->d_mpairs.p, nmp, g->pm->d_cell_node.p, L + 1, vis.p, level.p,
+                               fr[cur ^ 1].p, cnt.p);
+            HIPCHK(hipGetLastError());
+        }
         unsigned long long n_next = 0;
         HIPCHK(copy_sync(s, &n_next, cnt.p, 8, hipMemcpyDeviceToHost));
         cur ^= 1;
@@ -2380,7 +2476,8 @@ static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vecto
 int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
-    if (int rc = refuse_merges(g)) return rc;
+    if (int rc = refuse_ordered_merges(g, true)) return rc;
+    if (int rc = prepare_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
     HIPCHK(hipSetDevice(ctx->device));
@@ -2406,6 +2503,22 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
         }
     }
     if (seeds.empty()) return fail(DMX_ERR_STATE, "no filled cell selected");
+    // a selected cell's merge pixel takes level 0 and is extracted with it (vgavisualglobaldepth.cpp:55-63)
+    if (!g->merges.empty()) {
+        const auto& nc = g->pm->node_cell;
+        std::vector<int32_t> add;
+        for (size_t i = 0; i < g->merges.size(); i += 2) {
+            const int32_t a = g->merges[i], b = g->merges[i + 1];
+            const int32_t na = (int32_t)(std::lower_bound(nc.begin(), nc.end(), a) - nc.begin());
+            const int32_t nb = (int32_t)(std::lower_bound(nc.begin(), nc.end(), b) - nc.begin());
+            const bool sa = std::binary_search(seeds.begin(), seeds.end(), na);
+            const bool sb = std::binary_search(seeds.begin(), seeds.end(), nb);
+            if (sa && !sb) add.push_back(nb);
+            if (sb && !sa) add.push_back(na);
+        }
+        seeds.insert(seeds.end(), add.begin(), add.end());
+        std::sort(seeds.begin() + 1, seeds.end());   // seeds[0] stays the first selected cell
+    }
     const int tw = (cols + 7) / 8, th = (rows + 7) / 8, nt = tw * th;
     bool tile = nt <= 16 * 1024 && !getenv("DMX_VSD_TOPDOWN");
     int rc = DMX_OK;
@@ -2489,6 +2602,7 @@ int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const in
     if (acc != nruns) return fail(DMX_ERR_ARG, "bins do not account for the runs");
     std::unique_ptr<dmx_graph> g(new dmx_graph());
     g->ctx = ctx; g->pm = pm; g->nnodes = N; g->node_begin = 0; g->node_end = N; g->nruns = nruns;
+    inherit_merges(g.get());
     HIPCHK(g->pool.alloc(std::max<int64_t>(nruns, 1)));
     HIPCHK(g->node_run_start.alloc(std::max<int64_t>(N, 1)));
     HIPCHK(g->node_nruns.alloc(std::max<int64_t>(N, 1)));
@@ -2619,15 +2733,45 @@ int dmx_chunk_load(dmx_ctx* ctx, const dmx_chunk* c, const double* region, dmx_p
     int rc = dmx_graph_from_runs(ctx, pm.get(), N, p.bins.data(), p.runs.data(), (int64_t)p.runs.size() / 4,
                                  p.gridconn.data(), attrs.data(), &g);
     if (rc) return rc;
-    g->merges = p.merge_pairs;
+    std::unique_ptr<dmx_graph> gg(g);
+    rc = dmx_pointmap_set_merges(pm.get(), p.merge_pairs.data(), (int64_t)p.merge_pairs.size() / 2);
+    if (rc) return rc;
+    inherit_merges(g);
     *pm_out = pm.release();
-    *g_out = g;
+    *g_out = gg.release();
+    return DMX_OK;
+}
+
+int dmx_pointmap_set_merges(dmx_pointmap* pm, const int32_t* cell_pairs, int64_t n) {
+    if (!pm || n < 0 || (n && !cell_pairs)) return fail(DMX_ERR_ARG, "bad arguments");
+    std::vector<int32_t> per_cell, uniq;
+    if (int rc = normalize_merges(pm->host->cells(), cell_pairs, n, per_cell, uniq)) return rc;
+    pm->host->set_merge(std::move(per_cell));
     return DMX_OK;
 }
 
 int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n) {
     if (!g || n < 0 || (n && !cell_pairs)) return fail(DMX_ERR_ARG, "bad arguments");
-    g->merges.assign(cell_pairs, cell_pairs + 2 * n);
+    std::vector<int32_t> per_cell, uniq;
+    if (int rc = normalize_merges(g->pm->host->cells(), cell_pairs, n, per_cell, uniq)) return rc;
+    g->merges = std::move(uniq);
+    g->merges_ready = false;
+    return DMX_OK;
+}
+
+int dmx_chunk_merges(const dmx_chunk* c, int32_t* cell_pairs, int64_t* n) {
+    if (!c || !n) return fail(DMX_ERR_ARG, "bad arguments");
+    std::vector<int32_t> per_cell, uniq;
+    const ParsedChunk& p = c->pc;
+    if (int rc = normalize_merges((int64_t)p.cols * p.rows, p.merge_pairs.data(), (int64_t)p.merge_pairs.size() / 2,
+                                  per_cell, uniq))
+        return rc;
+    const int64_t m = (int64_t)uniq.size() / 2;
+    if (cell_pairs) {
+        if (*n < m) return fail(DMX_ERR_ARG, "buffer too small");
+        std::memcpy(cell_pairs, uniq.data(), uniq.size() * 4);
+    }
+    *n = m;
     return DMX_OK;
 }
 

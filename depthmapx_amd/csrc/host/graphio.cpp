@@ -165,8 +165,10 @@ int write_pointmap_chunk(const PointMapHost& h, int64_t nnodes, const int32_t* b
             w.put<int32_t>(0);   // m_block
             w.put<int32_t>(0);   // dummy
             w.put<int8_t>(node ? (int8_t)gridconn[k] : 0);
-            w.put<int16_t>(-1);  // m_merge = NoPixel
-            w.put<int16_t>(-1);
+            // m_merge: PixelRef {short x, short y} of the partner, NoPixel = (-1, -1)
+            const int32_t mc = h.merge().empty() ? -1 : h.merge()[(size_t)h.index(x, y)];
+            w.put<int16_t>(mc >= 0 ? (int16_t)(mc / C_rows) : (int16_t)-1);
+            w.put<int16_t>(mc >= 0 ? (int16_t)(mc % C_rows) : (int16_t)-1);
             w.put<uint8_t>(node ? 1 : 0);
             if (node) {
                 for (int b = 0; b < 32; b++) {

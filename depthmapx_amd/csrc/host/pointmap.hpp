@@ -63,6 +63,10 @@ class PointMapHost {
     const std::vector<int32_t>& seg_off() const { return seg_off_; }
     const std::vector<double>& segs() const { return segs_; }
     bool lines_blocked() const { return blocked_; }
+    // Point::m_merge of every cell: the merge partner (x-major cell) or -1; empty when the map has no
+    // merge links (PointMap::mergePixels, pointdata.cpp:1653-1680: both ends point at each other).
+    const std::vector<int32_t>& merge() const { return merge_; }
+    void set_merge(std::vector<int32_t>&& m) { merge_ = std::move(m); }
 
   private:
     void rasterise(const Seg& l, std::vector<int32_t>& out) const;
@@ -82,6 +86,7 @@ class PointMapHost {
     std::vector<double> segs_;
     bool blocked_ = false;
     int64_t filled_ = 0;
+    std::vector<int32_t> merge_;
 };
 
 } // namespace dmx

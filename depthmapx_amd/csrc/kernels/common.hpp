@@ -54,4 +54,54 @@ __device__ __forceinline__ int ctl_poll(DmxCtl* c, int w) {
     return w;
 }
 
+// Merge links (getMergePixel, vgavisualglobal.cpp:113-122, vgavisualglobaldepth.cpp:55-63): when a cell
+// is expanded at level L, its merge partner -- unless already visited -- is extracted at level L as well
+// and marked done without being counted.  With every cell of a level expanded (radius n, or a level
+// below the radius; context-filled merge cells are refused by the host where they would not expand),
+// the outcome does not depend on the pop order inside the level: per link, exactly one end is counted,
+// at the level the first end is discovered, and both ends' runs feed the next level.  So after level L
+// is published in the frontier F (its cells are new and expandable), for each link (a, b):
+//   a and b both in F: both were discovered at L, one of them is not counted (mcorr);
+//   one end in F, the other not yet visited: the other joins F and V at L, uncounted (cell_level = L
+//   in seed mode); a partner that is discoverable at all counts towards the early-exit total (mdisc).
+// The BFS kernels pre-set V with the never-discoverable seed cells, so "visited" is V without them.
+// Tiled bitmaps: word (y >> 3) * tw + (x >> 3), bit (y & 7) * 8 + (x & 7); V in LDS (v_lds) or in
+// per-workgroup HBM; Fsr / Fsc: optional per-tile frontier summaries of vga_tile.hip.
+__device__ __forceinline__ void merge_level_pass(const int2* mpairs, int nmp, int rows, int tw, int ntpb,
+                                                 unsigned long long* F, unsigned long long* V, bool v_lds,
+                                                 const unsigned long long* seed_tiles, unsigned long long* Fsr,
+                                                 unsigned long long* Fsc, int wr, int wc, int32_t* cell_level,
+                                                 int lev, unsigned long long* mcorr, unsigned long long* mdisc,
+                                                 unsigned long long* mass) {
+    for (int i = threadIdx.x; i < nmp; i += ntpb) {
+        const int2 pr = mpairs[i];
+        const int ax = pr.x / rows, ay = pr.x % rows, bx = pr.y / rows, by = pr.y % rows;
+        const int at = (ay >> 3) * tw + (ax >> 3), bt = (by >> 3) * tw + (bx >> 3);
+        const unsigned long long ab = 1ull << ((ay & 7) * 8 + (ax & 7)), bb = 1ull << ((by & 7) * 8 + (bx & 7));
+        const bool fa = (F[at] & ab) != 0ull, fb = (F[bt] & bb) != 0ull;
+        if (fa && fb) {
+            atomicAdd(mcorr, 1ull);
+        } else if (fa || fb) {
+            const int ot = fa ? bt : at;
+            const unsigned long long ob = fa ? bb : ab;
+            const bool seed = (seed_tiles[ot] & ob) != 0ull;
+            const unsigned long long vw =
+                v_lds ? V[ot] : __hip_atomic_load(&V[ot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (seed || !(vw & ob)) {
+                atomicOr(&F[ot], ob);
+                if (v_lds) atomicOr(&V[ot], ob);
+                else __hip_atomic_fetch_or(&V[ot], ob, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (Fsr) {
+                    const int tx = ot % tw, ty = ot / tw;
+                    atomicOr(&Fsr[ty * wr + (tx >> 6)], 1ull << (tx & 63));
+                    if (Fsc) atomicOr(&Fsc[tx * wc + (ty >> 6)], 1ull << (ty & 63));
+                }
+                if (cell_level) cell_level[(size_t)ot * 64 + __ffsll((long long)ob) - 1] = lev;
+                if (!seed) atomicAdd(mdisc, 1ull);
+                atomicAdd(mass, 1ull);
+            }
+        }
+    }
+}
+
 } // namespace dmx

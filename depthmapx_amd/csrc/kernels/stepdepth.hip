@@ -31,7 +31,10 @@ constexpr int SD_CHUNK = 32;       // cells per chunk
 constexpr int SD_BATCH = 8;        // cells whose state one lane loads at once
 constexpr unsigned long long SD_INF = ~0ull;
 
-enum : uint8_t { SDF_FILLED = 1, SDF_EXPAND = 2 };
+// SDF_MERGE: the cell has a merge link (Point::m_merge): it is queued even when it does not expand,
+// because its pop extracts the partner (vgametricdepth.cpp:68-83, vgametric.cpp:97-105,
+// vgaangular.cpp:95-104, vgaangulardepth.cpp:57-67)
+enum : uint8_t { SDF_FILLED = 1, SDF_EXPAND = 2, SDF_MERGE = 4 };
 
 struct StepDepthParams {
     int cols, rows;
@@ -46,6 +49,7 @@ struct StepDepthParams {
     int32_t* lastpix;              // [C] lastpixel of the queued entry with the smallest key (-1: NoPixel)
     unsigned long long* over;      // HBM overflow list of queue keys
     int64_t over_cap;
+    const int32_t* merge;          // [C] merge partner cell or -1 (nullptr: the map has no merge links)
     int* error;
     unsigned long long* stats;     // [0] expanders popped, [1] cells relaxed, [2] refills
 };
@@ -113,7 +117,7 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
             if (nk < kv) {
                 P.key[c] = nk;
                 P.lastpix[c] = pix_of(ux, uy);
-                if ((f & SDF_EXPAND) || nv == 0.0f) sd_push(S, P, nk);
+                if ((f & (SDF_EXPAND | SDF_MERGE)) || nv == 0.0f) sd_push(S, P, nk);
             }
         }
         return;
@@ -129,7 +133,7 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
         if (nk < kv) {                    // a new smallest entry: it carries this lastpixel
             P.key[c] = nk;
             P.lastpix[c] = pix_of(ux, uy);
-            if (f & SDF_EXPAND) sd_push(S, P, nk);
+            if (f & (SDF_EXPAND | SDF_MERGE)) sd_push(S, P, nk);
         }
     }
 }
@@ -168,6 +172,36 @@ __device__ __forceinline__ void sd_relax_span(SdShared& S, const StepDepthParams
             }
         }
     }
+}
+
+// Relax every cell of a node's runs from u = (ux, uy) (Node::extractMetric / extractAngular): runs up
+// to SD_CHUNK cells by their thread, longer tails through the LDS chunk queue (S.nchunk must be 0).
+// A cell is "already popped" for u iff its key is below ku.
+template <bool ANG>
+__device__ void sd_relax_node(SdShared& S, const StepDepthParams& P, int node, int ux, int uy, float du, float cumu,
+                              int lastu, unsigned long long ku, unsigned& relaxed) {
+    const int tid = threadIdx.x;
+    const int64_t rs = P.node_run_start[node];
+    const int nr = P.node_nruns[node];
+    for (int r = tid; r < nr; r += SD_THREADS) {
+        const Run ru = P.pool[rs + r];
+        const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+        sd_relax_span<ANG>(S, P, ru, 0, min(len, SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
+        for (int o = SD_CHUNK; o < len; o += SD_CHUNK) {
+            const int q = atomicAdd(&S.nchunk, 1);
+            if (q < SD_CHUNKQ) S.chunk[q] = make_int2(r, o);
+            else sd_relax_span<ANG>(S, P, ru, o, min(len, o + SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
+        }
+    }
+    __syncthreads();
+    const int nch = min(S.nchunk, SD_CHUNKQ);
+    for (int j = tid; j < nch; j += SD_THREADS) {
+        const int2 ch = S.chunk[j];
+        const Run ru = P.pool[rs + ch.x];
+        const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
+        sd_relax_span<ANG>(S, P, ru, ch.y, min(len, ch.y + SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
+    }
+    __syncthreads();
 }
 
 // The search of one workgroup from the nsel selected cells (all at distance 0).  rlim >= 0 stops it
@@ -290,29 +324,31 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
         popped++;
         const float cumu = P.cum[uc];
         const int lastu = P.lastpix[uc];
-        const int node = P.cell_node[uc];
-        const int64_t rs = P.node_run_start[node];
-        const int nr = P.node_nruns[node];
-        // ---- relax: runs up to SD_CHUNK cells by their thread, longer tails through the chunk queue
-        for (int r = tid; r < nr; r += SD_THREADS) {
-            const Run ru = P.pool[rs + r];
-            const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
-            sd_relax_span<ANG>(S, P, ru, 0, min(len, SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
-            for (int o = SD_CHUNK; o < len; o += SD_CHUNK) {
-                const int q = atomicAdd(&S.nchunk, 1);
-                if (q < SD_CHUNKQ) S.chunk[q] = make_int2(r, o);
-                else sd_relax_span<ANG>(S, P, ru, o, min(len, o + SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
+        // ---- relax: Node::extractMetric / extractAngular expand at distance (angle) 0, at BLOCKED and
+        // at blocked-adjacent cells (ngraph.cpp:67-85); only merge-linked cells are queued otherwise
+        if ((P.flags[uc] & SDF_EXPAND) || du == 0.0f)
+            sd_relax_node<ANG>(S, P, P.cell_node[uc], ux, uy, du, cumu, lastu, ku, relaxed);
+        // ---- merge pixel not popped yet: it takes u's cumulative angle and is extracted now from
+        // (here.dist, merge pixel, NoPixel), then counts as popped (vgametricdepth.cpp:68-83,
+        // vgaangulardepth.cpp:57-67); its key becomes ku, so every later expander skips it and the
+        // step-depth rows read u's distance; lastpix -2 marks it for VGAMetric/VGAAngular, which do not
+        // count it (vgametric.cpp:97-110, vgaangular.cpp:95-106)
+        if (P.merge) {
+            const int m2 = P.merge[uc];
+            const bool take = m2 >= 0 && !(P.key[m2] < ku);
+            __syncthreads();   // every lane has read key[m2]
+            if (take) {
+                if (tid == 0) {
+                    P.key[m2] = ku;
+                    P.cum[m2] = cumu;
+                    P.lastpix[m2] = -2;
+                    S.nchunk = 0;
+                }
+                __syncthreads();
+                if ((P.flags[m2] & SDF_EXPAND) || du == 0.0f)
+                    sd_relax_node<ANG>(S, P, P.cell_node[m2], m2 / P.rows, m2 % P.rows, du, cumu, -1, ku + 1ull, relaxed);
             }
         }
-        __syncthreads();
-        const int nch = min(S.nchunk, SD_CHUNKQ);
-        for (int j = tid; j < nch; j += SD_THREADS) {
-            const int2 ch = S.chunk[j];
-            const Run ru = P.pool[rs + ch.x];
-            const int len = max(ru.x1 - ru.x0, max(ru.y1 - ru.y0, ru.y0 - ru.y1)) + 1;
-            sd_relax_span<ANG>(S, P, ru, ch.y, min(len, ch.y + SD_CHUNK), ux, uy, du, cumu, lastu, ku, relaxed);
-        }
-        __syncthreads();
     }
     __syncthreads();
 }
@@ -705,7 +741,7 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
         unsigned md = 0u;
         for (int64_t c = tid; c < C; c += SD_THREADS) {
             const unsigned long long k = P.key[c];
-            if (k == SD_INF) continue;
+            if (k == SD_INF || (P.merge && P.lastpix[c] == -2)) continue;   // merged partners are not counted
             const float d = __uint_as_float((unsigned)(k >> 32));
             if (radius >= 0.0 && (ANG ? (double)d : (double)d * spacing) > radius) continue;
             n++;
@@ -723,7 +759,7 @@ __global__ void __launch_bounds__(SD_THREADS) vga_metric_kernel(StepDepthParams 
         // histogram + compaction (any order)
         for (int64_t c = tid; c < C; c += SD_THREADS) {
             const unsigned long long k = P.key[c];
-            if (k == SD_INF) continue;
+            if (k == SD_INF || (P.merge && P.lastpix[c] == -2)) continue;
             const float d = __uint_as_float((unsigned)(k >> 32));
             if (radius >= 0.0 && (ANG ? (double)d : (double)d * spacing) > radius) continue;
             const int bk = min(VM_BUCKETS - 1, (int)(d * inv));

@@ -53,6 +53,8 @@ struct VgaDoParams {
     unsigned long long* stats;  // [0] runs read, [2] cells reached, [3] bottom-up levels, [4] top-down levels,
                                 // [5] bottom-up cells that scanned every run without a hit, [6] their runs
     unsigned long long* gbm;    // GBM variant: per workgroup 3*tw*th words (V, F, X) in HBM
+    const int2* mpairs;         // [nmp] merge links (cell a, cell b), x-major (nullptr: none)
+    int nmp;
 };
 
 constexpr int DO_THREADS = 256;
@@ -155,9 +157,10 @@ __device__ __forceinline__ int run_push(unsigned long long* V, unsigned long lon
 }
 
 struct DoShared {
-    int list_n, hard_n, item, pad;
+    int list_n, hard_n, item, mpart;
     unsigned long long cnt, mass;   // next-level count and its expandable part
     unsigned long long tdnew;       // cells discovered so far in a top-down level
+    unsigned long long mcorr, mdisc;   // merge pass (vga_tile.hip, merge_level_pass)
 };
 
 // GBM = false: V/F/X bitmaps in LDS (grids up to ~1.7e5 cells); true: in HBM (per-workgroup slice).
@@ -201,11 +204,34 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
             X[i] = 0ull;
         }
         for (int i = tid; i < P.maxlev + 4; i += DO_THREADS) hist[i] = 0;
-        if (tid == 0) { hist[0] = 1; S->cnt = 0; S->mass = 0; S->list_n = 0; S->hard_n = 0; S->item = 0; S->tdnew = 0; }
+        if (tid == 0) {
+            hist[0] = 1; S->cnt = 0; S->mass = 0; S->list_n = 0; S->hard_n = 0; S->item = 0; S->tdnew = 0;
+            S->mpart = -1; S->mcorr = 0; S->mdisc = 0;
+        }
         const bool s_in_uf = (P.uf_tiles[stile] & sbit) != 0;
-        const long long target = P.uf_count - (s_in_uf ? 1 : 0); // cells still to discover
+        long long target = P.uf_count - (s_in_uf ? 1 : 0); // cells still to discover
+        long long m_f = 1;
+        if (P.nmp) {
+            // the source's merge partner is extracted at level 0, uncounted (vgavisualglobal.cpp:113-122)
+            __syncthreads();
+            for (int i = tid; i < P.nmp; i += DO_THREADS) {
+                const int2 pr = P.mpairs[i];
+                if (pr.x == scell) S->mpart = pr.y;
+                else if (pr.y == scell) S->mpart = pr.x;
+            }
+            __syncthreads();
+            const int pc = S->mpart;
+            if (pc >= 0) {
+                const int px = pc / rows, py = pc % rows;
+                const int pt = (py >> 3) * tw + (px >> 3);
+                const unsigned long long pb = 1ull << ((py & 7) * 8 + (px & 7));
+                if (tid == 0) { V[pt] |= pb; F[pt] |= pb; }
+                if (P.uf_tiles[pt] & pb) target--;
+                m_f = 2;
+            }
+        }
         // Beamer's direction test on cell counts: frontier size vs cells still unvisited
-        long long m_f = 1, m_u = target;
+        long long m_u = target;
         long long discovered = 0;
         int level = 0, nlev = 1;
         bool overflow = false;
@@ -371,15 +397,21 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                 m_loc += __shfl_xor(m_loc, off);
             }
             if (lane == 0 && c_loc) { atomicAdd(&S->cnt, c_loc); atomicAdd(&S->mass, m_loc); }
+            if (P.nmp && (P.radius == -1 || level + 1 < P.radius)) {
+                __syncthreads();   // the new level is in F and V
+                merge_level_pass(P.mpairs, P.nmp, rows, tw, DO_THREADS, F, V, !GBM, P.seed_tiles, nullptr, nullptr, 0, 0,
+                                 nullptr, level + 1, &S->mcorr, &S->mdisc, &S->mass);
+            }
             __syncthreads();
             const long long cnt = (long long)S->cnt, mass = (long long)S->mass;
+            const long long mcorr = (long long)S->mcorr, mdisc = (long long)S->mdisc;
             __syncthreads();
-            if (tid == 0) { S->cnt = 0; S->mass = 0; }
+            if (tid == 0) { S->cnt = 0; S->mass = 0; S->mcorr = 0; S->mdisc = 0; }
             if (cnt == 0) break;
             if (level + 1 >= P.maxlev) { overflow = true; break; }
-            if (tid == 0) hist[level + 1] = (int)cnt;
-            discovered += cnt;
-            m_u -= cnt;
+            if (tid == 0) hist[level + 1] = (int)(cnt - mcorr);
+            discovered += cnt + mdisc;
+            m_u -= cnt + mdisc;
             m_f = mass;
             level++;
             nlev = level + 1;

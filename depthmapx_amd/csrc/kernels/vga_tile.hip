@@ -78,6 +78,8 @@ struct VgaTileParams {
     int32_t* cell_level;
     int bext;                 // phase-B runs after the heads (BEXT_DEFAULT)
     int crk;                  // tile-common runs tested in phase A (<= CRK)
+    const int2* mpairs;       // [nmp] merge links (cell a, cell b), x-major (Point::m_merge; nullptr: none)
+    int nmp;
     int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
     int32_t* nlev_out;        // [N] levels (0: source skipped)
     int* error;
@@ -272,7 +274,9 @@ __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
 struct TileShared {
     int src, qn, hn, item, bn;
     int grp, grp_tries;   // XCD-grouped work: the group being drained, groups found empty
+    int mpart;            // merge partner cell of the source (-1: none)
     unsigned long long cnt, mass;
+    unsigned long long mcorr, mdisc;   // merge pass: pairs discovered together, partners of U_f joined
 };
 
 // Next work item.  xcd_ctr == nullptr: one counter for the whole grid.  Otherwise the items are split
@@ -416,6 +420,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
     if (tid == 0) {
         S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.cnt = 0; S.mass = 0; S.src = -1;
         S.grp = blockIdx.x & 7; S.grp_tries = 0;
+        S.mpart = -1; S.mcorr = 0; S.mdisc = 0;
     }
     int64_t chunk_end = 0;
     int64_t src = -1;
@@ -466,8 +471,31 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             __syncthreads();
             if (tid == 0) S.cnt = 0;
         }
+        // the source's merge partner is extracted at level 0 and never counted (vgavisualglobal.cpp:113-122);
+        // in seed mode the host lists the seeds' partners as seeds (they take level 0)
+        int64_t spart = -1;
+        if (P.nmp && !seeded) {
+            __syncthreads();
+            for (int i = tid; i < P.nmp; i += NT) {
+                const int2 pr = P.mpairs[i];
+                if (pr.x == scell) S.mpart = pr.y;
+                else if (pr.y == scell) S.mpart = pr.x;
+            }
+            __syncthreads();
+            const int pc = S.mpart;
+            if (pc >= 0) {
+                spart = P.cell_node[pc];
+                const int px = pc / rows, py = pc % rows;
+                const int pt = (py >> 3) * tw + (px >> 3);
+                const unsigned long long pb = 1ull << ((py & 7) * 8 + (px & 7));
+                if (tid == 0) or_wg(&Vg[pt], pb);
+                if (!(P.seed_tiles[pt] & pb)) n_in_uf++;
+            }
+            __syncthreads();
+            if (tid == 0) S.mpart = -1;
+        }
         const long long target = P.uf_count - n_in_uf;
-        long long m_f = seeded ? P.nseeds : 1, m_u = target, discovered = 0;
+        long long m_f = seeded ? P.nseeds : (spart >= 0 ? 2 : 1), m_u = target, discovered = 0;
         int level = 0, nlev = 1;
         bool overflow = false;
         __syncthreads();
@@ -479,8 +507,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             tmark = __builtin_amdgcn_s_memtime();
             if (level == 0) {
                 // ---- level 1: rasterise the source's runs (top-down from {s}, or from every seed)
-                for (int i = 0; i < (seeded ? P.nseeds : 1); i++) {
-                    const int64_t sn = seeded ? P.seeds[i] : node;
+                for (int i = 0; i < (seeded ? P.nseeds : (spart >= 0 ? 2 : 1)); i++) {
+                    const int64_t sn = seeded ? P.seeds[i] : (i == 0 ? node : spart);
                     const int64_t rs = P.node_run_start[sn];
                     const int nr = P.node_nruns[sn];
                     for (int r = tid; r < nr; r += NT) run_or(F, tw, P.pool[rs + r]);
@@ -830,6 +858,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 m_loc += __shfl_xor(m_loc, off);
             }
             if (lane == 0 && c_loc) { atomicAdd(&S.cnt, c_loc); atomicAdd(&S.mass, m_loc); }
+            if (P.nmp && (P.radius == -1 || level + 1 < P.radius)) {
+                __syncthreads();   // the new level is in F and V
+                merge_level_pass(P.mpairs, P.nmp, rows, tw, NT, F, Vg, false, P.seed_tiles, Fsr, RBM ? nullptr : Fsc, wr,
+                                 wc, P.cell_level, level + 1, &S.mcorr, &S.mdisc, &S.mass);
+            }
             if (RBM) {
                 // line-resolved summaries from the published frontier (plain stores, no atomics)
                 __syncthreads();
@@ -853,14 +886,15 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             }
             sync_global();
             const long long cnt = (long long)S.cnt, mass = (long long)S.mass;
+            const long long mcorr = (long long)S.mcorr, mdisc = (long long)S.mdisc;
             if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(12, n - tmark); tmark = n; }
             __syncthreads();
-            if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; }
+            if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.mcorr = 0; S.mdisc = 0; }
             if (cnt == 0) break;
             if (level + 1 >= VGA_HMAX) { overflow = true; break; }
-            if (tid == 0) hist[level + 1] = (int)cnt;
-            discovered += cnt;
-            m_u -= cnt;
+            if (tid == 0) hist[level + 1] = (int)(cnt - mcorr);
+            discovered += cnt + mdisc;
+            m_u -= cnt + mdisc;
             m_f = mass;
             level++;
             nlev = level + 1;

@@ -49,4 +49,21 @@ __global__ void __launch_bounds__(VSD_THREADS) vsd_level_kernel(int rows, int tw
     }
 }
 
+// Merge links after level L of the search (vgavisualglobaldepth.cpp:55-63): a link with one end new at
+// level L and the other not yet seen extracts the other now -- it takes level L and its node joins the
+// next frontier.  (Links between two cells new at L need nothing: both already hold L and expand.)
+__global__ void vsd_merge_kernel(int rows, int tw, const int2* mpairs, int nmp, const int32_t* cell_node, int lev,
+                                 unsigned long long* vis, int32_t* level, int32_t* next, unsigned long long* next_n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nmp) return;
+    const int2 pr = mpairs[i];
+    const int la = level[pr.x], lb = level[pr.y];
+    const int o = (la == lev && lb < 0) ? pr.y : ((lb == lev && la < 0) ? pr.x : -1);
+    if (o < 0) return;
+    const int x = o / rows, y = o % rows;
+    atomicOr(&vis[(y >> 3) * tw + (x >> 3)], 1ull << ((y & 7) * 8 + (x & 7)));
+    level[o] = lev;
+    next[atomicAdd(next_n, 1ull)] = cell_node[o];
+}
+
 } // namespace dmx

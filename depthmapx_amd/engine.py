@@ -181,6 +181,12 @@ class PointMap:
         N.check(N.lib().dmx_pointmap_cell_lines(self.h, N.ptr(counts), N.ptr(pieces), ctypes.byref(total)))
         return counts, pieces[:total.value]
 
+    def set_merges(self, cell_pairs):
+        """Merge links (Point::m_merge; PointMap::mergePixels, salalib/pointdata.cpp:1653-1680): pairs of
+        x-major cells.  Written into the map's .graph chunk and followed by the graphs made from it."""
+        arr = np.ascontiguousarray(cell_pairs, dtype=np.int32).reshape(-1, 2)
+        N.check(N.lib().dmx_pointmap_set_merges(self.h, N.ptr(arr), len(arr)))
+
     def make_graph(self, ctx, boundarygraph=False, maxdist=-1.0, node_begin=0, node_end=-1):
         h = ctypes.c_void_p()
         N.check(N.lib().dmx_makegraph(ctx.h, self.h, float(maxdist), int(bool(boundarygraph)), int(node_begin),
@@ -245,6 +251,12 @@ class Graph:
                                                  len(rr), None, None))
             out["runs"] = rr[:nr.value]
         return out
+
+    def set_merges(self, cell_pairs):
+        """Merge links followed by VGA global, visual / metric / angular step depth and VGA metric /
+        angular (the getMergePixel blocks of salalib/vgamodules); pairs of x-major cells."""
+        arr = np.ascontiguousarray(cell_pairs, dtype=np.int32).reshape(-1, 2)
+        N.check(N.lib().dmx_graph_set_merges(self.h, N.ptr(arr), len(arr)))
 
     def blob_size(self):
         b = ctypes.c_int64()

@@ -259,13 +259,24 @@ int dmx_chunk_load(dmx_ctx* ctx, const dmx_chunk* c, const double* region, dmx_p
 /* Device graph from host node records (e.g. a graph the reference itself built or loaded). */
 int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const int32_t* bins, const int16_t* runs,
                         int64_t nruns, const uint8_t* gridconn, const float* attrs, dmx_graph** out);
-/* Merge links of the map (Point::m_merge, set by the LINK mode): n pairs (cell, partner cell), x-major
- * indices.  dmx_chunk_load sets them from the chunk.  The searches that follow merge links in the
- * reference (VGA global, metric, angular, and the three step depths: getMergePixel in
- * vgavisualglobal.cpp:113-122, vgametric.cpp:97-104, vgaangular.cpp:95-102, vgametricdepth.cpp:68-82,
- * vgaangulardepth.cpp:57-66, vgavisualglobaldepth.cpp:55-64) return DMX_ERR_UNSUPPORTED on a graph with
- * merge links; VGA visual local has no merge logic and runs. */
+/* Merge links (Point::m_merge, set by the LINK mode / PointMap::mergePixels, salalib/pointdata.cpp:1653-1680):
+ * n pairs (cell, partner cell) of x-major indices; a pair may be listed in both directions (as
+ * PointMap::write stores it on both points); a cell belongs to at most one link (DMX_ERR_ARG otherwise).
+ * dmx_chunk_load sets them from the chunk.  Every search that follows merge links in the reference
+ * follows them here, with the reference's bookkeeping of the partner: VGA global (vgavisualglobal.cpp:
+ * 113-122), visual step depth (vgavisualglobaldepth.cpp:55-63), metric / angular all sources
+ * (vgametric.cpp:97-105, vgaangular.cpp:95-104) and metric / angular step depth (vgametricdepth.cpp:68-83,
+ * vgaangulardepth.cpp:57-67).  Both ends must be filled cells of the graph (DMX_ERR_ARG at the analysis).
+ * Links on CONTEXTFILLED cells make VGA global with a radius and visual step depth depend on the
+ * reference's pop order inside a level; those two analyses return DMX_ERR_UNSUPPORTED on such maps.
+ * VGA visual local has no merge logic. */
 int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n);
+/* The same links on a point map: written into its PointMap chunk (Point::write, point.cpp:51-73) and
+ * followed by the graphs made from it (dmx_makegraph, dmx_graph_assemble_device, dmx_graph_from_runs). */
+int dmx_pointmap_set_merges(dmx_pointmap* pm, const int32_t* cell_pairs, int64_t n);
+/* The merge links stored in a chunk, one entry per link (cell < partner cell): *n in = capacity of
+ * cell_pairs ([n][2]), out = number of links; cell_pairs NULL: only *n. */
+int dmx_chunk_merges(const dmx_chunk* c, int32_t* cell_pairs, int64_t* n);
 /* Editing a parsed chunk the way the reference edits a PointMap it read (PointMap::read then ::write,
  * pointdata.cpp:1073-1188): columns that are not set keep their bytes (stats, display parameters,
  * formula), point records are re-emitted with the state bits PointMap::read keeps.

@@ -130,7 +130,9 @@ bool loadMap(PointMap& map, const void* bytes) { return load(map, *static_cast<c
 
 bool sparkGraph2(PointMap& map, Communicator* comm, bool boundarygraph, double maxdist) {
     dmx_ctx* ctx = context();
-    if (!ctx || !map.getMergedPixelPairs().empty()) return false;   // merge links: the reference keeps them
+    // a processed map keeps the reference path (its sparkGraph2 re-adds attribute rows that exist and
+    // throws, attributetable.cpp:278)
+    if (!ctx || map.isProcessed()) return false;
     const QtRegion* parent = RegionAccess::parent(map);
     const double region[4] = {parent->bottom_left.x, parent->bottom_left.y, parent->top_right.x, parent->top_right.y};
     const std::vector<double> lines = drawing_lines(map);
@@ -148,6 +150,13 @@ bool sparkGraph2(PointMap& map, Communicator* comm, bool boundarygraph, double m
         for (int32_t y = 0; y < rows; y++)
             state[(size_t)x * rows + y] = map.getPoint(PixelRef((short)x, (short)y)).getState();
     check(dmx_pointmap_set_state(pm.p, state.data()));
+    // merge links stay on the points and are written back with them (Point::write, point.cpp:51-73)
+    std::vector<int32_t> links;
+    for (const auto& pr : map.getMergedPixelPairs()) {
+        links.push_back((int32_t)pr.first.x * rows + pr.first.y);
+        links.push_back((int32_t)pr.second.x * rows + pr.second.y);
+    }
+    if (!links.empty()) check(dmx_pointmap_set_merges(pm.p, links.data(), (int64_t)links.size() / 2));
     // makeGraph on the GPU
     Owned<dmx_graph, dmx_graph_free> g;
     {
@@ -197,7 +206,8 @@ bool vgaVisualGlobal(PointMap& map, Communicator* comm, double radius, bool gate
     {
         ScopedProgress sp(ctx, comm);
         const int rc = dmx_vga_global(ctx, g.p, radius, gates_only ? 1 : 0, 0, -1, out.data(), nullptr);
-        if (rc == DMX_ERR_UNSUPPORTED) return false;   // merge links (getMergePixel): the reference path
+        // merge links on context-filled cells with a radius (pop-order dependent): the reference path
+        if (rc == DMX_ERR_UNSUPPORTED) return false;
         check(rc);
     }
     // VGAVisualGlobal::run's columns (vgavisualglobal.cpp:31-63), alphabetical, " R<r>" suffix for a

@@ -158,6 +158,7 @@ struct dmxo_map {
     float* attrs;        /* [N][3] */
     uint8_t* gridconn;
     int runs_borrowed;   /* nodes[].runs point into a caller's array (dmxo_set_graph_view) */
+    int32_t* merge;      /* Point::m_merge per cell: partner cell (x-major) or -1 (point.h:56) */
 };
 
 static inline int64_t cidx(const dmxo_map* m, int x, int y) { return (int64_t)x * m->rows + y; }
@@ -204,7 +205,56 @@ dmxo_map* dmxo_create(const double region[4], double spacing, const double* line
     memcpy(d, lines, nlines * 4 * sizeof(double));
     m->draw = d;
     m->ndraw = nlines;
+    m->merge = (int32_t*)malloc(C * sizeof(int32_t));
+    for (int64_t i = 0; i < C; i++) m->merge[i] = -1;
     return m;
+}
+
+static void release_nodes(dmxo_map* m);
+static void index_nodes(dmxo_map* m);
+
+/* A map read back from a .graph PointMap chunk (PointMap::read, pointdata.cpp:1073-1156): the grid as
+ * stored (cols, rows, spacing, bottom-left cell centre) and no drawing -- enough to analyse a graph
+ * handed over with dmxo_set_state + dmxo_set_graph. */
+dmxo_map* dmxo_create_grid(int cols, int rows, double spacing, double blx, double bly) {
+    const double region[4] = {blx - spacing / 2.0, bly - spacing / 2.0, blx + spacing * (cols - 0.5),
+                              bly + spacing * (rows - 0.5)};
+    dmxo_map* m = dmxo_create(region, spacing, NULL, 0);
+    if (!m) return NULL;
+    free(m->state);
+    free(m->merge);
+    m->cols = cols;
+    m->rows = rows;
+    m->bl.x = blx;
+    m->bl.y = bly;
+    m->region.blx = region[0]; m->region.bly = region[1]; m->region.trx = region[2]; m->region.try_ = region[3];
+    const int64_t C = (int64_t)cols * rows;
+    m->state = (int32_t*)malloc(C * sizeof(int32_t));
+    m->merge = (int32_t*)malloc(C * sizeof(int32_t));
+    for (int64_t i = 0; i < C; i++) { m->state[i] = ST_EMPTY; m->merge[i] = -1; }
+    return m;
+}
+
+/* Cell states as stored (x-major); re-indexes the nodes (filled cells, x-major). */
+void dmxo_set_state(dmxo_map* m, const int32_t* state) {
+    const int64_t C = (int64_t)m->cols * m->rows;
+    memcpy(m->state, state, C * sizeof(int32_t));
+    release_nodes(m);
+    index_nodes(m);
+}
+
+/* PointMap::mergePixels (pointdata.cpp:1653-1680) for each pair: both cells point at each other.
+ * Pairs must join two distinct filled cells; a cell in two pairs keeps the last one. */
+int dmxo_set_merges(dmxo_map* m, const int32_t* pairs, int64_t n) {
+    const int64_t C = (int64_t)m->cols * m->rows;
+    for (int64_t i = 0; i < C; i++) m->merge[i] = -1;
+    for (int64_t i = 0; i < n; i++) {
+        const int32_t a = pairs[2 * i], b = pairs[2 * i + 1];
+        if (a < 0 || b < 0 || a >= C || b >= C || a == b) return -1;
+        m->merge[a] = b;
+        m->merge[b] = a;
+    }
+    return 0;
 }
 
 static void release_nodes(dmxo_map* m) {
@@ -220,7 +270,7 @@ static void release_nodes(dmxo_map* m) {
 void dmxo_free(dmxo_map* m) {
     if (!m) return;
     free(m->state); free((void*)m->draw); free(m->cl_off); free(m->cl);
-    free(m->node_of_cell); free(m->node_cell); free(m->attrs); free(m->gridconn);
+    free(m->node_of_cell); free(m->node_cell); free(m->attrs); free(m->gridconn); free(m->merge);
     release_nodes(m);
     free(m);
 }
@@ -1008,6 +1058,17 @@ int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t nb, int6
                         if (rad == -1 || (level < rad && (!(pst & ST_CONTEXTFILLED) || (cur.x % 2 == 0 && cur.y % 2 == 0)))) {
                             extract_unseen(m, &m->nodes[m->node_of_cell[cc]], &levels[level + 1], miscs, extx, exty);
                             miscs[idx] = ~0;
+                            /* the merge pixel's node is extracted at the same level, uncounted
+                               (vgavisualglobal.cpp:113-122) */
+                            const int32_t mc = m->merge[cc];
+                            if (mc >= 0) {
+                                const int64_t midx = (int64_t)(mc / m->rows) + (int64_t)(mc % m->rows) * m->cols;
+                                if (miscs[midx] != ~0) {
+                                    if (m->node_of_cell[mc] >= 0)
+                                        extract_unseen(m, &m->nodes[m->node_of_cell[mc]], &levels[level + 1], miscs, extx, exty);
+                                    miscs[midx] = ~0;
+                                }
+                            }
                         } else {
                             miscs[idx] = ~0;
                         }
@@ -1112,7 +1173,63 @@ static int blocked_adjacent(const dmxo_map* m, int x, int y) {
  * FILLED, not yet visited cells expand through Node::extractMetric when they are the search roots,
  * BLOCKED or blocked-adjacent; `visit` sees every resolved cell in pop order.  radius >= 0 stops the
  * search at the first popped triple with dist * spacing > radius (vgametric.cpp:86-88). */
-typedef void (*metric_visit_fn)(void* ctx, const dmxo_map* m, int64_t cell, float dist, float cum);
+typedef void (*metric_visit_fn)(void* ctx, const dmxo_map* m, int64_t cell, float dist, float cum, int merged);
+/* Node::extractMetric / Bin::extractMetric (ngraph.cpp:67-76, :330-345) of the node at cell hc for
+ * the triple (dist, hc, last): relaxes only when dist == 0 or hc is BLOCKED / blocked-adjacent. */
+static void metric_relax(dmxo_map* m, int64_t hc, float dist, int32_t last, float* mdist, float* cum, int32_t* misc,
+                         Vec* ins, MHeap* h) {
+    const int hx = (int)(hc / m->rows), hy = (int)(hc % m->rows);
+    if (!(dist == 0.0f || (m->state[hc] & ST_BLOCKED) || blocked_adjacent(m, hx, hy))) return;
+    if (m->node_of_cell[hc] < 0) return;
+    const NodeG* nd = &m->nodes[m->node_of_cell[hc]];
+    const Run* r = nd->runs;
+    const int lx = last >> 16, ly = last & 0xffff;
+    const int32_t hpix = pix_int(hx, hy);
+    for (int b = 0; b < 32; b++) {
+        char dir = nd->dir[b];
+        for (int k = 0; k < nd->nruns[b]; k++, r++) {
+            int px = r->x0, py = r->y0;
+            int endc = (dir & D_V) ? r->y1 : r->x1;
+            for (;;) {
+                int col = (dir & D_V) ? py : px;
+                if (col > endc) break;
+                int64_t pc = cidx(m, px, py);
+                /* non-filled cells (diagonal gaps) can be queued but never resolve */
+                if ((m->state[pc] & ST_FILLED) && misc[pc] == 0) {
+                    double dd = pix_dist(px, py, hx, hy);
+                    if (mdist[pc] == -1.0 || (double)dist + dd < (double)mdist[pc]) {
+                        mdist[pc] = dist + (float)dd;
+                        cum[pc] = cum[hc] + (last == -1 ? 0.0f : (float)(pix_angle(px, py, hx, hy, lx, ly) / (M_PI_ * 0.5)));
+                        int dup = 0;
+                        for (int64_t q = 0; q < ins[pc].n; q++)
+                            if (((float*)ins[pc].p)[q] == mdist[pc]) { dup = 1; break; }
+                        if (!dup) {
+                            float* d = (float*)vec_push(&ins[pc], sizeof(float));
+                            *d = mdist[pc];
+                            MTrip t = {mdist[pc], pix_int(px, py), hpix};
+                            mh_push(h, t);
+                        }
+                    }
+                }
+                switch (dir) {
+                case D_PD: px++; py++; break;
+                case D_ND: px++; py--; break;
+                case D_H: px++; break;
+                case D_V: py++; break;
+                }
+            }
+        }
+    }
+}
+
+/* The std::set<MetricTriple> search shared by VGAMetricDepth::run (vgametricdepth.cpp:45-84) and
+ * VGAMetric::run (vgametric.cpp:82-112): every selected cell enters at dist 0; a popped triple of a
+ * FILLED, not yet visited cell relaxes through Node::extractMetric, is marked visited and visited
+ * (`visit`, merged = 0, in pop order); then a merge pixel not yet visited takes the popped cell's
+ * cumulative angle, is visited (merged = 1: VGAMetricDepth writes its row, VGAMetric does not count
+ * it), relaxes from (here.dist, merge pixel, NoPixel) and is marked visited (vgametricdepth.cpp:68-83,
+ * vgametric.cpp:97-105).  radius >= 0 stops the search at the first popped triple with
+ * dist * spacing > radius (vgametric.cpp:86-88). */
 static void metric_search(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, double radius, metric_visit_fn visit,
                           void* vctx, float* mdist, float* cum, int32_t* misc, Vec* ins) {
     const int64_t C = (int64_t)m->cols * m->rows;
@@ -1132,56 +1249,23 @@ static void metric_search(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, d
         int hx = here.pix >> 16, hy = here.pix & 0xffff;
         int64_t hc = cidx(m, hx, hy);
         if (!(m->state[hc] & ST_FILLED) || misc[hc] == ~0) continue;
-        if (here.dist == 0.0f || (m->state[hc] & ST_BLOCKED) || blocked_adjacent(m, hx, hy)) {
-            /* Node::extractMetric / Bin::extractMetric (ngraph.cpp:67-76, :330-345) */
-            const NodeG* nd = &m->nodes[m->node_of_cell[hc]];
-            const Run* r = nd->runs;
-            int lx = here.last >> 16, ly = here.last & 0xffff;
-            for (int b = 0; b < 32; b++) {
-                char dir = nd->dir[b];
-                for (int k = 0; k < nd->nruns[b]; k++, r++) {
-                    int px = r->x0, py = r->y0;
-                    int endc = (dir & D_V) ? r->y1 : r->x1;
-                    for (;;) {
-                        int col = (dir & D_V) ? py : px;
-                        if (col > endc) break;
-                        int64_t pc = cidx(m, px, py);
-                        /* non-filled cells (diagonal gaps) can be queued but never resolve */
-                        if ((m->state[pc] & ST_FILLED) && misc[pc] == 0) {
-                            double dd = pix_dist(px, py, hx, hy);
-                            if (mdist[pc] == -1.0 || (double)here.dist + dd < (double)mdist[pc]) {
-                                mdist[pc] = here.dist + (float)dd;
-                                cum[pc] = cum[hc] + (here.last == -1 ? 0.0f
-                                                                     : (float)(pix_angle(px, py, hx, hy, lx, ly) / (M_PI_ * 0.5)));
-                                int dup = 0;
-                                for (int64_t q = 0; q < ins[pc].n; q++)
-                                    if (((float*)ins[pc].p)[q] == mdist[pc]) { dup = 1; break; }
-                                if (!dup) {
-                                    float* d = (float*)vec_push(&ins[pc], sizeof(float));
-                                    *d = mdist[pc];
-                                    MTrip t = {mdist[pc], pix_int(px, py), here.pix};
-                                    mh_push(&h, t);
-                                }
-                            }
-                        }
-                        switch (dir) {
-                        case D_PD: px++; py++; break;
-                        case D_ND: px++; py--; break;
-                        case D_H: px++; break;
-                        case D_V: py++; break;
-                        }
-                    }
-                }
-            }
-        }
+        metric_relax(m, hc, here.dist, here.last, mdist, cum, misc, ins, &h);
         misc[hc] = ~0;
-        visit(vctx, m, hc, here.dist, cum[hc]);
+        visit(vctx, m, hc, here.dist, cum[hc], 0);
+        const int32_t mc = m->merge[hc];
+        if (mc >= 0 && misc[mc] != ~0) {
+            cum[mc] = cum[hc];
+            visit(vctx, m, mc, here.dist, cum[mc], 1);
+            metric_relax(m, mc, here.dist, -1, mdist, cum, misc, ins, &h);
+            misc[mc] = ~0;
+        }
     }
     free(h.a);
 }
 
 typedef struct { float* out; int64_t nsel; int sx0, sy0; } StepVisit;
-static void stepdepth_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
+static void stepdepth_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv, int merged) {
+    (void)merged;   /* the merge pixel's row is written like the popped cell's (vgametricdepth.cpp:71-80) */
     StepVisit* v = (StepVisit*)vctx;
     float* o = v->out + 3 * m->node_of_cell[hc];
     o[0] = cumv;
@@ -1211,7 +1295,8 @@ int dmxo_metric_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
  * Metric Mean Shortest-Path Angle, Mean Shortest-Path Distance, Mean Straight-Line Distance,
  * Node Count (-1 for every source when gates_only). */
 typedef struct { float ftd, fta, fte; int64_t tn; int sx, sy; } MetricVisit;
-static void metric_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
+static void metric_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv, int merged) {
+    if (merged) return;   /* merge pixels are not counted (vgametric.cpp:97-110) */
     MetricVisit* v = (MetricVisit*)vctx;
     v->ftd += (float)(dist * m->spacing);
     v->fta += cumv;
@@ -1255,6 +1340,52 @@ int dmxo_vga_metric(dmxo_map* m, double radius, int gates_only, int64_t nb, int6
     return 0;
 }
 
+/* Node::extractAngular / Bin::extractAngular (ngraph.cpp:78-85, :348-366) of the node at cell hc for
+ * the triple (angle, hc, last): relaxes when angle == 0 or hc is BLOCKED / blocked-adjacent. */
+static void angular_relax(dmxo_map* m, int64_t hc, float angle, int32_t last, float* cum, int32_t* misc, Vec* ins,
+                          MHeap* h) {
+    const int hx = (int)(hc / m->rows), hy = (int)(hc % m->rows);
+    if (!(angle == 0.0f || (m->state[hc] & ST_BLOCKED) || blocked_adjacent(m, hx, hy))) return;
+    if (m->node_of_cell[hc] < 0) return;
+    const NodeG* nd = &m->nodes[m->node_of_cell[hc]];
+    const Run* r = nd->runs;
+    const int lx = last >> 16, ly = last & 0xffff;
+    const int32_t hpix = pix_int(hx, hy);
+    for (int b = 0; b < 32; b++) {
+        char dir = nd->dir[b];
+        for (int k = 0; k < nd->nruns[b]; k++, r++) {
+            int px = r->x0, py = r->y0;
+            int endc = (dir & D_V) ? r->y1 : r->x1;
+            for (;;) {
+                int col = (dir & D_V) ? py : px;
+                if (col > endc) break;
+                int64_t pc = cidx(m, px, py);
+                if (misc[pc] == 0) {
+                    float ang = last == -1 ? 0.0f : (float)(pix_angle(px, py, hx, hy, lx, ly) / (M_PI_ * 0.5));
+                    if (cum[pc] == -1.0 || angle + ang < cum[pc]) {
+                        cum[pc] = cum[hc] + ang;
+                        int dup = 0;
+                        for (int64_t q = 0; q < ins[pc].n; q++)
+                            if (((float*)ins[pc].p)[q] == cum[pc]) { dup = 1; break; }
+                        if (!dup) {
+                            float* d = (float*)vec_push(&ins[pc], sizeof(float));
+                            *d = cum[pc];
+                            MTrip t = {cum[pc], pix_int(px, py), hpix};
+                            mh_push(h, t);
+                        }
+                    }
+                }
+                switch (dir) {
+                case D_PD: px++; py++; break;
+                case D_ND: px++; py--; break;
+                case D_H: px++; break;
+                case D_V: py++; break;
+                }
+            }
+        }
+    }
+}
+
 /* The std::set<AngularTriple> search shared by VGAAngularDepth::run (vgaangulardepth.cpp:23-75) and
  * VGAAngular::run (vgaangular.cpp:26-133): selected cells enter with cumangle 0; a popped FILLED,
  * unvisited cell expands through Node::extractAngular (ngraph.cpp:78-85) when its angle is 0 or it is
@@ -1262,7 +1393,10 @@ int dmxo_vga_metric(dmxo_map* m, double radius, int gates_only, int64_t nb, int6
  * of its runs (no FILLED test) with ang = angle(pix, here, last)/(pi/2) when cumangle == -1 or
  * here.angle + ang < cumangle.  cum[] starts at -1 for every cell (VGAAngular resets all points;
  * VGAAngularDepth only the filled ones, but unfilled cells are never counted nor expanded).
- * radius >= 0 stops at the first popped triple with angle > radius (vgaangular.cpp:86-88). */
+ * A merge pixel not yet visited takes the popped cell's cumangle, is visited (merged = 1), relaxes
+ * from (here.angle, merge pixel, NoPixel) and is marked visited (vgaangular.cpp:95-104,
+ * vgaangulardepth.cpp:57-67).  radius >= 0 stops at the first popped triple with angle > radius
+ * (vgaangular.cpp:86-88). */
 static void angular_search(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, double radius, metric_visit_fn visit,
                            void* vctx, float* cum, int32_t* misc, Vec* ins) {
     const int64_t C = (int64_t)m->cols * m->rows;
@@ -1288,52 +1422,22 @@ static void angular_search(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, 
         int hx = here.pix >> 16, hy = here.pix & 0xffff;
         int64_t hc = cidx(m, hx, hy);
         if (!(m->state[hc] & ST_FILLED) || misc[hc] == ~0) continue;
-        if (here.dist == 0.0f || (m->state[hc] & ST_BLOCKED) || blocked_adjacent(m, hx, hy)) {
-            const NodeG* nd = &m->nodes[m->node_of_cell[hc]];
-            const Run* r = nd->runs;
-            int lx = here.last >> 16, ly = here.last & 0xffff;
-            for (int b = 0; b < 32; b++) {
-                char dir = nd->dir[b];
-                for (int k = 0; k < nd->nruns[b]; k++, r++) {
-                    int px = r->x0, py = r->y0;
-                    int endc = (dir & D_V) ? r->y1 : r->x1;
-                    for (;;) {
-                        int col = (dir & D_V) ? py : px;
-                        if (col > endc) break;
-                        int64_t pc = cidx(m, px, py);
-                        if (misc[pc] == 0) {
-                            float ang = here.last == -1 ? 0.0f : (float)(pix_angle(px, py, hx, hy, lx, ly) / (M_PI_ * 0.5));
-                            if (cum[pc] == -1.0 || here.dist + ang < cum[pc]) {
-                                cum[pc] = cum[hc] + ang;
-                                int dup = 0;
-                                for (int64_t q = 0; q < ins[pc].n; q++)
-                                    if (((float*)ins[pc].p)[q] == cum[pc]) { dup = 1; break; }
-                                if (!dup) {
-                                    float* d = (float*)vec_push(&ins[pc], sizeof(float));
-                                    *d = cum[pc];
-                                    MTrip t = {cum[pc], pix_int(px, py), here.pix};
-                                    mh_push(&h, t);
-                                }
-                            }
-                        }
-                        switch (dir) {
-                        case D_PD: px++; py++; break;
-                        case D_ND: px++; py--; break;
-                        case D_H: px++; break;
-                        case D_V: py++; break;
-                        }
-                    }
-                }
-            }
-        }
+        angular_relax(m, hc, here.dist, here.last, cum, misc, ins, &h);
         misc[hc] = ~0;
-        visit(vctx, m, hc, here.dist, cum[hc]);
+        visit(vctx, m, hc, here.dist, cum[hc], 0);
+        const int32_t mc = m->merge[hc];
+        if (mc >= 0 && misc[mc] != ~0) {
+            cum[mc] = cum[hc];
+            visit(vctx, m, mc, here.dist, cum[mc], 1);
+            angular_relax(m, mc, here.dist, -1, cum, misc, ins, &h);
+            misc[mc] = ~0;
+        }
     }
     free(h.a);
 }
 
-static void angular_step_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
-    (void)dist;
+static void angular_step_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv, int merged) {
+    (void)dist; (void)merged;   /* the merge pixel's row is written too (vgaangulardepth.cpp:60-62) */
     ((float*)vctx)[m->node_of_cell[hc]] = cumv;
 }
 
@@ -1351,8 +1455,9 @@ int dmxo_angular_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, 
 }
 
 typedef struct { float total; int64_t n; } AngularVisit;
-static void angular_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv) {
+static void angular_visit(void* vctx, const dmxo_map* m, int64_t hc, float dist, float cumv, int merged) {
     (void)m; (void)hc; (void)dist;
+    if (merged) return;   /* merge pixels are not counted (vgaangular.cpp:95-106) */
     AngularVisit* v = (AngularVisit*)vctx;
     v->total += cumv;
     v->n += 1;
@@ -1425,8 +1530,22 @@ int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
             const int64_t cc = cidx(m, pc.x, pc.y), idx = (int64_t)pc.x + (int64_t)pc.y * m->cols;
             if ((m->state[cc] & ST_FILLED) && miscs[idx] != ~0) {
                 out[m->node_of_cell[cc]] = (float)level;
-                if (!(m->state[cc] & ST_CONTEXTFILLED) || (pc.x % 2 == 0 && pc.y % 2 == 0) || level == 0)
+                if (!(m->state[cc] & ST_CONTEXTFILLED) || (pc.x % 2 == 0 && pc.y % 2 == 0) || level == 0) {
                     extract_unseen(m, &m->nodes[m->node_of_cell[cc]], &next, miscs, extx, exty);
+                    miscs[idx] = ~0;
+                    /* the merge pixel takes this level and is extracted now (vgavisualglobaldepth.cpp:55-63) */
+                    const int32_t mc = m->merge[cc];
+                    if (mc >= 0) {
+                        const int64_t midx = (int64_t)(mc / m->rows) + (int64_t)(mc % m->rows) * m->cols;
+                        if (miscs[midx] != ~0) {
+                            if (m->node_of_cell[mc] >= 0) {
+                                out[m->node_of_cell[mc]] = (float)level;
+                                extract_unseen(m, &m->nodes[m->node_of_cell[mc]], &next, miscs, extx, exty);
+                            }
+                            miscs[midx] = ~0;
+                        }
+                    }
+                }
                 miscs[idx] = ~0;
             }
         }

@@ -22,6 +22,10 @@ typedef struct dmxo_map dmxo_map;
  * blockLines() sees them (pointdata.cpp:308-320). lines: [L][4] = x1,y1,x2,y2. */
 dmxo_map* dmxo_create(const double region[4], double spacing, const double* lines, int64_t nlines);
 void dmxo_free(dmxo_map* m);
+/* A grid as a .graph PointMap chunk stores it (PointMap::read, pointdata.cpp:1073-1156), no drawing;
+ * dmxo_set_state then gives the cell states and dmxo_set_graph the nodes. */
+dmxo_map* dmxo_create_grid(int cols, int rows, double spacing, double bl_x, double bl_y);
+void dmxo_set_state(dmxo_map* m, const int32_t* state);
 void dmxo_grid_info(const dmxo_map* m, int32_t* cols, int32_t* rows, double* bl_x, double* bl_y);
 
 /* PointMap::makePoints(seed, FULLFILL) (pointdata.cpp:402-481). Returns 1 on success, 0 if the
@@ -43,6 +47,10 @@ int64_t dmxo_num_runs(const dmxo_map* m);
 /* attrs [N][3] (Connectivity, First, Second Moment); bins [N][32][4] (dir, count, dist bits, nruns);
  * runs [R][4] int16 (x0,y0,x1,y1) in reference order; gridconn [N]. */
 void dmxo_get_graph(const dmxo_map* m, float* attrs, int32_t* bins, int16_t* runs, uint8_t* gridconn);
+/* Merge links (Point::m_merge, PointMap::mergePixels pointdata.cpp:1653-1680): n pairs of distinct
+ * x-major cells.  VGA global, visual / metric / angular step depth and VGA metric / angular then
+ * follow them as the reference does (getMergePixel blocks of the vgamodules).  Returns -1 on a bad pair. */
+int dmxo_set_merges(dmxo_map* m, const int32_t* cell_pairs, int64_t n);
 /* Replace the graph with externally supplied bins/runs (e.g. a reference dump), same layout. */
 int dmxo_set_graph(dmxo_map* m, const int32_t* bins, const int16_t* runs, int64_t nruns);
 /* same, borrowing `runs` (kept alive by the caller) instead of copying it */

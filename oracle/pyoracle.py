@@ -64,6 +64,14 @@ def lib():
         L.dmxo_makegraph_sample.argtypes = [vp, dbl, vp, i64, i32, vp]
         L.dmxo_vga_global_sample.restype = i32
         L.dmxo_vga_global_sample.argtypes = [vp, dbl, vp, i64, i32, vp, vp]
+        L.dmxo_create_grid.restype = vp
+        L.dmxo_create_grid.argtypes = [i32, i32, dbl, dbl, dbl]
+        L.dmxo_set_state.restype = None
+        L.dmxo_set_state.argtypes = [vp, vp]
+        L.dmxo_set_merges.restype = i32
+        L.dmxo_set_merges.argtypes = [vp, vp, i64]
+        L.dmxo_set_graph.restype = i32
+        L.dmxo_set_graph.argtypes = [vp, vp, vp, i64]
         _lib = L
     return _lib
 
@@ -85,6 +93,25 @@ class OracleMap:
         L.dmxo_grid_info(self.h, ctypes.byref(c), ctypes.byref(r), ctypes.byref(bx), ctypes.byref(by))
         self.cols, self.rows = c.value, r.value
         self.bottom_left = (bx.value, by.value)
+
+    @classmethod
+    def from_grid(cls, cols, rows, spacing, bottom_left, state):
+        """A map as a .graph PointMap chunk stores it (grid + cell states, no drawing): for analysing a
+        graph handed over with set_graph."""
+        L = lib()
+        self = cls.__new__(cls)
+        self.h = L.dmxo_create_grid(int(cols), int(rows), float(spacing), float(bottom_left[0]), float(bottom_left[1]))
+        self.cols, self.rows = int(cols), int(rows)
+        self.bottom_left = tuple(bottom_left)
+        st = np.ascontiguousarray(state, dtype=np.int32)
+        L.dmxo_set_state(self.h, _p(st))
+        return self
+
+    def set_merges(self, cell_pairs):
+        """Merge links (Point::m_merge): pairs of x-major cells, followed by the VGA searches."""
+        arr = np.ascontiguousarray(cell_pairs, dtype=np.int32).reshape(-1, 2)
+        if lib().dmxo_set_merges(self.h, _p(arr), len(arr)):
+            raise ValueError("bad merge pair")
 
     def __del__(self):
         if getattr(self, "h", None):

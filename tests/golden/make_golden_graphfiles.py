@@ -85,18 +85,36 @@ CASES = [
     ("vga_angular", "@turns_remake", ["-m", "VGA", "-vm", "angular"],
      ["Angular Mean Depth", "Angular Total Depth", "Angular Node Count"], True, "vga_angular (turns map without merge "
                                                                               "links)"),
-    # the regression inputs with merge links (LINK mode): VGA visual local has no merge logic and runs; the
-    # searches that follow merge links are refused (dmx.h, dmx_graph_set_merges)
+    # the regression inputs with merge links (LINK mode, PointMap::mergePixels): the reference's own
+    # VGA / STEPDEPTH regression cases (RegressionTest/regressionconfig.json) run on these maps
     ("vis_local", "gallery_connected.graph", ["-m", "VGA", "-vm", "visibility", "-vl"],
      ["Visual Clustering Coefficient", "Visual Control", "Visual Controllability"], True, "visibility_local"),
     ("merge_vis_global_n", "gallery_connected.graph", ["-m", "VGA", "-vm", "visibility", "-vg", "-vr", "n"], VGA_VIS,
-     True, "visibility_global_n (merge links: refused)"),
+     True, "visibility_global_n"),
+    ("merge_vis_global_3", "gallery_connected.graph", ["-m", "VGA", "-vm", "visibility", "-vg", "-vr", "3"],
+     [c + " R3" for c in VGA_VIS], True, "visibility_global_3"),
+    ("merge_sd_visual", "gallery_connected.graph", ["-m", "STEPDEPTH", "-sdt", "visual", "-sdp", "3,5"],
+     ["Visual Step Depth"], True, "vga_visual_step_depth"),
     ("merge_sd_metric", "gallery_connected.graph", ["-m", "STEPDEPTH", "-sdt", "metric", "-sdp", "3,5"],
      ["Metric Step Shortest-Path Angle", "Metric Step Shortest-Path Length", "Metric Straight-Line Distance"], True,
-     "vga_metric_step_depth (merge links: refused)"),
+     "vga_metric_step_depth"),
+    ("merge_sd_angular", "gallery_connected.graph", ["-m", "STEPDEPTH", "-sdt", "angular", "-sdp", "3,5"],
+     ["Angular Step Depth"], True, "vga_angular_step_depth"),
     ("merge_vga_metric", "turns_connected.graph", ["-m", "VGA", "-vm", "metric", "-vr", "n"],
      ["Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance", "Metric Mean Straight-Line Distance",
-      "Metric Node Count"], True, "vga_metric (merge links: refused)"),
+      "Metric Node Count"], True, "vga_metric"),
+    ("merge_vga_angular", "turns_connected.graph", ["-m", "VGA", "-vm", "angular"],
+     ["Angular Mean Depth", "Angular Total Depth", "Angular Node Count"], True, "vga_angular"),
+    ("merge_vga_metric_gallery", "gallery_connected.graph", ["-m", "VGA", "-vm", "metric", "-vr", "n"],
+     ["Metric Mean Shortest-Path Angle", "Metric Mean Shortest-Path Distance", "Metric Mean Straight-Line Distance",
+      "Metric Node Count"], True, "vga_metric_only_map (its VGA step)"),
+    ("merge_vga_angular_gallery", "gallery_connected.graph", ["-m", "VGA", "-vm", "angular"],
+     ["Angular Mean Depth", "Angular Total Depth", "Angular Node Count"], True, "vga_angular_only_map (its VGA step)"),
+    # a map with merge links unmade without -pl keeps them; making its graph again writes them back
+    ("merge_unmake", "gallery_connected.graph", ["-m", "VISPREP", "-pu"], [], False, "(-pu keeping merge links)"),
+    ("merge_remake", "@merge_unmake", ["-m", "VISPREP", "-pm"], [], True, "(making a map with merge links)"),
+    ("merge_remake_vga", "@merge_remake", ["-m", "VGA", "-vm", "visibility", "-vg", "-vr", "n"], VGA_VIS, True,
+     "(VGA global on the re-made merge-linked map)"),
 ]
 
 
@@ -116,7 +134,7 @@ def main():
             outputs[name] = dst
             b = open(dst, "rb").read()
             m = {"input": inp, "args": args, "gpu": gpu, "regression": regression, "size": len(b),
-                 "sha256": hashlib.sha256(b).hexdigest(), "columns": cols, "refused": name.startswith("merge_")}
+                 "sha256": hashlib.sha256(b).hexdigest(), "columns": cols}
             if cols:
                 m["masked_sha256"] = gu.masked_digest(b, cols)
                 got = gu.columns(b, cols)

@@ -157,3 +157,44 @@ def masked_digest(buf, names):
 def column_names(buf):
     p = parse(buf)
     return [c[0] for c in p["maps"][0]["columns"]] if p["maps"] else []
+
+
+def load_pointmap(path, i=-1):
+    """Point map i (-1: the displayed one) of a .graph file through libdmx's host reader (no GPU): dict with
+    cols, rows, spacing, bottom_left, state (x-major), bins [N][32][4], runs [R][4], merges [m][2] (cells)."""
+    import ctypes
+    from depthmapx_amd import _native as N
+    lib = N.lib()
+    h = ctypes.c_void_p()
+    N.check(lib.dmx_graphfile_read(str(path).encode(), ctypes.byref(h)))
+    try:
+        npm, disp = ctypes.c_int32(), ctypes.c_int32()
+        N.check(lib.dmx_graphfile_info(h, None, None, None, None, ctypes.byref(npm), ctypes.byref(disp)))
+        idx = disp.value if i < 0 else i
+        buf, size = ctypes.POINTER(ctypes.c_uint8)(), ctypes.c_int64()
+        N.check(lib.dmx_graphfile_pointmap(h, idx, ctypes.byref(buf), ctypes.byref(size)))
+        data = ctypes.string_at(buf, size.value)
+    finally:
+        lib.dmx_graphfile_free(h)
+    c = ctypes.c_void_p()
+    raw = np.frombuffer(data, dtype=np.uint8).copy()
+    N.check(lib.dmx_chunk_parse(N.ptr(raw), len(raw), ctypes.byref(c)))
+    try:
+        cols, rows = ctypes.c_int32(), ctypes.c_int32()
+        spacing = ctypes.c_double()
+        bl = np.zeros(2)
+        nn, nr = ctypes.c_int64(), ctypes.c_int64()
+        N.check(lib.dmx_chunk_info(c, ctypes.byref(cols), ctypes.byref(rows), ctypes.byref(spacing), N.ptr(bl),
+                                   ctypes.byref(nn), ctypes.byref(nr), None, None, None))
+        state = np.zeros(cols.value * rows.value, dtype=np.int32)
+        bins = np.zeros((nn.value, 32, 4), dtype=np.int32)
+        runs = np.zeros((max(nr.value, 1), 4), dtype=np.int16)
+        N.check(lib.dmx_chunk_arrays(c, N.ptr(state), N.ptr(bins), N.ptr(runs), None))
+        m = ctypes.c_int64()
+        N.check(lib.dmx_chunk_merges(c, None, ctypes.byref(m)))
+        merges = np.zeros((max(m.value, 1), 2), dtype=np.int32)
+        N.check(lib.dmx_chunk_merges(c, N.ptr(merges), ctypes.byref(m)))
+    finally:
+        lib.dmx_chunk_free(c)
+    return dict(cols=cols.value, rows=rows.value, spacing=spacing.value, bottom_left=(bl[0], bl[1]), state=state,
+                bins=bins, runs=runs[:nr.value], merges=merges[:m.value])

@@ -67,6 +67,27 @@ def test_help_and_missing_file(tmp_path):
     assert rc == 255 and "Failed to load graph from file" in out
 
 
+def test_remaking_a_processed_map_is_an_error(tmp_path):
+    """VISPREP -pm on a map that already has a graph: the reference's sparkGraph2 re-adds attribute rows
+    that exist and AttributeTable::addRow throws a pointer (`throw new std::invalid_argument("Duplicate
+    key")`, salalib/attributetable.cpp:278) that main's catch (std::exception&) (depthmapXcli/main.cpp:47)
+    does not catch, so depthmapXcli aborts (SIGABRT; oracle/_ref/ref_cli reproduces it in this container).
+    dmxcli reports an error with the CLI's exit code instead, before touching the GPU, and writes nothing."""
+    import lzma
+    src = tmp_path / "gallery_connected.graph"
+    with lzma.open(os.path.join(GOLDEN, "graphfiles", "inputs", "gallery_connected.graph.xz")) as f:
+        src.write_bytes(f.read())
+    out = tmp_path / "out.graph"
+    rc, msg = run("-f", str(src), "-o", str(out), "-m", "VISPREP", "-pm")
+    assert rc == 255 and "already has a graph" in msg and "Type 'depthmapXcli -h' for help" in msg, msg
+    assert not out.exists()
+    ref_cli = os.path.join(REPO, "oracle", "_ref", "ref_cli")
+    if os.path.exists(ref_cli):
+        p = subprocess.run([ref_cli, "-f", str(src), "-o", str(tmp_path / "ref.graph"), "-m", "VISPREP", "-pm"],
+                           capture_output=True, text=True)
+        assert p.returncode == -6 and "invalid_argument" in p.stderr
+
+
 @pytest.mark.gpu
 def test_cli_pipeline_matches_reference(tmp_path):
     """VISPREP -pg 1 -pp 0.5,0.5 -pm -> VGA -vm visibility -vg -vr n -> STEPDEPTH -sdt metric on the
