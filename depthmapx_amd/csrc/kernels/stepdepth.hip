@@ -105,6 +105,9 @@ __device__ __forceinline__ void sd_relax(SdShared& S, const StepDepthParams& P, 
                                          int lastu, unsigned long long ku, unsigned& relaxed) {
     if (!(f & SDF_FILLED)) return;        // diagonal-gap cells never resolve (p.filled() check)
     if (kv < ku) return;                  // already popped: m_misc == ~0
+    // merge-linked cells carry explicit marks (lastpix -3 popped, -2 merged): with angular ties a cell
+    // may be popped before u with a larger key, and a merged partner keeps the key of its link's pop
+    if ((f & SDF_MERGE) && P.lastpix[c] <= -2) return;
     relaxed++;
     if (ANG) {
         const float cv = mv;              // P.cum[c]
@@ -328,26 +331,28 @@ __device__ void sd_run(SdShared& S, const StepDepthParams& P, const int32_t* sel
         // at blocked-adjacent cells (ngraph.cpp:67-85); only merge-linked cells are queued otherwise
         if ((P.flags[uc] & SDF_EXPAND) || du == 0.0f)
             sd_relax_node<ANG>(S, P, P.cell_node[uc], ux, uy, du, cumu, lastu, ku, relaxed);
-        // ---- merge pixel not popped yet: it takes u's cumulative angle and is extracted now from
-        // (here.dist, merge pixel, NoPixel), then counts as popped (vgametricdepth.cpp:68-83,
-        // vgaangulardepth.cpp:57-67); its key becomes ku, so every later expander skips it and the
-        // step-depth rows read u's distance; lastpix -2 marks it for VGAMetric/VGAAngular, which do not
-        // count it (vgametric.cpp:97-110, vgaangular.cpp:95-106)
-        if (P.merge) {
+        // ---- merge pixel neither popped nor merged yet: it takes u's cumulative angle and is extracted
+        // now from (here.dist, merge pixel, NoPixel), then counts as done (vgametricdepth.cpp:68-83,
+        // vgaangulardepth.cpp:57-67).  Marks (lastpix): -3 = a merge-linked cell popped, -2 = merged.
+        // The merged cell's key becomes ku (the step-depth rows read u's distance); VGAMetric /
+        // VGAAngular do not count it (vgametric.cpp:97-110, vgaangular.cpp:95-106).  Keys cannot tell
+        // "popped" here: an angular relaxation at equal angle queues a smaller PixelRef after u.
+        if (P.merge && (P.flags[uc] & SDF_MERGE)) {
             const int m2 = P.merge[uc];
-            const bool take = m2 >= 0 && !(P.key[m2] < ku);
-            __syncthreads();   // every lane has read key[m2]
-            if (take) {
-                if (tid == 0) {
+            const bool take = P.lastpix[m2] > -2;
+            __syncthreads();   // every lane has read the marks
+            if (tid == 0) {
+                P.lastpix[uc] = -3;
+                if (take) {
                     P.key[m2] = ku;
                     P.cum[m2] = cumu;
                     P.lastpix[m2] = -2;
                     S.nchunk = 0;
                 }
-                __syncthreads();
-                if ((P.flags[m2] & SDF_EXPAND) || du == 0.0f)
-                    sd_relax_node<ANG>(S, P, P.cell_node[m2], m2 / P.rows, m2 % P.rows, du, cumu, -1, ku + 1ull, relaxed);
             }
+            __syncthreads();
+            if (take && ((P.flags[m2] & SDF_EXPAND) || du == 0.0f))
+                sd_relax_node<ANG>(S, P, P.cell_node[m2], m2 / P.rows, m2 % P.rows, du, cumu, -1, ku, relaxed);
         }
     }
     __syncthreads();
