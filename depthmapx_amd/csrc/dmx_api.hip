@@ -6,6 +6,10 @@
 // fails with a status code.
 #include <hip/hip_runtime.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <array>
 #include <chrono>
@@ -432,6 +436,43 @@ size_t makegraph_lds(int gcap, int bcap, int D) {
 
 } // namespace
 
+// Diagnostics (DMX_ABORT_BACKTRACE=1): SIGABRT / SIGSEGV print the native stack (frames as
+// module+offset, resolved offline with addr2line against the same build) before the previously
+// installed handler (Python's faulthandler) runs.
+namespace {
+struct sigaction g_prev_abrt, g_prev_segv;
+void dmx_crash_handler(int sig, siginfo_t* info, void* uc) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char hdr[] = "[dmx] native backtrace:\n";
+    (void)!write(2, hdr, sizeof(hdr) - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    struct sigaction* prev = sig == SIGABRT ? &g_prev_abrt : &g_prev_segv;
+    sigaction(sig, prev, nullptr);
+    if (prev->sa_flags & SA_SIGINFO) {
+        if (prev->sa_sigaction) prev->sa_sigaction(sig, info, uc);
+    } else if (prev->sa_handler != SIG_DFL && prev->sa_handler != SIG_IGN) {
+        prev->sa_handler(sig);
+    }
+    raise(sig);
+}
+void install_crash_handler() {
+    static bool done = false;
+    const char* e = getenv("DMX_ABORT_BACKTRACE");
+    if (done || !e || strcmp(e, "1") != 0) return;
+    done = true;
+    void* warm[2];
+    backtrace(warm, 2);   // loads the unwinder now: the handler must not allocate (the heap may be broken)
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = dmx_crash_handler;
+    sa.sa_flags = SA_SIGINFO;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGABRT, &sa, &g_prev_abrt);
+    sigaction(SIGSEGV, &sa, &g_prev_segv);
+}
+} // namespace
+
 extern "C" {
 
 int dmx_abi_version(void) { return DMX_ABI_VERSION; }
@@ -443,6 +484,7 @@ int dmx_ctx_create(int device, dmx_ctx** out) {
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(DMX_ERR_ARG, "device ordinal out of range");
     HIPCHK(hipSetDevice(device));
+    install_crash_handler();
     auto* c = new dmx_ctx();
     c->device = device;
     hipDeviceProp_t prop;
@@ -1422,7 +1464,10 @@ static int prepare_symmetry(dmx_graph* g) {
     HIPCHK(d_outn.alloc(nspec));
     HIPCHK(copy_sync(g->ctx->stream, d_is.p, is_spec.data(), N, hipMemcpyHostToDevice));
     HIPCHK(copy_sync(g->ctx->stream, d_specs.p, specs.data(), nspec * 4, hipMemcpyHostToDevice));
-    HIPCHK(hipMemset(d_outn.p, 0, nspec * 4));
+    // on the context stream: a null-stream hipMemset is not ordered before the kernel on this
+    // non-blocking stream, and under load the kernel then counted from stale memory (the 4-rank
+    // one-GPU rehearsal's heap abort)
+    HIPCHK(hipMemsetAsync(d_outn.p, 0, nspec * 4, s));
     hipLaunchKernelGGL(sym_special_out_kernel, dim3(nspec), dim3(256), 0, s, rows, d_specs.p, nspec,
                        g->pm->d_node_cell.p, g->pm->d_cell_node.p, d_is.p, g->node_run_start.p, g->node_nruns.p,
                        g->pool.p, d_out.p, d_outn.p, nspec);
@@ -1433,8 +1478,14 @@ static int prepare_symmetry(dmx_graph* g) {
     HIPCHK(hipStreamSynchronize(s));
     // A[a][b] = b in cells(a), over special nodes (asymmetric pairs only involve special nodes)
     std::vector<std::vector<char>> A((size_t)nspec, std::vector<char>((size_t)nspec, 0));
-    for (int a = 0; a < nspec; a++)
-        for (int j = 0; j < std::min(outn[a], nspec); j++) A[a][sidx[out[(size_t)a * nspec + j]]] = 1;
+    for (int a = 0; a < nspec; a++) {
+        if (outn[a] < 0) return fail(DMX_ERR_STATE, "internal: special-node list count out of range");
+        for (int j = 0; j < std::min(outn[a], nspec); j++) {
+            const int32_t v = out[(size_t)a * nspec + j];
+            if (v < 0 || v >= N || sidx[v] < 0) return fail(DMX_ERR_STATE, "internal: special-node list entry out of range");
+            A[a][sidx[v]] = 1;
+        }
+    }
     std::vector<std::vector<int32_t>> extra((size_t)nspec), missing((size_t)nspec);
     for (int a = 0; a < nspec; a++)
         for (int b = 0; b < nspec; b++)

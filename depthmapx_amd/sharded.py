@@ -26,7 +26,13 @@ def _rccl(dist):
 
 def _gather_host(dist, t):
     """all_gather of equal-shaped tensors on a non-RCCL backend, staged through host memory (gloo
-    rehearsals: its collectives on CUDA tensors are avoided); returns the concatenation on t's device."""
+    rehearsals: its collectives on CUDA tensors are avoided); returns the concatenation on t's device.
+    DMX_GLOO_DEVICE_TENSORS=1 hands gloo the device tensors instead (diagnostic of DESIGN.md section 5)."""
+    import os
+    if os.environ.get("DMX_GLOO_DEVICE_TENSORS") == "1":
+        parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, t)
+        return torch.cat(parts)
     parts = [torch.empty(t.shape, dtype=t.dtype) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, t.cpu())
     return torch.cat(parts).to(t.device)
@@ -35,28 +41,6 @@ def _gather_host(dist, t):
 def shard_range(n, rank, world):
     """Contiguous, balanced split of n units over `world` ranks."""
     return (n * rank) // world, (n * (rank + 1)) // world
-
-
-def allgather_blobs(blob, dist, device=None):
-    """All-gather ragged 1-D uint8 tensors.  Returns (flat tensor of world*maxlen bytes, sizes):
-    rank i's blob occupies flat[i*maxlen : i*maxlen + sizes[i]]."""
-    world = dist.get_world_size()
-    device = device if device is not None else blob.device
-    sz = torch.tensor([blob.numel()], dtype=torch.int64, device=device)
-    sizes = [torch.zeros_like(sz) for _ in range(world)]
-    dist.all_gather(sizes, sz)
-    sizes = [int(s.item()) for s in sizes]
-    mx = max(sizes)
-    mine = torch.zeros(mx, dtype=torch.uint8, device=device)
-    mine[: blob.numel()] = blob
-    flat = torch.empty(world * mx, dtype=torch.uint8, device=device)
-    if _rccl(dist) and device.type == "cuda":
-        dist.all_gather_into_tensor(flat, mine)
-    else:
-        parts = list(flat.view(world, mx).unbind(0))
-        dist.all_gather(parts, mine)
-        flat = torch.stack(parts).reshape(-1)
-    return flat, mx, sizes
 
 
 def exchange_graph(pm, ctx, shard, dist, device):
@@ -115,28 +99,6 @@ def choose_mk_mode(dist, device, world, mk_shard_s, exchange_s, shard_frac):
     return ("replicate" if replicate_s < shard_s else "shard"), {"predicted_replicate_s": replicate_s,
                                                                  "predicted_shard_s": shard_s,
                                                                  "mk_shard_s": mk, "exchange_s": ex}
-
-
-def allgather_rows(full, n, dist):
-    """full: [n, k] tensor where this rank filled rows shard_range(n, rank, world); afterwards every
-    rank holds all rows."""
-    world, rank = dist.get_world_size(), dist.get_rank()
-    b, e = shard_range(n, rank, world)
-    per = (n + world - 1) // world
-    k = full.shape[1]
-    mine = torch.zeros((per, k), dtype=full.dtype, device=full.device)
-    mine[: e - b] = full[b:e]
-    if _rccl(dist) and full.device.type == "cuda":
-        gathered = torch.empty((world * per, k), dtype=full.dtype, device=full.device)
-        dist.all_gather_into_tensor(gathered, mine)
-    else:
-        parts = [torch.empty_like(mine) for _ in range(world)]
-        dist.all_gather(parts, mine)
-        gathered = torch.cat(parts)
-    for r in range(world):
-        rb, re_ = shard_range(n, r, world)
-        full[rb:re_] = gathered[r * per: r * per + (re_ - rb)]
-    return full
 
 
 def device_view(ptr, count, dtype, device):

@@ -197,3 +197,27 @@ def test_2000_vga_sources_match_oracle(big2000, ctx):
     np.testing.assert_array_equal(got[:, 5], want[:, 5])
     assert (np.abs(got - want) <= 1e-6 * np.maximum(1.0, np.abs(want))).all()
     assert (want[:, 5] > 0.5 * N).all()
+
+
+def test_2000_metric_stepdepth_matches_oracle(big2000, ctx):
+    """configs[4] step depth at size against the pinned oracle: the C restatement's std::set search
+    (oracle/dmx_oracle.c metric_search, vgametricdepth.cpp:23-92) over the same 2000^2 graph from the
+    same cell.  Lengths and straight-line distances bit-exact, angles within 1e-6 (north_star)."""
+    import time
+    import bench
+    pm, g, om = big2000
+    cell = bench.nearest_filled(pm, 1000.0, 1000.0)
+    a = g.metric_step_depth(cells=[cell])
+    assert ctx.last_stepdepth()["mode"] == "batched"
+    if getattr(om, "_borrowed", None) is None:
+        full = g.copy(runs=True)
+        om.set_graph_view(full["bins"], full["runs"])
+        del full
+    t0 = time.perf_counter()
+    ref = om.metric_stepdepth([cell])
+    print("oracle metric step depth at 2000^2/5000: %.1f s" % (time.perf_counter() - t0))
+    np.testing.assert_array_equal(a[:, 1:].view(np.uint32), ref[:, 1:].view(np.uint32))
+    reached = ref[:, 1] >= 0
+    assert reached.mean() > 0.99
+    assert np.allclose(a[reached, 0], ref[reached, 0], rtol=1e-6, atol=1e-6)
+    np.testing.assert_array_equal(a[~reached], ref[~reached])

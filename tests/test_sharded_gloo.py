@@ -98,9 +98,11 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_matches_single_process():
+@pytest.mark.parametrize("world", [2, 4])
+def test_multi_rank_gloo_matches_single_process(world):
+    """World 2 and 4 (the 4-rank one-GPU rehearsal's shard ranges, blob sizes and row lists, DESIGN.md
+    section 5) through the same helpers bench.py runs."""
     from pyoracle import OracleMap
-    world = 2
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -117,8 +119,10 @@ def test_two_rank_gloo_matches_single_process():
     om.make_graph()
     g = om.graph()
     ref = om.vga_global()
-    assert len({r[4] for r in res}) == 1 and res[0][5]["mk_shard_s"] == 2.0 and res[0][5]["exchange_s"] == 0.5
-    assert res[0][4] == "shard"       # 2.0 + 0.5 < 2.0 / (1/2)
+    # every rank measured mk = 1 + rank, exchange = 0.5 rank: the decision uses the max over ranks
+    assert len({r[4] for r in res}) == 1 and res[0][5]["mk_shard_s"] == float(world)
+    assert res[0][5]["exchange_s"] == 0.5 * (world - 1)
+    assert res[0][4] == "shard"       # world + 0.5 (world - 1) < world / (1 / world)
     for _, bins, runs, out, _, _ in res:
         np.testing.assert_array_equal(bins, g["bins"])
         np.testing.assert_array_equal(runs, g["runs"])
