@@ -3,6 +3,9 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/${TAG:-r3scale}
 mkdir -p $OUT
+(while true; do date >> $OUT/heartbeat.txt; sleep 45; done) &
+HB=$!
+trap "kill $HB" EXIT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_sharded_1000.py -x -v -s -m gpu --timeout 500 --timeout-method thread > $OUT/sharded1000.log 2>&1
 rc1=$?
 echo "sharded1000 rc=$rc1"; tail -5 $OUT/sharded1000.log

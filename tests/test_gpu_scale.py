@@ -219,5 +219,10 @@ def test_2000_metric_stepdepth_matches_oracle(big2000, ctx):
     np.testing.assert_array_equal(a[:, 1:].view(np.uint32), ref[:, 1:].view(np.uint32))
     reached = ref[:, 1] >= 0
     assert reached.mean() > 0.99
-    assert np.allclose(a[reached, 0], ref[reached, 0], rtol=1e-6, atol=1e-6)
+    ga, ra = a[reached, 0], ref[reached, 0]
+    # acos of a rounded cosine above 1 is NaN in the reference too (pixelref.h:121-131)
+    assert np.array_equal(np.isnan(ga), np.isnan(ra)), (int(np.isnan(ga).sum()), int(np.isnan(ra).sum()))
+    fin = ~np.isnan(ra)
+    bad = ~np.isclose(ga[fin], ra[fin], rtol=1e-6, atol=1e-6)
+    assert not bad.any(), (int(bad.sum()), float(np.abs(ga[fin] - ra[fin]).max()))
     np.testing.assert_array_equal(a[~reached], ref[~reached])

@@ -8,8 +8,8 @@ calls on each rank (depthmapx_amd/sharded.py):
      the rank's slot of the padded exchange buffer (what all_gather_into_tensor fills over RCCL);
   2. assembly of the whole graph from the 8 blobs: byte-identical to the one-shot graph's blob;
   3. the VGA preparation split by node range (Graph.set_prep_shard): every rank's partial buffers are
-     recorded call by call and summed on the host -- the in-process stand-in for the RCCL all-reduce --
-     and the final rank receives the sums through the same callback protocol;
+     summed on the host call by call -- the in-process stand-in for the RCCL all-reduce, call k resolved
+     in pass k over the ranks -- and the final graph receives the sums through the same callback;
   4. VGA global for each rank's interleaved source chunks (vga_nodes) into the shared [N][7] output
      (the row all-gather is pure data movement), which must be bit-identical to the single-process run.
 Reference path: vgavisualglobal.cpp:23-216 (the single-process run is pinned to the oracle by
@@ -82,36 +82,48 @@ def test_1000_sharded_choreography_matches_single_run(ctx):
     g2.close()
     _release()
 
-    # 3. sharded preparation: record every rank's partial buffers, sum them call by call
+    # 3. sharded preparation.  The all-reduce is a collective: a call returns only with the sum of every
+    #    rank's partial buffer, and what a rank computes next may depend on it.  Emulated one rank at a
+    #    time, call k is resolved in pass k: each rank replays the known sums of calls 0..k-1, hands in
+    #    its partial for call k and stops there (the callback fails the preparation); the partials are
+    #    summed on the host.  A pass in which no rank reaches call k ends the protocol.
     sums = []
+    for k in range(16):
+        reached = 0
+        for r, (b, e) in enumerate(ranges):
+            gr = pm.assemble(ctx, ptrs, sizes)
+            calls = [0]
 
-    def recorder():
-        calls = [0]
-
-        def fn(ptr, count, dtype):
-            i = calls[0]
-            calls[0] += 1
-            part = device_view(ptr, count, dtype, dev).cpu()
-            if i == len(sums):
-                sums.append(part.clone())
-            else:
-                assert sums[i].shape == part.shape and sums[i].dtype == part.dtype
-                sums[i] += part
-            return 0
-        return fn, calls
-
-    ncalls = None
-    for r, (b, e) in enumerate(ranges):
-        gr = pm.assemble(ctx, ptrs, sizes)
-        fn, calls = recorder()
-        gr.set_prep_shard(b, e, fn)
-        scratch = torch.empty((1, 7), dtype=torch.float32, device=dev)
-        gr.vga_visual_global_device_list(scratch.data_ptr(), np.zeros(0, dtype=np.int64))   # preparation only
-        assert ncalls in (None, calls[0])          # every rank calls the all-reduce equally often
-        ncalls = calls[0]
-        gr.close()
-        _release()
-    assert ncalls >= 3                             # symmetry sums, veto, tile-visibility rows
+            def fn(ptr, count, dtype, k=k, calls=calls):
+                i = calls[0]
+                calls[0] += 1
+                t = device_view(ptr, count, dtype, dev)
+                if i < k:
+                    assert t.numel() == sums[i].numel()
+                    t.copy_(sums[i].to(dev))
+                    torch.cuda.synchronize(dev)
+                    return 0
+                part = t.cpu()
+                if len(sums) == k:
+                    sums.append(part.clone())
+                else:
+                    assert sums[k].shape == part.shape and sums[k].dtype == part.dtype
+                    sums[k] += part
+                return -1                          # stop this rank's preparation at call k
+            gr.set_prep_shard(b, e, fn)
+            scratch = torch.empty((1, 7), dtype=torch.float32, device=dev)
+            try:
+                gr.vga_visual_global_device_list(scratch.data_ptr(), np.zeros(0, dtype=np.int64))
+            except dmx.DmxError:
+                pass
+            reached += calls[0] > k
+            gr.close()
+            _release()
+        assert reached in (0, W)                   # every rank makes the same calls
+        if reached == 0:
+            break
+    ncalls = len(sums)
+    assert ncalls >= 5                             # symmetry sums (2), veto, tile-visibility rows (2)
 
     # the final rank gets the sums through the callback, then every rank's sources run on its graph
     g = pm.assemble(ctx, ptrs, sizes)
