@@ -9,8 +9,9 @@ BFS of any source walks the whole graph, so every rank needs all of it:
   --mk-mode shard:     each rank builds its source range, the run-length shards are all-gathered
                        over RCCL and assembled (bytes ~ 8 B/run: 574 MB at 256^2, 36 GB at 1000^2);
   --mk-mode replicate: every rank builds the whole graph (no data-path collective);
-  auto:                shard (the all-gather moves ~36 GB at 1000^2, well under a second over xGMI,
-                       against ~10 s of makeGraph that replicate would repeat on every rank).
+  auto (default):      the first warm-up step runs sharded and measures the shard build and the
+                       exchange (max over ranks); every rank then keeps the mode that measurement
+                       predicts faster (sharded.choose_mk_mode).  With no warm-up step it stays sharded.
 then VGA for the rank's sources and one RCCL all-gather of the 7 float columns.
 Inputs (grid state + occluder pieces) are resident in HBM before the timed region; value =
 filled cells / step time (max over ranks).
@@ -69,13 +70,14 @@ def nearest_filled(pm, x, y):
     raise RuntimeError("no filled cell")
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r2_pmc_1000.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r3_pmc.json")
 FP64_PEAK_TF = 78.6    # MI355X FP64 vector (MI355X_MICROARCH.md)
 
 
 def load_pmc(workload):
     """Per-kernel PMC summary of the same workload and build (scripts/gpu_pmc.sh -> scripts/pmc_summary.py ->
-    profiles/r2_pmc_1000.json): HBM bytes raw and 2x-FETCH corrected, VALU issue, FP64 instruction counts."""
+    profiles/r3_pmc.json): HBM bytes raw and 2x-FETCH corrected, L2 hit rate, VALU issue, FP64 instruction
+    counts."""
     if not os.path.exists(PMC_SUMMARY):
         return {}
     try:
@@ -110,7 +112,10 @@ def calibration():
     p = os.path.join(REPO, "tests", "golden", "oracle_calibration.json")
     try:
         d = json.load(open(p))
-        return {"makegraph": d["ref_over_port_makegraph"], "vga": d["ref_over_port_vga"], "measured_on": d["cpu"]}
+        out = {"makegraph": d["ref_over_port_makegraph"], "vga": d["ref_over_port_vga"], "measured_on": d["cpu"]}
+        if "ref_over_port_stepdepth" in d:
+            out["stepdepth"] = d["ref_over_port_stepdepth"]
+        return out
     except Exception:
         return None
 
@@ -130,7 +135,7 @@ def _legs(mk1, mkT, v1=None, vT=None):
     return one, allc
 
 
-def cpu_baseline(region, lines, spacing, fill, g, budget_s, seed=2026, stepdepth=False, N=None):
+def cpu_baseline(region, lines, spacing, fill, g, budget_s, seed=2026, stepdepth=False, N=None, sd_cell=None):
     """The C restatement (oracle/dmx_oracle.c, bit-exact vs the reference) on the GPU box's host cores, on a
     bounded seeded sample of the same workload:
       makeGraph: S=200 random sources (seed 2026): one thread, then all cores (OpenMP over sources);
@@ -158,11 +163,21 @@ def cpu_baseline(region, lines, spacing, fill, g, budget_s, seed=2026, stepdepth
                                        "source_s_max": float(mk_secs.max())}}
     cal = calibration()
     if stepdepth:
-        # config 5: the step-depth leg needs the whole ~94 GB graph on the host; not sampled (rate overstated)
-        one, allc = _legs(mk1, mkT)
-        rec["sample"] = ("oracle/dmx_oracle.c: makeGraph on %d seeded random sources, 1 thread %.2f s, %d threads "
-                         "%.2f s; metric step depth not sampled (CPU rate overstated)" % (len(mk_nodes), mk1_wall, T,
-                                                                                          mkT_wall))
+        # config 5: the metric step depth from the config cell over the whole graph (~94 GB, copied from the
+        # GPU and read in place): one search, single-threaded like the reference, run in full (not sampled)
+        print("[bench] CPU baseline: graph copy + metric step depth", file=sys.stderr, flush=True)
+        gn = g.copy(runs=True)
+        om.set_graph_view(gn["bins"], gn["runs"])
+        t0 = time.perf_counter()
+        om.metric_stepdepth([sd_cell])
+        sd_s = time.perf_counter() - t0
+        del om, gn
+        # a step = every cell's makeGraph sweep + the one search: per-cell cost mk + sd / N
+        one, allc = _legs(mk1 + sd_s / N, mkT + sd_s / N)
+        rec["stepdepth"] = {"cell": int(sd_cell), "one_thread_s": sd_s}
+        rec["sample"] = ("oracle/dmx_oracle.c: makeGraph on %d seeded random sources (1 thread %.2f s, %d threads "
+                         "%.2f s) + the whole metric step depth from cell %d on 1 thread (%.1f s; the search is "
+                         "sequential on every core count)" % (len(mk_nodes), mk1_wall, T, mkT_wall, sd_cell, sd_s))
     else:
         print("[bench] CPU baseline: graph copy + BFS sample", file=sys.stderr, flush=True)
         gn = g.copy(runs=True)
@@ -189,8 +204,10 @@ def cpu_baseline(region, lines, spacing, fill, g, budget_s, seed=2026, stepdepth
     rec["value"] = allc
     rec["single_thread"] = {"value": one, "cores": 1}
     if cal:
-        ref = 1.0 / (mk1 * cal["makegraph"] + (rec["vga"]["s_per_source_one_thread"] * cal["vga"]
-                                                if "vga" in rec else 0.0))
+        if stepdepth:
+            ref = 1.0 / (mk1 * cal["makegraph"] + rec["stepdepth"]["one_thread_s"] * cal.get("stepdepth", 1.0) / N)
+        else:
+            ref = 1.0 / (mk1 * cal["makegraph"] + rec["vga"]["s_per_source_one_thread"] * cal["vga"])
         rec["reference_equivalent"] = {"value": ref, "cores": 1, "ref_over_port": cal,
                                        "note": "one-thread rate / the reference-over-restatement ratio measured on "
                                                "identical inputs (tests/golden/oracle_calibration.json)"}
@@ -250,9 +267,8 @@ def main():
         W, lmin, lmax = args.grid or (256 if args.config == 1 else 1000), 0.02, 0.10
     # makeGraph across ranks: "auto" runs the first warm-up step sharded, measures the shard build and the
     # graph exchange, then keeps whichever of shard / replicate the measurement predicts faster (max over
-    # ranks: sharded.choose_mk_mode).  With no warm-up step it stays sharded (the
-    # exchange moves ~36 GB at 1000^2, well under a second at xGMI all-gather rates, against ~5 s of makeGraph
-    # that replicate repeats on every rank).
+    # ranks: sharded.choose_mk_mode).  With no warm-up step it stays sharded.  The exchange over xGMI is not
+    # measured on a one-GPU box: DESIGN.md section 5 gives the prediction per world size.
     mk_mode = args.mk_mode
     mk_auto = None
     if world == 1 and mk_mode == "auto":
@@ -302,6 +318,7 @@ def main():
                 kt["exchange_s"] += xt["blob_s"] + xt["allgather_s"] + xt["assemble_s"]
                 kt["allgather_s"] += xt["allgather_s"]
                 kt["xbytes"] = xt["bytes"]
+                kt["xpeak"] = max(kt.get("xpeak") or 0, xt.get("device_peak_bytes") or 0)
         else:
             g = shard
         if stepdepth:
@@ -393,22 +410,30 @@ def main():
             second = "stepdepth_kernel"
         dominant = second if vga_s >= mk_s else "makegraph_kernel"
         dom_bytes, dom_s = (vga_bytes, vga_s) if vga_s >= mk_s else (mk_bytes, mk_s)
-        achieved = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
+        work_rate = dom_bytes / dom_s / 1e9 if dom_s > 0 else 0.0
         pmc = load_pmc(workload) if world == 1 else {}
         dpm = pmc.get(dominant, {})
         dps = dpm.get("per_step", {})
-        roof = {"bound": "hbm", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                # HBM bytes per launch from the PMC passes of this workload and build: FETCH_SIZE + WRITE_SIZE as
-                # read (neither kernel streams 16 B/lane, where the guide's 2x FETCH correction applies); the
-                # corrected figure is an upper bound
-                # per step: a kernel launched more than once per step (makeGraph: the sample pass, the main
-                # launch and the capacity retry) is counted over all its launches, like the live time
-                "traffic": dps.get("hbm_bytes_raw", dpm.get("hbm_bytes_raw")),
-                "traffic_corrected_2x_fetch": dps.get("hbm_bytes_corrected", dpm.get("hbm_bytes_corrected")),
+        traffic = dps.get("hbm_bytes_raw", dpm.get("hbm_bytes_raw"))
+        traffic_2x = dps.get("hbm_bytes_corrected", dpm.get("hbm_bytes_corrected"))
+        # achieved = HBM bytes the counters measured for the dominant kernel (FETCH_SIZE + WRITE_SIZE per step,
+        # PMC passes of this workload and build) over its live time; the 2x-FETCH figure (the guide's
+        # correction for 16 B/lane streaming loads, which neither kernel issues) bounds it from above.  The
+        # kernels' work models (bytes of run records, bitmap words and rows they read, most of them served
+        # by the L2 / MALL / LDS) are reported as work_model_rate.  The binding limit
+        # is instruction issue and memory latency, not HBM bandwidth: bound = "issue".
+        if traffic:
+            achieved, basis = traffic / dom_s / 1e9, "pmc FETCH_SIZE + WRITE_SIZE per step / live kernel time"
+        else:
+            achieved, basis = work_rate, "work model (no PMC summary of this workload and build)"
+        roof = {"bound": "issue", "kernel": dominant, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "achieved_basis": basis,
+                "frac_upper_2x_fetch": traffic_2x / dom_s / 1e9 / HBM_PEAK_GBS if traffic_2x else None,
+                "traffic": traffic, "traffic_corrected_2x_fetch": traffic_2x,
                 "traffic_source": os.path.relpath(PMC_SUMMARY, REPO) if dpm else None,
-                "algorithmic_bytes": dom_bytes, "launches_per_step": dpm.get("calls"),
-                "kernel_s_live": dom_s,
+                "l2_hit_rate": dpm.get("l2_hit_rate"),
+                "algorithmic_bytes": dom_bytes, "work_model_rate": work_rate,
+                "launches_per_step": dpm.get("calls"), "kernel_s_live": dom_s,
                 "kernel_s_rocprof": dps.get("duration_ns", dpm.get("duration_ns", 0)) * 1e-9 if dpm else None}
         if not stepdepth:
             # SURVEY.md section 8(d) B_vga at batch size 1 = the reference's BFS work (every source reads every
@@ -424,7 +449,8 @@ def main():
             kp = pmc.get(kname)   # (not `e`: b, e is this rank's makeGraph shard, used below)
             if kp and "valu_active_frac" in kp:
                 issue[kname] = {"valu_busy_frac": kp["valu_active_frac"], "valu_issue_frac": kp.get("valu_issue_frac"),
-                                "wave_cycles_split": kp.get("wave_cycles_split"), "clock_ghz": kp.get("clock_ghz")}
+                                "wave_cycles_split": kp.get("wave_cycles_split"), "clock_ghz": kp.get("clock_ghz"),
+                                "l2_hit_rate": kp.get("l2_hit_rate")}
         if issue:
             roof["issue"] = issue
         mkp = pmc.get("makegraph_kernel", {})
@@ -468,7 +494,7 @@ def main():
         if kt["exchange_s"] or mk_auto:
             rec["kernels"]["graph_exchange"] = {
                 "s_per_step": kt["exchange_s"] / max(kt["n"], 1), "allgather_s": kt["allgather_s"] / max(kt["n"], 1),
-                "bytes": kt["xbytes"], "auto": mk_auto}
+                "bytes": kt["xbytes"], "device_peak_bytes": kt.get("xpeak"), "auto": mk_auto}
         if stepdepth:
             rec["metric"] = "grid cells/sec for VISPREP makeGraph + metric step depth on N×N grid"
             kk = rec["kernels"]
@@ -480,7 +506,7 @@ def main():
                        "stepdepth_reached_cells": int((sd_out[0][:, 0] >= 0).sum())})
         if not args.no_cpu_baseline and world == 1:
             rec["cpu_baseline"] = cpu_baseline(region, lines, 1.0, fill, g, args.cpu_budget, stepdepth=stepdepth,
-                                               N=N)
+                                               N=N, sd_cell=sd_cell)
             rec["vs_cpu_baseline"] = rec["value"] / rec["cpu_baseline"]["value"]
         print(json.dumps(rec), flush=True)
         if args.dump_out and out_full is not None:

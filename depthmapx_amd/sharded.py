@@ -44,16 +44,24 @@ def shard_range(n, rank, world):
 
 
 def exchange_graph(pm, ctx, shard, dist, device):
-    """Step 2 on device memory: every rank's run-length shard blob is written straight into its padded
-    send buffer, all-gathered (RCCL all_gather_into_tensor over xGMI) and assembled into the whole graph.
-    Returns (graph, {"blob_s", "allgather_s", "assemble_s", "bytes"}); the phases are bracketed by device
-    synchronisations so that bench.py can size the exchange against replicated makeGraph."""
+    """Step 2 on device memory: every rank writes its run-length shard blob straight into its own slot of
+    the padded exchange buffer, the buffer is all-gathered in place (RCCL all_gather_into_tensor over xGMI,
+    the rank's slot as the input: no separate send buffer) and assembled into the whole graph.  The shard
+    graph is closed once its blob is written, so the rank holds at most the exchange buffer and the
+    assembled graph at once.  Returns (graph, {"blob_s", "allgather_s", "assemble_s", "bytes",
+    "padded_bytes", "device_peak_bytes"}); the phases are bracketed by device synchronisations so that
+    bench.py can size the exchange against replicated makeGraph, and device_peak_bytes is the most
+    device memory in use (torch.cuda.mem_get_info: libdmx's allocations included) at the phase ends."""
     import time
-    world = dist.get_world_size()
+    world, rank = dist.get_world_size(), dist.get_rank()
+    cuda = device.type == "cuda"
+    peak = [0]
 
     def sync():
-        if device.type == "cuda":
+        if cuda:
             torch.cuda.synchronize(device)
+            free, total = torch.cuda.mem_get_info(device)
+            peak[0] = max(peak[0], total - free)
     sync()
     t0 = time.perf_counter()
     n = shard.blob_size()
@@ -65,11 +73,13 @@ def exchange_graph(pm, ctx, shard, dist, device):
     else:
         sizes = [int(v) for v in _gather_host(dist, sz).tolist()]
     mx = max(sizes)
-    mine = torch.empty(mx, dtype=torch.uint8, device=device)
+    flat = torch.empty(world * mx, dtype=torch.uint8, device=device)
+    mine = flat[rank * mx:(rank + 1) * mx]
     shard.write_blob_device(mine.data_ptr(), n)
     sync()
+    if hasattr(shard, "close"):
+        shard.close()   # the shard's pool and tables are in the blob now
     t1 = time.perf_counter()
-    flat = torch.empty(world * mx, dtype=torch.uint8, device=device)
     if _rccl(dist):
         dist.all_gather_into_tensor(flat, mine)
     else:
@@ -83,7 +93,7 @@ def exchange_graph(pm, ctx, shard, dist, device):
     t3 = time.perf_counter()
     del flat
     return g, {"blob_s": t1 - t0, "allgather_s": t2 - t1, "assemble_s": t3 - t2, "bytes": sum(sizes),
-               "padded_bytes": world * mx}
+               "padded_bytes": world * mx, "device_peak_bytes": peak[0] if cuda else None}
 
 
 def choose_mk_mode(dist, device, world, mk_shard_s, exchange_s, shard_frac):

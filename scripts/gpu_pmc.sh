@@ -18,6 +18,7 @@ pass() {
 pass stats --kernel-trace --stats && \
 pass fetch --pmc FETCH_SIZE && \
 pass write --pmc WRITE_SIZE && \
+pass l2 --pmc TCC_HIT_sum TCC_MISS_sum && \
 pass issue --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY \
   SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU GRBM_GUI_ACTIVE && \
 pass mix --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 \

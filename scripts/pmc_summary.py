@@ -11,6 +11,7 @@ Per kernel (makegraph_kernel, vga_tile_kernel, ...), averaged per launch:
                         uncalibrated.  Neither kernel streams 16 B/lane (makeGraph: 4-8 B gathers,
                         VGA: 8 B run records and 8 B bitmap words), so the raw figure is the reported
                         traffic and the corrected one an upper bound.
+  l2_hit_rate         = TCC_HIT / (TCC_HIT + TCC_MISS) (guide, "L2 (per XCD)")
   clock_ghz           = GRBM_GUI_ACTIVE / 8 XCDs / duration (guide, "DVFS give-back")
   valu_issue_frac     = SQ_INSTS_VALU x 2 cycles / (1024 SIMDs x cycles): a wave64 VALU instruction
                         occupies its SIMD for 2 cycles (guide, "SIMD-32"), so 1.0 = every SIMD issuing
@@ -80,6 +81,9 @@ def main():
             f, w = 1024.0 * c["FETCH_SIZE"], 1024.0 * c["WRITE_SIZE"]
             e["fetch_bytes"], e["write_bytes"] = f, w
             e["hbm_bytes_raw"], e["hbm_bytes_corrected"] = f + w, 2.0 * f + w
+        hit, miss = c.get("TCC_HIT_sum", c.get("TCC_HIT")), c.get("TCC_MISS_sum", c.get("TCC_MISS"))
+        if hit is not None and miss is not None and hit + miss > 0:
+            e["l2_hit_rate"] = hit / (hit + miss)   # MI355X_MICROARCH.md "L2 (per XCD)"
         cyc = c.get("GRBM_GUI_ACTIVE", 0.0) / N_XCD
         if cyc > 0:
             e["cycles"] = cyc
