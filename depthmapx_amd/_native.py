@@ -7,7 +7,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "libdmx.so")
+# DMX_LIB: another in-tree build of the same library (A/B kernel experiments, scripts/gpu_mk_ab.sh)
+LIB_PATH = os.environ.get("DMX_LIB") or os.path.join(_HERE, "_lib", "libdmx.so")
 
 DMX_OK = 0
 STATUS_NAMES = {-1: "DMX_ERR_ARG", -2: "DMX_ERR_HIP", -3: "DMX_ERR_CAPACITY", -4: "DMX_ERR_STATE",
@@ -33,6 +34,7 @@ SIGNATURES = {
     "dmx_pointmap_state": (_i32, [_vp, _vp]),
     "dmx_pointmap_cell_lines": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_makegraph": (_i32, [_vp, _vp, _dbl, _i32, _i64, _i64, _vp]),
+    "dmx_makegraph_balance": (_i32, [_vp, _vp, _dbl, _i32, _i32, _i64, _vp]),
     "dmx_graph_free": (_i32, [_vp]),
     "dmx_graph_info": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_graph_copy": (_i32, [_vp, _vp, _vp, _vp, _vp]),

@@ -504,7 +504,7 @@ int dmx_ctx_create(int device, dmx_ctx** out) {
 }
 
 int dmx_ctx_set_progress(dmx_ctx* ctx, dmx_progress_fn fn, void* user, double interval_s) {
-    if (!ctx || !(interval_s >= 0.0)) return fail(DMX_ERR_ARG, "bad arguments");
+    if (!ctx || interval_s != interval_s) return fail(DMX_ERR_ARG, "bad arguments");   // NaN only: <= 0 means 0.5 s
     ctx->progress = fn;
     ctx->progress_user = user;
     ctx->progress_interval = interval_s > 0.0 ? interval_s : 0.5;
@@ -842,20 +842,23 @@ int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, i
 // makeGraph kernel variant: VGPR budget (waves per SIMD) chosen at launch (DMX_MK_WPE, default 5).
 // The kernel is latency-bound (one wave walks one source's sieve depth by depth), so waves beat
 // registers: at 1000^2, 3 waves/SIMD 6.9 s, 4: 5.7 s, 5: 5.3 s (96 VGPRs, some spills), 6: 5.4 s.
+// fixed: the first-pass LDS capacities compiled in; count: the cost-sample counters (makegraph.hip).
 typedef void (*mk_kernel_t)(const MakeGraphParams*);
-static mk_kernel_t mk_kernel() {
+static mk_kernel_t mk_kernel(bool fixed, bool count) {
     const char* e = getenv("DMX_MK_WPE");
     const int w = e ? atoi(e) : 5;
-    const bool prof = verbose() != 0;
-    if (w >= 8) return prof ? makegraph_kernel<8, true> : makegraph_kernel<8, false>;
-    if (w >= 6) return prof ? makegraph_kernel<6, true> : makegraph_kernel<6, false>;
-    if (w == 5) return prof ? makegraph_kernel<5, true> : makegraph_kernel<5, false>;
-    if (w == 4) return prof ? makegraph_kernel<4, true> : makegraph_kernel<4, false>;
-    return prof ? makegraph_kernel<3, true> : makegraph_kernel<3, false>;
+    if (verbose()) return fixed ? makegraph_kernel<5, true, true, false> : makegraph_kernel<5, true, false, false>;
+    if (count) return fixed ? makegraph_kernel<5, false, true, true> : makegraph_kernel<5, false, false, true>;
+    if (w >= 6) return fixed ? makegraph_kernel<6, false, true, false> : makegraph_kernel<6, false, false, false>;
+    if (w == 4) return fixed ? makegraph_kernel<4, false, true, false> : makegraph_kernel<4, false, false, false>;
+    return fixed ? makegraph_kernel<5, false, true, false> : makegraph_kernel<5, false, false, false>;
 }
 
-int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int64_t node_begin, int64_t node_end,
-                  dmx_graph** out) {
+// makeGraph over [node_begin, node_end), or only over the listed nodes of that range (`only`: the cost
+// sample of dmx_makegraph_balance; the graph's other nodes stay unset).  d_work (optional, [n][2]) receives
+// each published source's sieve depth steps and candidate chunks.
+static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int64_t node_begin,
+                          int64_t node_end, const std::vector<int64_t>* only, uint32_t* d_work, dmx_graph** out) {
     if (!ctx || !pm || !out) return fail(DMX_ERR_ARG, "bad arguments");
     HIPCHK(hipSetDevice(ctx->device));
     const double t_start = now_s();
@@ -897,7 +900,11 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     if (const char* e = getenv("DMX_MK_SPILL")) spill_cap = std::max(1, atoi(e));
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    int64_t pool_cap = std::max<int64_t>(n * std::max<int64_t>(64, 6 * (int64_t)D), 1024);
+    const int64_t n_src = only ? (int64_t)only->size() : n;   // sources this call sweeps
+    if (only)
+        for (int64_t v : *only)
+            if (v < node_begin || v >= node_end) return fail(DMX_ERR_ARG, "sample node outside the range");
+    int64_t pool_cap = std::max<int64_t>(n_src * std::max<int64_t>(64, 6 * (int64_t)D), 1024);
     ctx->last_mk_s = 0;
     DevBuf<int64_t> fail_list, node_list;
     DevBuf<MakeGraphParams> dP;   // kernel parameters in device memory (see makegraph_kernel)
@@ -911,13 +918,18 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
     // still re-runs everything with a doubled pool.
     const int64_t kSample = 4096;
     const bool big_pool = (double)pool_cap * sizeof(Run) > 0.4 * (double)(free_b + cached_bytes());
-    bool sampling = !getenv("DMX_MK_NOSAMPLE") &&
+    bool sampling = !only && !getenv("DMX_MK_NOSAMPLE") &&
                     ((n >= 16 * kSample && big_pool) || (n >= kSample && getenv("DMX_MK_SAMPLE")));   // test hook
     double mk_total_s = 0.0;
     for (int restart = 0; restart < 4; restart++) {
         // one full pass, then re-runs of only the sources that overflowed an LDS / staging capacity
         double kernel_s = 0.0;
         int64_t list_n = -1;   // -1: the whole range
+        if (only) {
+            list_n = n_src;
+            if (list_n)
+                HIPCHK(hipMemcpyAsync(node_list.p, only->data(), list_n * 8, hipMemcpyHostToDevice, ctx->stream));
+        }
         bool pool_over = false;
         const int64_t pool_cap_full = pool_cap;
         if (sampling) {
@@ -931,7 +943,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), ctx->stream));
         size_t lds0 = makegraph_lds(gcap, bcap, D);
         int occ0 = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, mk_kernel(), 64, lds0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, mk_kernel(false, d_work != nullptr), 64, lds0));
         {
             const int64_t waves0 = std::min<int64_t>((int64_t)ctx->num_cu * std::max(occ0, 1), std::max<int64_t>(n, 1));
             const size_t stage0 = (size_t)waves0 * (capB * 16 + (3 * ((size_t)D + 1) + 4) * 4) * 4;   // headroom for retries
@@ -947,8 +959,10 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         for (int attempt = 0; attempt < 8; attempt++) {
             size_t lds = makegraph_lds(gcap, bcap, D);
             if (lds > 160 * 1024) return fail(DMX_ERR_CAPACITY, "makegraph LDS requirement exceeds 160 KiB");
+            const mk_kernel_t kern = mk_kernel(gcap == MK_GCAP0 && bcap == MK_BCAP0 && !getenv("DMX_MK_NOFIXED"),
+                                               d_work != nullptr);
             int occ = 0;
-            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, mk_kernel(), 64, lds));
+            HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64, lds));
             if (occ < 1) occ = 1;
             const int64_t todo = list_n < 0 ? n : list_n;
             const int64_t waves = std::min<int64_t>((int64_t)ctx->num_cu * occ, std::max<int64_t>(todo, 1));
@@ -991,13 +1005,14 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
             P.fail_list = fail_list.p;
             P.fail_count = ctx->counters.p + 4;
             P.profile = verbose() ? 1 : 0;
-            // the first pass certifies parallel moment sums; re-runs (list mode) use the serial chains
-            P.exact_moments = (list_n >= 0 || getenv("DMX_MK_EXACT")) ? 1 : 0;
+            // the first pass certifies parallel moment sums; re-runs of failed sources use the serial chains
+            P.exact_moments = (attempt > 0 || getenv("DMX_MK_EXACT")) ? 1 : 0;
+            P.src_work = d_work;
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
                 HIPCHK(dP.alloc(1));
                 HIPCHK(hipMemcpyAsync(dP.p, &P, sizeof(P), hipMemcpyHostToDevice, ctx->stream));
-                hipLaunchKernelGGL(mk_kernel(), dim3((unsigned)waves), dim3(64), lds, ctx->stream,
+                hipLaunchKernelGGL(kern, dim3((unsigned)waves), dim3(64), lds, ctx->stream,
                                    (const MakeGraphParams*)dP.p);
                 HIPCHK(hipGetLastError());
             }
@@ -1042,7 +1057,7 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         }
         if (pool_over) { mk_total_s += kernel_s; continue; }
         HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
-        if (n > 0) {
+        if (n > 0 && !only) {   // (a sample leaves the other nodes' run starts unset)
             hipLaunchKernelGGL(gridconn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, h.rows(),
                                pm->d_node_cell.p + node_begin, n, g->node_run_start.p, g->bin_nruns.p, g->pool.p,
                                g->gridconn.p);
@@ -1073,6 +1088,8 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         ctx->last_stats[0] = (long long)st[0];
         ctx->last_stats[1] = (long long)st[1];
         ctx->last_stats[2] = (long long)used;
+        ctx->last_stats[32] = (long long)st[2];   // sieve depth steps
+        ctx->last_stats[33] = (long long)st[3];   // 64-candidate chunks
         ctx->last_mk_s = mk_total_s + kernel_s;   // every pass counted (sample, overflow re-runs)
         g->nruns = (int64_t)used;
         VLOG("makegraph: kernels %.3f s, total %.3f s\n", kernel_s, now_s() - t_start);
@@ -1080,6 +1097,61 @@ int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, 
         return DMX_OK;
     }
     return fail(DMX_ERR_CAPACITY, "makegraph capacities exceeded after retries");
+}
+
+int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int64_t node_begin, int64_t node_end,
+                  dmx_graph** out) {
+    return makegraph_impl(ctx, pm, maxdist, boundary, node_begin, node_end, nullptr, nullptr, out);
+}
+
+// Cost model of one source's sweep, in units of one depth step: a source pays a fixed setup, one unit per
+// sieve depth step (collectgarbage + visit ranges) and kMkChunkCost per 64-candidate chunk (tests, bins,
+// moments, run tracking).  Fitted to per-strip kernel times on MI355X.
+static const double kMkSourceCost = 0.0, kMkChunkCost = 0.7;
+
+int dmx_makegraph_balance(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int32_t world, int64_t stride,
+                          int64_t* bounds) {
+    if (!ctx || !pm || !bounds || world < 1 || stride < 1) return fail(DMX_ERR_ARG, "bad arguments");
+    HIPCHK(hipSetDevice(ctx->device));
+    PointMapHost& h = *pm->host;
+    if (!h.lines_blocked()) h.block_lines();
+    if (boundary) { h.keep_edges_only(); pm->version++; }
+    int rc = upload_pointmap(ctx, pm);
+    if (rc) return rc;
+    const int64_t N = pm->nnodes;
+    bounds[0] = 0;
+    for (int r = 1; r <= world; r++) bounds[r] = N;
+    if (N == 0 || world == 1) return DMX_OK;
+    // sample j stands for the nodes [j*stride, (j+1)*stride): its middle node is swept
+    const int64_t ns = (N + stride - 1) / stride;
+    std::vector<int64_t> sample((size_t)ns);
+    for (int64_t j = 0; j < ns; j++) sample[j] = std::min<int64_t>(N - 1, j * stride + stride / 2);
+    DevBuf<uint32_t> d_work;
+    HIPCHK(d_work.alloc((size_t)N * 2));
+    dmx_graph* g = nullptr;
+    rc = makegraph_impl(ctx, pm, maxdist, 0, 0, N, &sample, d_work.p, &g);   // boundary already applied
+    if (rc) return rc;
+    dmx_graph_free(g);
+    std::vector<uint32_t> w2((size_t)N * 2);
+    HIPCHK(copy_sync(ctx->stream, w2.data(), d_work.p, (size_t)N * 2 * 4, hipMemcpyDeviceToHost));
+    // cumulative modelled cost at the interval ends; bounds at equal shares (same doubles on every rank)
+    std::vector<double> cum((size_t)ns + 1, 0.0);
+    for (int64_t j = 0; j < ns; j++) {
+        const int64_t v = sample[j];
+        const double w = kMkSourceCost + (double)w2[2 * v] + kMkChunkCost * (double)w2[2 * v + 1];
+        const int64_t cnt = std::min<int64_t>(N, (j + 1) * stride) - j * stride;
+        cum[j + 1] = cum[j] + w * (double)cnt;
+    }
+    int64_t j = 0;
+    for (int r = 1; r < world; r++) {
+        const double target = cum[ns] * (double)r / (double)world;
+        while (j < ns - 1 && cum[j + 1] < target) j++;
+        const double per = (cum[j + 1] - cum[j]) / (double)(std::min<int64_t>(N, (j + 1) * stride) - j * stride);
+        int64_t b = j * stride + (per > 0.0 ? (int64_t)((target - cum[j]) / per) : 0);
+        b = std::max<int64_t>(b, bounds[r - 1]);
+        bounds[r] = std::min<int64_t>(b, N);
+    }
+    return DMX_OK;
 }
 
 int dmx_graph_free(dmx_graph* g) {
@@ -2311,6 +2383,7 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
     HIPCHK(hipSetDevice(ctx->device));
+    CANCEL_POINT(ctx);   // a cancel requested while nothing ran stops this call (dmx.h)
     PointMapHost& h = *g->pm->host;
     const int cols = h.cols(), rows = h.rows();
     const int64_t C = (int64_t)cols * rows, N = g->nnodes;
@@ -2532,6 +2605,7 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
     HIPCHK(hipSetDevice(ctx->device));
+    CANCEL_POINT(ctx);   // (before any output is written)
     PointMapHost& h = *g->pm->host;
     const int cols = h.cols(), rows = h.rows();
     const int64_t C = (int64_t)cols * rows, N = g->nnodes;

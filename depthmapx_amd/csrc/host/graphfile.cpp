@@ -14,18 +14,18 @@ struct Rd {
     bool ok = true;
     template <typename T> T get() {
         T v{};
-        if (o + sizeof(T) > n) { ok = false; o = n; return v; }
+        if (sizeof(T) > n - o) { ok = false; o = n; return v; }
         std::memcpy(&v, p + o, sizeof(T));
         o += sizeof(T);
         return v;
     }
-    void skip(size_t k) {
-        if (o + k > n) { ok = false; o = n; return; }
+    void skip(size_t k) {   // (o <= n always: the tests cannot overflow)
+        if (k > n - o) { ok = false; o = n; return; }
         o += k;
     }
     std::string str() {   // dXstring::readString: u32 length + bytes
         const uint32_t len = get<uint32_t>();
-        if (!ok || o + len > n) { ok = false; o = n; return std::string(); }
+        if (!ok || len > n - o) { ok = false; o = n; return std::string(); }
         std::string s(reinterpret_cast<const char*>(p + o), len);
         o += len;
         return s;
@@ -260,9 +260,11 @@ int read_graphfile(const uint8_t* buf, size_t size, GraphFile& gf, std::string& 
     }
     if (r.eof() && type != 'l' && type != 'p') { gf.state = state; return 0; }
     if (type == 'v') {   // skipVirtualMem (mgraph.cpp:2760-2774)
-        int32_t nodes = r.get<int32_t>();
+        const int32_t nodes = r.get<int32_t>();
+        if (nodes < 0) r.ok = false;
         for (int64_t i = 0; i < (int64_t)nodes * 2 && r.ok; i++) {
             const int32_t c = r.get<int32_t>();
+            if (c < 0) { r.ok = false; break; }
             r.skip((size_t)c * 4);
         }
         if (!r.ok || r.eof()) { err = "damaged virtual graph section"; return -1; }

@@ -19,7 +19,10 @@
 //   All geometry is IEEE double in the reference's operation order (-ffp-contract=off).
 #include "common.hpp"
 
+
 namespace dmx {
+
+constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
 
 struct MakeGraphParams {
     int cols, rows;
@@ -59,6 +62,7 @@ struct MakeGraphParams {
     int* fail_count;
     int profile;               // 1: accumulate per-phase clocks into stats[8..13]
     int exact_moments;         // 1: the reference's serial FP64 moment chains; 0: certified parallel sums
+    uint32_t* src_work;        // optional [n][2]: depth steps and candidate chunks of each published source
 };
 
 // phase clocks (profile builds of a run only; wave-uniform scalar reads)
@@ -261,7 +265,13 @@ struct Lds {
 
 // WPE: waves per SIMD the register allocation targets; PROF: per-phase clocks (DMX_VERBOSE builds of
 // a run) -- a template flag so that the 8 clock counters cost no registers otherwise
-template <int WPE, bool PROF>
+// FIXED: the first pass's LDS capacities (gcap 16, bcap 32) as constants, so the LDS arrays sit at constant
+// offsets instead of holding 13 SGPRs (the kernel's time follows its register allocation: spills go to
+// scratch memory on the depth loop's critical path); re-runs with larger capacities take FIXED = false.
+// COUNT: count each source's depth steps and candidate chunks (the cost sample of dmx_makegraph_balance;
+// two more live counters cost the main pass ~10 % through the register allocation, so only the sample
+// pass carries them).
+template <int WPE, bool PROF, bool FIXED, bool COUNT>
 // The parameters are read through a pointer to device memory rather than passed by value: the compiler
 // then reloads cold fields with scalar loads instead of keeping ~50 pointers live in SGPRs and
 // spilling them (VGA tile kernel: 210 -> 105 SGPR spills).
@@ -269,7 +279,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const MakeGraphParams& P = *PP;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
-    const int gcap = P.gcap, bcap = P.bcap, D = P.dmax;
+    const int gcap = FIXED ? MK_GCAP0 : P.gcap, bcap = FIXED ? MK_BCAP0 : P.bcap, D = P.dmax;
     Lds L;
     {
         unsigned char* p = smem;
@@ -343,6 +353,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         int mcnt = 0;                // this lane's summand count
         int nsize = 0;
         unsigned long long examined = 0;
+        uint32_t nsteps = 0, nchunks = 0;   // sieve depth steps / 64-candidate chunks (the source's work)
         int bpos = 0;        // next free run slot in stageB
         bool failed = false;
 
@@ -551,6 +562,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 // loop condition: sieve.hasGaps() (pointdata.cpp:1454)
                 if (ng == 0) break;
                 depth++;
+                if (COUNT) nsteps++;
                 // ---------------- sieve2 for this depth (pointdata.cpp:1512-1565)
                 // per-gap visit ranges with the monotone firstind rule
                 int carryF = 0, carryT = 0;
@@ -610,6 +622,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 bool hasgaps = false;
                 int gcur = 0; // per-lane gap pointer (t increases monotonically)
                 for (int t0 = 0; t0 < T; t0 += 64) {
+                    if (COUNT) nchunks++;
                     int t = t0 + lane;
                     bool valid = t < T;
                     int ind = 0, hx = 0, hy = 0;
@@ -975,6 +988,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         if (lane == 0) {
             atomicAdd(&P.stats[0], examined);
             atomicAdd(&P.stats[1], (unsigned long long)nsize);
+            if (COUNT) {
+                atomicAdd(&P.stats[2], (unsigned long long)nsteps);
+                atomicAdd(&P.stats[3], (unsigned long long)nchunks);
+                P.src_work[2 * k] = nsteps;
+                P.src_work[2 * k + 1] = nchunks;
+            }
             if (PROF)
                 for (int i = 0; i < 8; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
             P.attrs[k * 3 + 0] = (float)nsize;

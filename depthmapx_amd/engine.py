@@ -97,7 +97,7 @@ class Context:
                 "vga_cells_reached", "vga_sources", "vga_fail_cells", "vga_fail_runs", "vga_hbm_bitmaps",
                 "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",
                 "vga_hard_cells", "vga_hard_certain", "vga_topdown_cycles", "vga_b_tiles", "vga_b_cells", "vga_tt_tiles", "vga_c_busy", "vga_c_scan", "vga_c_spec", "vga_n_spec", "vga_tt_pruned", "vga_b_row_cycles", "vga_b_cell_tiles",
-                "vga_b_cell_cycles", "vga_b_ext_cells"]
+                "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks"]
         d = {k: int(v) for k, v in zip(keys, out)}
         lv = d.pop("vga_levels")
         d["vga_bottom_up_levels"], d["vga_top_down_levels"] = lv & 0xFFFFFFFF, lv >> 32
@@ -192,6 +192,14 @@ class PointMap:
         N.check(N.lib().dmx_makegraph(ctx.h, self.h, float(maxdist), int(bool(boundarygraph)), int(node_begin),
                                       int(node_end), ctypes.byref(h)))
         return Graph(h, ctx, self)
+
+    def shard_bounds(self, ctx, world, stride=256, boundarygraph=False, maxdist=-1.0):
+        """Contiguous node ranges of equal modelled makeGraph cost for `world` ranks (dmx_makegraph_balance):
+        a list of world + 1 bounds, the same on every rank."""
+        b = np.zeros(int(world) + 1, dtype=np.int64)
+        N.check(N.lib().dmx_makegraph_balance(ctx.h, self.h, float(maxdist), int(bool(boundarygraph)), int(world),
+                                              int(stride), N.ptr(b)))
+        return [int(v) for v in b]
 
     def assemble(self, ctx, blob_ptrs, blob_sizes):
         """Whole-map graph from shard blobs living in device memory (e.g. all-gathered torch tensors)."""

@@ -67,7 +67,8 @@ typedef int32_t (*dmx_progress_fn)(void* user, int32_t phase, int64_t done, int6
 int dmx_ctx_set_progress(dmx_ctx* ctx, dmx_progress_fn fn, void* user, double interval_s);
 /* Request cancellation of the operation running on ctx (callable from any thread).  The request is
  * consumed by the operation that observes it; one made while no operation runs cancels the next
- * makegraph / VGA-global / step-depth call at its first poll. */
+ * makegraph, VGA-global or step-depth (metric, angular, visual) call at its first poll -- before that
+ * call writes any output.  VGA local / metric / angular do not poll (a pending request waits). */
 int dmx_ctx_cancel(dmx_ctx* ctx);
 /* Wall time of the kernels of the last makegraph / vga call, measured with HIP events on the
  * context stream (seconds); kernel_ms receives per-kernel averages. */
@@ -124,6 +125,14 @@ int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, i
  * order (node_end < 0: all) -- a sub-range is one rank's shard.  maxdist = -1: unrestricted. */
 int dmx_makegraph(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int64_t node_begin,
                   int64_t node_end, dmx_graph** out);
+/* Shard bounds for `world` ranks (no reference counterpart: the reference builds the graph on one
+ * host, pointdata.cpp:1246-1341).  Sweeps every stride-th source (the middle node of each run of
+ * `stride` nodes), models each source's cost from its sieve depth steps and candidate chunks, and writes
+ * bounds[0..world] (bounds[0] = 0, bounds[world] = nodes) so that the contiguous ranges
+ * [bounds[r], bounds[r+1]) carry equal modelled makeGraph cost.  The counts are deterministic: every rank
+ * computes the same bounds without communicating.  boundary as for dmx_makegraph (applied to pm here). */
+int dmx_makegraph_balance(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int boundary, int32_t world,
+                          int64_t stride, int64_t* bounds);
 int dmx_graph_free(dmx_graph* g);
 /* nodes in the whole map, first/last node built here, runs held. */
 int dmx_graph_info(const dmx_graph* g, int64_t* nnodes, int64_t* node_begin, int64_t* node_end, int64_t* nruns);

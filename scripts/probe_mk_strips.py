@@ -41,10 +41,12 @@ def main():
         st = ctx.last_stats()
         g.close()
         res.append({"strip": s, "x0": s * a.width, "nodes": e - b, "s": t, "us_per_src": 1e6 * t / max(e - b, 1),
-                    "sieve_cells": st["mk_cells_examined"], "pairs": st["mk_visible_pairs"], "runs": st["mk_runs"]})
+                    "sieve_cells": st["mk_cells_examined"], "pairs": st["mk_visible_pairs"], "runs": st["mk_runs"],
+                    "steps": st["mk_depth_steps"], "chunks": st["mk_chunks"]})
         r = res[-1]
-        print("strip %3d x %4d..%4d  %7d src  %.3f s  %.2f us/src  sieve %.3g  pairs %.3g  runs %.3g" % (
-            s, r["x0"], r["x0"] + a.width, r["nodes"], t, r["us_per_src"], r["sieve_cells"], r["pairs"], r["runs"]),
+        print("strip %3d x %4d..%4d  %7d src  %.3f s  %.2f us/src  sieve %.3g  pairs %.3g  runs %.3g  steps %.3g  "
+              "chunks %.3g" % (s, r["x0"], r["x0"] + a.width, r["nodes"], t, r["us_per_src"], r["sieve_cells"],
+                               r["pairs"], r["runs"], r["steps"], r["chunks"]),
             flush=True)
     print(json.dumps({"config": a.config, "N": N, "rows": rows, "strips": res}))
 

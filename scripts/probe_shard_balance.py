@@ -18,6 +18,8 @@ from depthmapx_amd.sharded import shard_range  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--balanced", action="store_true", help="cost-balanced bounds (PointMap.shard_bounds)")
+    ap.add_argument("--stride", type=int, default=256)
     a = ap.parse_args()
     if a.config == 5:
         W, occ, lmin, lmax = 1999, 5000, 0.0025, 0.01
@@ -33,8 +35,15 @@ def main():
     res = {"config": a.config, "N": N, "whole_s": whole, "worlds": {}}
     for world in (2, 4, 8):
         ts = []
+        if a.balanced:
+            import time
+            t0 = time.perf_counter()
+            bounds = pm.shard_bounds(ctx, world, stride=a.stride)
+            bal_s = time.perf_counter() - t0
+            bal_k = ctx.last_timing()[0]
+            print("W=%d balanced bounds %s (%.3f s wall, %.3f s kernels)" % (world, bounds, bal_s, bal_k), flush=True)
         for r in range(world):
-            b, e = shard_range(N, r, world)
+            b, e = (bounds[r], bounds[r + 1]) if a.balanced else shard_range(N, r, world)
             s = pm.make_graph(ctx, node_begin=b, node_end=e)
             ts.append(ctx.last_timing()[0])
             s.close()

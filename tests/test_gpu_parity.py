@@ -156,6 +156,30 @@ def test_shards_assemble_to_whole_graph(ctx):
     assert (o[:100] == -1).all() and (o[900:] == -1).all()
 
 
+@pytest.mark.parametrize("stride", [1, 7, 64])
+def test_balanced_shard_bounds_assemble_to_whole_graph(ctx, stride):
+    """dmx_makegraph_balance: bounds cover [0, N) in order, repeat exactly (every rank computes them on
+    its own), and the shards they cut reassemble to the one-shot graph."""
+    import torch
+    meta, A = load_case("gallery")
+    pm = _map(meta)
+    n = meta["nodes"]
+    b = pm.shard_bounds(ctx, 4, stride=stride)
+    assert b[0] == 0 and b[-1] == n and all(x <= y for x, y in zip(b, b[1:]))
+    assert pm.shard_bounds(ctx, 4, stride=stride) == b
+    assert pm.shard_bounds(ctx, 1, stride=stride) == [0, n]
+    blobs = []
+    for i in range(4):
+        s = pm.make_graph(ctx, node_begin=b[i], node_end=b[i + 1])
+        t = torch.empty(s.blob_size(), dtype=torch.uint8, device="cuda:0")
+        s.write_blob_device(t.data_ptr(), t.numel())
+        blobs.append(t)
+        s.close()
+    torch.cuda.synchronize()
+    g = pm.assemble(ctx, [t.data_ptr() for t in blobs], [t.numel() for t in blobs])
+    _assert_graph_equal(g.copy(), A, True)
+
+
 @pytest.mark.parametrize("kernel", ["v1", "topdown", "do"])
 def test_vga_kernels_agree(ctx, kernel, monkeypatch):
     """The tile-resolved BFS (default), the direction-optimising BFS, its top-down-only mode and

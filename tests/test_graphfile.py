@@ -141,3 +141,19 @@ def test_graph_roundtrip_rejects_legacy_and_garbage(tmp_path):
     bad = tmp_path / "bad.graph"
     bad.write_bytes(b"grf" + (440).to_bytes(4, "little") + b"\x00\x00")
     assert lib.dmx_graphfile_read(str(bad).encode(), ctypes.byref(h)) < 0
+
+
+@pytest.mark.parametrize("nodes,count", [(-1, 0), (1, -1), (1, -(1 << 30)), (2, 1 << 30)])
+def test_graph_virtual_section_bad_counts_are_rejected(tmp_path, nodes, count):
+    """skipVirtualMem (mgraph.cpp:2760-2774) with a negative node count, a negative per-node count or a
+    count past the end of the file: rejected as damaged, never a backwards or wrapped seek."""
+    import ctypes
+    import struct
+    from depthmapx_amd import _native as N
+    lib = N.lib()
+    body = b"grf" + struct.pack("<iii", 440, 0, 0) + b"\x00\x00" + b"v" + struct.pack("<ii", nodes, count)
+    bad = tmp_path / "virtual.graph"
+    bad.write_bytes(body + b"\x00" * 64)
+    h = ctypes.c_void_p()
+    assert lib.dmx_graphfile_read(str(bad).encode(), ctypes.byref(h)) == -1   # DMX_ERR_ARG: damaged
+    assert b"virtual graph" in lib.dmx_last_error()

@@ -84,3 +84,32 @@ def test_pending_cancel_stops_next_call_once(ctx):
     assert ei.value.status == -7
     g = pm.make_graph(ctx)          # the request was consumed
     assert g.info()["nruns"] == meta["runs"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["metric", "angular", "visual"])
+def test_pending_cancel_stops_next_stepdepth_once(ctx, kind):
+    """A cancel made while nothing runs is consumed by the next step-depth call of every type (dmx.h),
+    before it writes its output, and does not linger to abort a later call."""
+    meta, A = load_case("syn32")
+    pm = _map(meta)
+    g = pm.make_graph(ctx)
+    sel = A["stepdepth_sel"]
+    cells = (sel >> 16) * meta["rows"] + (sel & 0xFFFF)
+    fn = {"metric": g.metric_step_depth, "angular": g.angular_step_depth, "visual": g.visual_step_depth}[kind]
+
+    def run(c):
+        return fn(cells=c)
+    ref = run(cells)
+    ctx.cancel()
+    with pytest.raises(N.DmxError) as ei:
+        run(cells)
+    assert ei.value.status == -7
+    np.testing.assert_array_equal(run(cells).view(np.uint32), ref.view(np.uint32))
+
+
+def test_progress_interval_contract():
+    """interval_s <= 0 means the default 0.5 s (dmx.h); only NaN is refused.  No GPU needed: the context
+    is never created, the argument check runs first."""
+    lib = N.lib()
+    assert lib.dmx_ctx_set_progress(None, N.PROGRESS_FN(0), None, -1.0) == -1   # NULL context
