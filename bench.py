@@ -4,8 +4,10 @@ W x W open-plan grid with 50 random occluders (BASELINE.json metric; SURVEY.md s
 
 One step = the whole hot path for every filled cell of the grid:
   makeGraph (sparkGraph2) -> VGA global BFS + measures (VGAVisualGlobal::run) for every source.
-Multi-GPU (one process per GPU, RCCL): sources are split into contiguous x-major ranges.  The VGA
-BFS of any source walks the whole graph, so every rank needs all of it:
+Multi-GPU (one process per GPU, RCCL): makeGraph sources are split into contiguous x-major ranges of
+equal modelled cost (--balance cost: PointMap.shard_bounds, a sampled sweep every rank runs alike; the
+time is reported as graph_exchange.balance_s).  The VGA BFS of any source walks the whole graph, so every
+rank needs all of it:
   --mk-mode shard:     each rank builds its source range, the run-length shards are all-gathered
                        over RCCL and assembled (bytes ~ 8 B/run: 574 MB at 256^2, 36 GB at 1000^2);
   --mk-mode replicate: every rank builds the whole graph (no data-path collective);
@@ -225,6 +227,8 @@ def main():
     ap.add_argument("--grid", type=int, default=None, help="W: region [0,W]^2 at spacing 1 -> (W+1)^2 cells")
     ap.add_argument("--occluders", type=int, default=50)
     ap.add_argument("--mk-mode", choices=["auto", "shard", "replicate"], default="auto")
+    ap.add_argument("--balance", choices=["cost", "even"], default="cost",
+                    help="makeGraph shard bounds: equal modelled cost (PointMap.shard_bounds) or equal node counts")
     ap.add_argument("--prep-mode", choices=["shard", "replicate"], default="shard",
                     help="N>1: split the VGA pre-passes by node range (partials all-reduced) or repeat them")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="unused (the CPU sample is fixed: S=200 / S=20)")
@@ -284,7 +288,8 @@ def main():
     assert pm.make_points(*fill)
     info = pm.info()
     N = info["filled"]
-    b, e = shard_range(N, rank, world)          # makeGraph sources of this rank
+    shard_be = list(shard_range(N, rank, world))   # [b, e): makeGraph sources of this rank (re-cut by cost each step)
+    bal_stride = max(1, N // 4096)              # ~4096 sampled sources: one wave each, one round of the GPU
     vnodes = vga_nodes(N, rank, world) if world > 1 else None   # VGA sources of this rank
     workload = "synthetic-%d/%d-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + VGA -vm visibility -vg -vr n" % (
         W, args.occluders)
@@ -296,13 +301,22 @@ def main():
 
     out_full = None if stepdepth else torch.full((N, 7), -1.0, dtype=torch.float32, device=dev)
     sd_out = [None]
-    kt = {"makegraph_s": 0.0, "vga_s": 0.0, "n": 0, "exchange_s": 0.0, "allgather_s": 0.0, "xbytes": 0}
+    kt = {"makegraph_s": 0.0, "vga_s": 0.0, "n": 0, "exchange_s": 0.0, "allgather_s": 0.0, "xbytes": 0,
+          "balance_s": 0.0}
     stats = {}
 
     def step(record):
-        # 1. makeGraph: this rank's sources (shard) or all of them (replicate)
+        # 1. makeGraph: this rank's sources (shard) or all of them (replicate).  Sharded over several ranks,
+        #    the contiguous ranges are cut at equal modelled cost (dmx_makegraph_balance: a sampled sweep,
+        #    deterministic, so every rank cuts the same bounds without a collective)
         if mk_mode == "shard":
-            shard = pm.make_graph(ctx, node_begin=b, node_end=e)
+            if world > 1 and args.balance == "cost":
+                bounds = pm.shard_bounds(ctx, world, stride=bal_stride)
+                shard_be[:] = bounds[rank:rank + 2]
+                if record:
+                    kt["balance_s"] += ctx.last_timing()[0]
+                    kt["bounds"] = bounds
+            shard = pm.make_graph(ctx, node_begin=shard_be[0], node_end=shard_be[1])
         else:
             shard = pm.make_graph(ctx)
         t_mk = ctx.last_timing()[0]
@@ -337,7 +351,7 @@ def main():
         #    the O(runs) pre-passes are split by contiguous node range, partials all-reduced
         if world > 1:
             if args.prep_mode == "shard":
-                g.set_prep_shard(b, e, prep_allreduce(dist, dev))
+                g.set_prep_shard(shard_be[0], shard_be[1], prep_allreduce(dist, dev))
             g.vga_visual_global_device_list(out_full.data_ptr(), vnodes)
         else:
             g.vga_visual_global_device(out_full.data_ptr())
@@ -365,7 +379,8 @@ def main():
         progress("warm-up step %d/%d" % (w + 1, args.warmup))
         if w == 0 and mk_auto is not None:
             mk_mode, dec = choose_mk_mode(dist, dev, world, mk_auto["mk_shard_s"], mk_auto["blob_s"] +
-                                          mk_auto["allgather_s"] + mk_auto["assemble_s"], (e - b) / max(N, 1))
+                                          mk_auto["allgather_s"] + mk_auto["assemble_s"],
+                                          (shard_be[1] - shard_be[0]) / max(N, 1))
             mk_auto.update(dec)
             mk_auto["chosen"] = mk_mode
     torch.cuda.synchronize()
@@ -446,7 +461,7 @@ def main():
         # issue-rate roofline (VALU) for the two hot kernels, and makeGraph's FP64 rate
         issue = {}
         for kname in ("makegraph_kernel", "vga_tile_kernel", "stepdepth_kernel"):
-            kp = pmc.get(kname)   # (not `e`: b, e is this rank's makeGraph shard, used below)
+            kp = pmc.get(kname)
             if kp and "valu_active_frac" in kp:
                 issue[kname] = {"valu_busy_frac": kp["valu_active_frac"], "valu_issue_frac": kp.get("valu_issue_frac"),
                                 "wave_cycles_split": kp.get("wave_cycles_split"), "clock_ghz": kp.get("clock_ghz"),
@@ -478,7 +493,7 @@ def main():
                        "parallelism": "source-shard x%d (makeGraph %s, VGA prep %s)" % (
                            world, mk_mode, args.prep_mode if world > 1 else "local")},
             "kernels": {"makegraph_s": mk_s, "vga_s": vga_s,
-                        "makegraph_cells_per_s": (N if mk_mode == "replicate" or world == 1 else e - b) / mk_s
+                        "makegraph_cells_per_s": (N if mk_mode == "replicate" or world == 1 else shard_be[1] - shard_be[0]) / mk_s
                         if mk_s else None,
                         "visible_pairs": stats.get("mk_visible_pairs"),
                         "vga_kernel": stats.get("vga_kernel"),
@@ -494,7 +509,8 @@ def main():
         if kt["exchange_s"] or mk_auto:
             rec["kernels"]["graph_exchange"] = {
                 "s_per_step": kt["exchange_s"] / max(kt["n"], 1), "allgather_s": kt["allgather_s"] / max(kt["n"], 1),
-                "bytes": kt["xbytes"], "device_peak_bytes": kt.get("xpeak"), "auto": mk_auto}
+                "bytes": kt["xbytes"], "device_peak_bytes": kt.get("xpeak"), "auto": mk_auto,
+                "balance": args.balance, "balance_s": kt["balance_s"] / max(kt["n"], 1), "bounds": kt.get("bounds")}
         if stepdepth:
             rec["metric"] = "grid cells/sec for VISPREP makeGraph + metric step depth on N×N grid"
             kk = rec["kernels"]

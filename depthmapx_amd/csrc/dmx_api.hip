@@ -430,7 +430,7 @@ size_t makegraph_lds(int gcap, int bcap, int D) {
     b += 4 * 32 * 3 + 4 * 32;                        // binc, bfar, bnr, misc
     b += 16 * (size_t)bcap;                          // bsorted
     b += 4 * (size_t)gcap + 8 * (size_t)gcap + 4 * (size_t)bcap + 4 * ((size_t)gcap + 4);
-    b += 4 * ((size_t)D + 4);   // open-run state per row (the run counters live in HBM scratch)
+    b += 4 * (size_t)std::min(D + 4, MK_OPEN_LDS);   // open-run state of the near rows (makegraph.hip)
     return (b + 15) & ~(size_t)15;
 }
 
@@ -839,20 +839,26 @@ int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, i
     return DMX_OK;
 }
 
-// makeGraph kernel variant: VGPR budget (waves per SIMD) chosen at launch (DMX_MK_WPE, default 5).
-// The kernel is latency-bound (one wave walks one source's sieve depth by depth), so waves beat
-// registers: at 1000^2, 3 waves/SIMD 6.9 s, 4: 5.7 s, 5: 5.3 s (96 VGPRs, some spills), 6: 5.4 s.
-// fixed: the first-pass LDS capacities compiled in; count: the cost-sample counters (makegraph.hip).
+// makeGraph kernel variants (makegraph.hip).  VGPR budget: 5 waves per SIMD.  The kernel is latency-bound
+// (one wave walks one source's sieve depth by depth), so waves beat registers: at 1000^2, 3 waves/SIMD
+// 6.9 s, 4: 5.4 s, 5: 4.9 s (96 VGPRs, some cold spills), 6: 5.4 s.  fixed: the first pass (LDS
+// capacities, certified moment sums and the maxdist test compiled in); count: the cost-sample counters.
 typedef void (*mk_kernel_t)(const MakeGraphParams*);
-static mk_kernel_t mk_kernel(bool fixed, bool count) {
-    const char* e = getenv("DMX_MK_WPE");
-    const int w = e ? atoi(e) : 5;
-    if (verbose()) return fixed ? makegraph_kernel<5, true, true, false> : makegraph_kernel<5, true, false, false>;
-    if (count) return fixed ? makegraph_kernel<5, false, true, true> : makegraph_kernel<5, false, false, true>;
-    if (w >= 6) return fixed ? makegraph_kernel<6, false, true, false> : makegraph_kernel<6, false, false, false>;
-    if (w == 4) return fixed ? makegraph_kernel<4, false, true, false> : makegraph_kernel<4, false, false, false>;
-    return fixed ? makegraph_kernel<5, false, true, false> : makegraph_kernel<5, false, false, false>;
+#define MKK(PROF, FIXED, COUNT, MAXD, FAR) makegraph_kernel<5, PROF, FIXED, COUNT, MAXD, FAR>
+static mk_kernel_t mk_kernel(bool fixed, bool count, bool maxd, bool far) {
+    if (verbose()) {   // per-phase clocks (maxdist runs take the generic kernel)
+        if (!fixed || maxd) return MKK(true, false, false, false, false);
+        return far ? MKK(true, true, false, false, true) : MKK(true, true, false, false, false);
+    }
+    if (count) {       // the cost sample of dmx_makegraph_balance
+        if (!fixed || maxd) return MKK(false, false, true, false, false);
+        return far ? MKK(false, true, true, false, true) : MKK(false, true, true, false, false);
+    }
+    if (!fixed) return MKK(false, false, false, false, false);
+    if (maxd) return far ? MKK(false, true, false, true, true) : MKK(false, true, false, true, false);
+    return far ? MKK(false, true, false, false, true) : MKK(false, true, false, false, false);
 }
+#undef MKK
 
 // makeGraph over [node_begin, node_end), or only over the listed nodes of that range (`only`: the cost
 // sample of dmx_makegraph_balance; the graph's other nodes stay unset).  d_work (optional, [n][2]) receives
@@ -892,7 +898,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
     // LDS gap / block lists: small lists keep the per-wave LDS near 12 KB at 1000^2 (13 waves per CU
     // instead of 10 with 64-entry lists: 8.27 s -> 6.6 s); longer block lists spill to HBM, longer gap
     // lists re-run the source with larger capacities
-    int gcap = 16, bcap = 32;
+    int gcap = MK_GCAP0, bcap = MK_BCAP0;
     int spill_cap = 4096;      // per-wave HBM blocks past bcap
     int64_t capB = 32 * (int64_t)D + 2048;
     if (const char* e = getenv("DMX_MK_GCAP")) gcap = std::max(2, atoi(e));   // test hooks for the retry path
@@ -921,6 +927,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
     bool sampling = !only && !getenv("DMX_MK_NOSAMPLE") &&
                     ((n >= 16 * kSample && big_pool) || (n >= kSample && getenv("DMX_MK_SAMPLE")));   // test hook
     double mk_total_s = 0.0;
+    int64_t reruns = 0;   // sources re-run after a first-pass capacity or certification failure
     for (int restart = 0; restart < 4; restart++) {
         // one full pass, then re-runs of only the sources that overflowed an LDS / staging capacity
         double kernel_s = 0.0;
@@ -943,7 +950,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         HIPCHK(hipMemsetAsync(ctx->stats.p, 0, 32 * sizeof(unsigned long long), ctx->stream));
         size_t lds0 = makegraph_lds(gcap, bcap, D);
         int occ0 = 0;
-        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, mk_kernel(false, d_work != nullptr), 64, lds0));
+        HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ0, mk_kernel(false, d_work != nullptr, false, false), 64, lds0));
         {
             const int64_t waves0 = std::min<int64_t>((int64_t)ctx->num_cu * std::max(occ0, 1), std::max<int64_t>(n, 1));
             const size_t stage0 = (size_t)waves0 * (capB * 16 + (3 * ((size_t)D + 1) + 4) * 4) * 4;   // headroom for retries
@@ -959,8 +966,10 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         for (int attempt = 0; attempt < 8; attempt++) {
             size_t lds = makegraph_lds(gcap, bcap, D);
             if (lds > 160 * 1024) return fail(DMX_ERR_CAPACITY, "makegraph LDS requirement exceeds 160 KiB");
-            const mk_kernel_t kern = mk_kernel(gcap == MK_GCAP0 && bcap == MK_BCAP0 && !getenv("DMX_MK_NOFIXED"),
-                                               d_work != nullptr);
+            const bool exact_pass = attempt > 0 || getenv("DMX_MK_EXACT");   // re-runs: the serial moment chains
+            const mk_kernel_t kern = mk_kernel(gcap == MK_GCAP0 && bcap == MK_BCAP0 && !exact_pass &&
+                                                   !getenv("DMX_MK_NOFIXED"),
+                                               d_work != nullptr, maxdist != -1.0, D + 4 > MK_OPEN_LDS);
             int occ = 0;
             HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 64, lds));
             if (occ < 1) occ = 1;
@@ -975,6 +984,10 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
             HIPCHK(pref.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
             HIPCHK(rcnt.alloc((size_t)waves * (3 * ((size_t)D + 1) + 4)));
             HIPCHK(hipMemsetAsync(rcnt.p, 0, (size_t)waves * (3 * ((size_t)D + 1) + 4) * 4, ctx->stream));
+            const int openh_n = std::max(0, D + 4 - MK_OPEN_LDS);
+            DevBuf<uint32_t> openh;
+            HIPCHK(openh.alloc(std::max<size_t>((size_t)waves * openh_n, 1)));
+            HIPCHK(hipMemsetAsync(openh.p, 0, std::max<size_t>((size_t)waves * openh_n, 1) * 4, ctx->stream));
             DevBuf<double2> bsp;
             DevBuf<int> bspf;
             HIPCHK(bsp.alloc((size_t)waves * 2 * spill_cap));
@@ -1006,8 +1019,9 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
             P.fail_count = ctx->counters.p + 4;
             P.profile = verbose() ? 1 : 0;
             // the first pass certifies parallel moment sums; re-runs of failed sources use the serial chains
-            P.exact_moments = (attempt > 0 || getenv("DMX_MK_EXACT")) ? 1 : 0;
+            P.exact_moments = exact_pass ? 1 : 0;
             P.src_work = d_work;
+            P.openh = openh.p; P.openh_n = openh_n;
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
                 HIPCHK(dP.alloc(1));
@@ -1036,6 +1050,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
                 break;
             }
             if (nfail == 0) break;
+            if (!sampling) reruns += nfail;
             if (err & KERR_GAP_CAPACITY) gcap *= 2;
             if (err & KERR_BLOCK_CAPACITY) spill_cap *= 4;
             if (err & KERR_STAGE_CAPACITY) capB *= 2;
@@ -1090,6 +1105,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         ctx->last_stats[2] = (long long)used;
         ctx->last_stats[32] = (long long)st[2];   // sieve depth steps
         ctx->last_stats[33] = (long long)st[3];   // 64-candidate chunks
+        ctx->last_stats[34] = (long long)reruns;
         ctx->last_mk_s = mk_total_s + kernel_s;   // every pass counted (sample, overflow re-runs)
         g->nruns = (int64_t)used;
         VLOG("makegraph: kernels %.3f s, total %.3f s\n", kernel_s, now_s() - t_start);

@@ -23,6 +23,10 @@
 namespace dmx {
 
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
+// open-run state of rows 0 .. MK_OPEN_LDS-1 lives in LDS, of farther rows (grids above ~1020 cells a
+// side) in per-wave scratch memory: rows past 1024 are reached only by sight lines longer than 1024
+// cells, and a full-length LDS array would cost a 2000^2 grid a quarter of its waves
+constexpr int MK_OPEN_LDS = 1024;
 
 struct MakeGraphParams {
     int cols, rows;
@@ -63,6 +67,8 @@ struct MakeGraphParams {
     int profile;               // 1: accumulate per-phase clocks into stats[8..13]
     int exact_moments;         // 1: the reference's serial FP64 moment chains; 0: certified parallel sums
     uint32_t* src_work;        // optional [n][2]: depth steps and candidate chunks of each published source
+    uint32_t* openh;           // per wave: open-run state of rows >= MK_OPEN_LDS (zeroed by the host, kept zero)
+    int openh_n;               // its length per wave: max(0, dmax + 4 - MK_OPEN_LDS)
 };
 
 // phase clocks (profile builds of a run only; wave-uniform scalar reads)
@@ -254,7 +260,7 @@ struct Lds {
     int* ga;          // [gcap] first visited ind per gap
     int2* gc;         // [gcap] centregap ind range per gap: ceil(fl(start*depth)), floor(fl(end*depth))
     int* gpre;        // [gcap+1] exclusive prefix of visited counts
-    uint32_t* openr;  // [dmax+2]
+    uint32_t* openr;  // [min(dmax + 4, MK_OPEN_LDS)]
     unsigned* binc;   // [32] node counts per bin
     unsigned* bfar;   // [32] far distance (float bits)
     int* bnr;         // [32] runs per bin
@@ -271,7 +277,9 @@ struct Lds {
 // COUNT: count each source's depth steps and candidate chunks (the cost sample of dmx_makegraph_balance;
 // two more live counters cost the main pass ~10 % through the register allocation, so only the sample
 // pass carries them).
-template <int WPE, bool PROF, bool FIXED, bool COUNT>
+// MAXD (FIXED kernels): maxdist != -1 (the maxdist test compiled in).  FAR (FIXED kernels): the grid has
+// rows past MK_OPEN_LDS (the scratch-memory branch of the open-run accessors compiled in).
+template <int WPE, bool PROF, bool FIXED, bool COUNT, bool MAXD, bool FAR>
 // The parameters are read through a pointer to device memory rather than passed by value: the compiler
 // then reloads cold fields with scalar loads instead of keeping ~50 pointers live in SGPRs and
 // spilling them (VGA tile kernel: 210 -> 105 SGPR spills).
@@ -280,6 +288,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int lane = lane_id();
     const int gcap = FIXED ? MK_GCAP0 : P.gcap, bcap = FIXED ? MK_BCAP0 : P.bcap, D = P.dmax;
+    // FIXED kernels run the first pass: certified moment sums, maxdist test only in the MAXD variant
+    const bool exact = FIXED ? false : (P.exact_moments != 0);
+    const bool hasmax = FIXED ? MAXD : (P.maxdist != -1.0);
     Lds L;
     {
         unsigned char* p = smem;
@@ -295,7 +306,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         L.ga = (int*)p; p += 4 * gcap;
         L.bflag = (int*)p; p += 4 * bcap;
         L.gpre = (int*)p; p += 4 * (gcap + 4);
-        L.openr = (uint32_t*)p; p += 4 * (D + 4);
+        L.openr = (uint32_t*)p; p += 4 * min(D + 4, MK_OPEN_LDS);
     }
     const int wave_global = blockIdx.x;
     unsigned long long* stA = P.stageA + (size_t)wave_global * P.capA;
@@ -323,7 +334,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
     // LDS state that persists across sources is reset here once
     const int AX = 3 * (D + 1); // rcnt[AX] counts the runs of the axis row (ind 0)
-    for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
+    uint32_t* openh = P.openh + (size_t)wave_global * P.openh_n;
+    const bool far_rows = FIXED ? FAR : (D + 4 > MK_OPEN_LDS);
+    auto ld_open = [&](int i) -> uint32_t {
+        return (!far_rows || i < MK_OPEN_LDS) ? L.openr[i] : ld_l2(&openh[i - MK_OPEN_LDS]);
+    };
+    auto st_open = [&](int i, uint32_t v) {
+        if (!far_rows || i < MK_OPEN_LDS) L.openr[i] = v;
+        else st_l2(&openh[i - MK_OPEN_LDS], v);
+    };
+    for (int i = lane; i < min(D + 4, MK_OPEN_LDS); i += 64) L.openr[i] = 0;
     __syncthreads();
     // 0 depth-0 + collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible: bins,
     // 4 visible: serial moments, 5 visible: run tracking, 6 octant flush + placement, 7 publish
@@ -648,9 +668,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             // sparkSieve2::testblock (sparksieve2.cpp:45-63)
                             const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
                             bool blocked = false;
-                            if (P.maxdist != -1.0 || nl > 0) {
+                            if (hasmax || nl > 0) {
                                 Seg ray = make_seg(Vec2{c0x, c0y}, Vec2{px, py});
-                                if (P.maxdist != -1.0 && ray.length() > P.maxdist) blocked = true;
+                                if (hasmax && ray.length() > P.maxdist) blocked = true;
                                 const double tol = sp * 1e-10;
                                 for (int k = 0; k < nl && !blocked; k++) {
                                     const double* sg = P.segs + 4 * (size_t)(off + k);
@@ -701,7 +721,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
                         }
                         MK_T(3);
-                        if (P.exact_moments) {
+                        if (exact) {
                             // serial sums in lane order = reference addlist order
                             // (the lane index is wave-uniform: v_readlane into SGPRs keeps the serial
                             // chain on two dependent FP64 adds per cell instead of an LDS round trip)
@@ -732,16 +752,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                                 int slot;
                                 if (ind == 0) { slot = 3; if (bin != q_axis) atomicOr(P.error, KERR_BIN_MISMATCH); }
                                 else { slot = bin - q_sector; if (slot < 0 || slot > 2) { atomicOr(P.error, KERR_BIN_MISMATCH); slot = 0; } }
-                                uint32_t o = L.openr[ind];
+                                uint32_t o = ld_open(ind);
                                 int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
                                 if ((o & 1u) && oslot == slot && ol == depth - 1) {
-                                    L.openr[ind] = pack_open(slot, os, depth);
+                                    st_open(ind, pack_open(slot, os, depth));
                                 } else {
                                     if (o & 1u) {   // the rank within (slot, row) is set after the octant
                                         emit = true;
                                         rec = pack_emit(oslot, ind, os, ol, 0);
                                     }
-                                    L.openr[ind] = pack_open(slot, depth, depth);
+                                    st_open(ind, pack_open(slot, depth, depth));
                                 }
                             }
                         }
@@ -795,6 +815,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     }
                     pf_ok = true;
                 }
+                // rows past MK_OPEN_LDS live in scratch memory: order this depth's stores before the next
+                // depth's loads of the same rows (other lanes); only sight lines past 1024 cells get here
+                if (depth >= MK_OPEN_LDS) __syncthreads();
                 wave_sync();
             }
             if (failed) break;
@@ -805,13 +828,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 bool emit = false;
                 unsigned long long rec = 0;
                 if (ind <= dq) {
-                    uint32_t o = L.openr[ind];
+                    uint32_t o = ld_open(ind);
                     if (o & 1u) {
                         int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
                         emit = true;
                         rec = pack_emit(oslot, ind, os, ol, 0);
                     }
-                    L.openr[ind] = 0;
+                    st_open(ind, 0u);
                 }
                 unsigned long long em = ballot(emit);
                 if (em) {
@@ -935,7 +958,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         }
         float m1f = 0.0f, m2f = 0.0f;
         if (!failed) {
-            if (P.exact_moments) {
+            if (exact) {
                 m1f = (float)tsum;
                 m2f = (float)tsum2;
             } else {
@@ -955,7 +978,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         if (failed) {
             if (lane == 0) P.fail_list[atomicAdd(P.fail_count, 1)] = node;
             // leave the wave in a clean LDS state and drop this source
-            for (int i = lane; i < D + 4; i += 64) L.openr[i] = 0;
+            for (int i = lane; i < D + 4; i += 64) st_open(i, 0u);
             for (int i = lane; i <= AX; i += 64) st_l2(&rcnt[i], 0u);
             __syncthreads();
             continue;

@@ -673,8 +673,14 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 // C0 tests their tile-visibility rows two cells at a time (16 row words a lane in
                 // flight): a frontier tile the cell sees completely is a certain hit (regular cell:
                 // in-set == out-set), no tile in view holding a frontier cell a certain miss.  C1
-                // scans the run lists of the undecided cells, 256 runs a step (4 loads a lane).
+                // scans the run lists of the undecided cells, CSTEP * 64 runs a step (CSTEP loads a lane).
                 constexpr int CCH = 16;
+                // runs a lane loads per scan step (1000^2: 4 -> 9.61 s, 8 -> 9.71 s, 16 -> 14.6 s: more loads
+                // in flight per round trip do not pay for the registers and the over-read past the first hit)
+#ifndef DMX_VGA_CSTEP
+#define DMX_VGA_CSTEP 4
+#endif
+                constexpr int CSTEP = DMX_VGA_CSTEP;
                 const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
                 for (;;) {
                     int it0 = 0;
@@ -746,23 +752,23 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             nr = P.tnruns[id];
                             int base = KH + P.bext;   // the first KH + bext runs were tested in phase B
                             const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
-                            for (; base < nr && !found; base += 256) {
-                                Run rr[4];
+                            for (; base < nr && !found; base += CSTEP * 64) {
+                                Run rr[CSTEP];
 #pragma unroll
-                                for (int k = 0; k < 4; k++) {
+                                for (int k = 0; k < CSTEP; k++) {
                                     const int r = base + k * 64 + lane;
                                     if (r < nr) rr[k] = P.scan_pool[rs + r];
                                     else rr[k].x0 = -1;
                                 }
-                                // the four tests are independent (no early-out between them), so
-                                // their LDS round trips overlap
-                                bool h4[4];
+                                // the tests are independent (no early-out between them), so their LDS
+                                // round trips overlap
+                                bool hk[CSTEP];
 #pragma unroll
-                                for (int k = 0; k < 4; k++) h4[k] = rr[k].x0 >= 0 && run_hits_fs(FV, rr[k]);
+                                for (int k = 0; k < CSTEP; k++) hk[k] = rr[k].x0 >= 0 && run_hits_fs(FV, rr[k]);
                                 int fpos = -1;
 #pragma unroll
-                                for (int k = 3; k >= 0; k--) {
-                                    const unsigned long long hmk = __ballot(h4[k]);
+                                for (int k = CSTEP - 1; k >= 0; k--) {
+                                    const unsigned long long hmk = __ballot(hk[k]);
                                     if (hmk) fpos = base + k * 64 + __ffsll((long long)hmk) - 1;
                                 }
                                 found = fpos >= 0;

@@ -1,9 +1,11 @@
 """Multi-GPU choreography for the hot path (one process per GPU, torch.distributed over RCCL).
 
-The units are source cells: rank r owns the contiguous x-major node range shard_range(N, r, W).
+The units are source cells: rank r owns a contiguous x-major node range -- cut at equal modelled cost by
+PointMap.shard_bounds (a source's sweep cost varies ~3x across a map: sources on open map edges see
+more cells), or at equal node counts by shard_range.
 Per step
-  1. makeGraph for the owned sources (no communication; its cost is about the same for every
-     source, so contiguous ranges balance);
+  1. makeGraph for the owned sources (no communication: the cost-balanced bounds come from a sampled
+     sweep whose counts are deterministic, so every rank cuts the same bounds on its own);
   2. all-gather of the run-length graph shards (ragged byte blobs, padded to the largest) so every
      rank holds the whole graph -- VGA BFS from any source can reach any node;
   3. VGA global for the rank's VGA sources (its preparation pre-passes split by contiguous node

@@ -29,7 +29,8 @@ def main():
         st = ctx.last_stats()
         g.close()
     print(json.dumps({"lib": os.environ.get("DMX_LIB", "default"), "config": a.config, "mk_s": ts,
-                      "pairs": st["mk_visible_pairs"], "runs": st["mk_runs"]}), flush=True)
+                      "pairs": st["mk_visible_pairs"], "runs": st["mk_runs"],
+                      "reruns": st["mk_reruns"]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -113,6 +113,35 @@ def test_random_occluders_match_oracle(ctx, seed):
     _assert_vga_close(g.vga_visual_global(), om.vga_global(threads=8))
 
 
+@pytest.mark.parametrize("shape", [(1300, 5), (6, 1300)])
+def test_far_rows_past_lds_match_oracle(ctx, shape):
+    """Sight lines longer than 1024 cells: the open-run state of rows past MK_OPEN_LDS lives in scratch
+    memory (makegraph.hip).  A long narrow corridor with a few occluders, both orientations (rows are
+    x-rows in the horizontal octants, y-rows in the vertical ones)."""
+    from pyoracle import OracleMap
+    W, H = shape
+    rng = np.random.default_rng(5)
+    lines = []
+    for _ in range(6):
+        x = rng.uniform(0.1, 0.9) * W
+        y = rng.uniform(0.1, 0.9) * H
+        lines.append([x, y, x + (0.7 if W > H else 0.3), y + (0.3 if W > H else 0.7)])
+    lines = np.array(lines, dtype=np.float64)
+    region = [0.0, 0.0, float(W), float(H)]
+    pm = dmx.PointMap(region, lines, 1.0)
+    om = OracleMap(region, 1.0, lines)
+    assert pm.make_points(0.5, 0.5) == om.fill(0.5, 0.5)
+    g = pm.make_graph(ctx)
+    om.make_graph(threads=8)
+    ref = om.graph()
+    got = g.copy(runs=True)
+    np.testing.assert_array_equal(got["bins"], ref["bins"])
+    np.testing.assert_array_equal(got["runs"], ref["runs"])
+    np.testing.assert_array_equal(got["attrs"].view(np.uint32), ref["attrs"].view(np.uint32))
+    assert int(np.abs(got["runs"][:, 0].astype(np.int64) - got["runs"][:, 2]).max()) > 1024 or \
+        int(np.abs(got["runs"][:, 1].astype(np.int64) - got["runs"][:, 3]).max()) > 1024
+
+
 def test_maxdist_and_radius_match_oracle(ctx):
     from pyoracle import OracleMap
     meta, _ = load_case("syn32")
