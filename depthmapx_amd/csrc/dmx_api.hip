@@ -262,6 +262,9 @@ struct dmx_graph {
     DevBuf<unsigned long long> tvis;   // tile-visibility rows (empty: not built / too large)
     DevBuf<unsigned long long> ftvis;  // full-visibility rows (every non-seed cell of the tile seen)
     DevBuf<unsigned long long> ttvis;  // tile-to-tile full visibility (AND of ftvis over regular cells)
+    DevBuf<unsigned long long> pmask;  // partial-tile masks (the cells of each partly seen tile a cell sees)
+    DevBuf<int64_t> poff;              // [Ct + 1] start of each cell's masks
+    DevBuf<uint16_t> ppre;             // [Ct][tvw] partial tiles of a cell before each row word
     int tvw = 0;
     DevBuf<unsigned long long> regular_tiles;
     // sharded VGA preparation (dmx_graph_set_prep_shard): the node scatters run over [prep_b, prep_e)
@@ -1602,6 +1605,60 @@ static int prepare_symmetry(dmx_graph* g) {
     return DMX_OK;
 }
 
+// Partial-tile masks for phase C's exact test (vga_tile.hip pmask_hit): counts from the full rows
+// (every rank after the rows' all-reduce), an exclusive scan into per-cell offsets, then the masks over
+// the rank's node range (summed over ranks: a cell's masks come from one node, so ranks never
+// overlap).  ~10 GB at 1000^2 (about 1,300 partial tiles a cell); skipped, with phase C scanning runs
+// instead, when that would take more than a quarter of the free memory.
+static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_t Ct) {
+    dmx_ctx* ctx = g->ctx;
+    hipStream_t s = ctx->stream;
+    DevBuf<int64_t> cnt, scratch;
+    HIPCHK(cnt.alloc(Ct));
+    HIPCHK(g->poff.alloc(Ct + 1));
+    HIPCHK(g->ppre.alloc((size_t)Ct * tvw));
+    HIPCHK(scratch.alloc(scan_scratch_size(Ct)));
+    hipLaunchKernelGGL(tile_pcount_kernel, dim3((unsigned)((Ct + 3) / 4)), dim3(256), 0, s, Ct, tvw, g->tvis.p, g->ftvis.p,
+                       cnt.p, g->ppre.p);
+    HIPCHK(hipGetLastError());
+    scan_excl(s, cnt.p, Ct, g->poff.p, scratch.p);
+    HIPCHK(hipGetLastError());
+    int64_t total = 0;
+    HIPCHK(copy_sync(s, &total, g->poff.p + Ct, 8, hipMemcpyDeviceToHost));
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    bool build = total > 0 && (size_t)total * 8 <= free_b / 4;
+    if (g->prep_fn) {
+        // the same decision on every rank (the masks are all-reduced)
+        DevBuf<int64_t> veto;
+        HIPCHK(veto.alloc(1));
+        const int64_t v = build ? 0 : 1;
+        HIPCHK(hipMemcpyAsync(veto.p, &v, 8, hipMemcpyHostToDevice, s));
+        if (int rc = prep_allreduce(g, veto.p, 1, DMX_I64)) return rc;
+        int64_t vs = 0;
+        HIPCHK(copy_sync(s, &vs, veto.p, 8, hipMemcpyDeviceToHost));
+        build = vs == 0;
+    }
+    if (!build) {
+        g->poff.reset();
+        g->ppre.reset();
+        return DMX_OK;
+    }
+    HIPCHK(g->pmask.alloc((size_t)total));
+    HIPCHK(hipMemsetAsync(g->pmask.p, 0, (size_t)total * 8, s));
+    int64_t pb, pe;
+    prep_range(g, pb, pe);
+    if (pe > pb) {
+        const int64_t nb = std::min<int64_t>(pe - pb, (int64_t)ctx->num_cu * 16);
+        hipLaunchKernelGGL(tile_pmask_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), 0, s, rows, tw, th,
+                           g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb, g->pool.p,
+                           g->tvis.p, g->ftvis.p, g->poff.p, g->pmask.p);
+        HIPCHK(hipGetLastError());
+    }
+    if (int rc = prep_allreduce(g, g->pmask.p, total, DMX_I64)) return rc;
+    return DMX_OK;
+}
+
 // Tile-ordered per-cell arrays, head runs and tile-common runs for vga_tile_kernel (O(runs)).
 static int prepare_tiles(dmx_graph* g) {
     if (g->tiles_ready) return DMX_OK;
@@ -1696,6 +1753,9 @@ static int prepare_tiles(dmx_graph* g) {
                                g->ftvis.p, g->tvis.p, g->ttvis.p, g->ttvis.p + (size_t)nt * tvw);
             HIPCHK(hipGetLastError());
         }
+        const char* pm_env = getenv("DMX_VGA_PMASK");
+        if (ftv_on && !(pm_env && atoi(pm_env) == 0))
+            if (int rc = prepare_pmask(g, rows, tw, th, tvw, Ct)) return rc;
         g->tvw = tvw;
     }
     HIPCHK(hipStreamSynchronize(s));
@@ -1714,9 +1774,9 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     HIPCHK(xg.alloc((size_t)blocks * 2 * nt));
     HIPCHK(queue.alloc((size_t)blocks * nt));
     HIPCHK(list.alloc((size_t)blocks * nt * 64 * 2));
-    DevBuf<uint16_t> hint;
+    DevBuf<uint32_t> hint;
     HIPCHK(hint.alloc((size_t)nt * 64));
-    HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 2, ctx->stream));
+    HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
     VgaTileParams P = Q;
     P.xg = xg.p;
     P.queue = queue.p;
@@ -1777,6 +1837,10 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.ftvis = (g->tvw && g->ftvis.p) ? g->ftvis.p : nullptr;
     Q.ttvis = (g->tvw && g->ttvis.p) ? g->ttvis.p : nullptr;
     Q.ttany = Q.ttvis ? g->ttvis.p + (size_t)tw * th * g->tvw : nullptr;
+    const char* pmk_env = getenv("DMX_VGA_PMASK");   // also a launch-time switch (the masks stay built)
+    Q.pmask = (Q.ftvis && g->pmask.p && !(pmk_env && atoi(pmk_env) == 0)) ? g->pmask.p : nullptr;
+    Q.poff = Q.pmask ? g->poff.p : nullptr;
+    Q.ppre = Q.pmask ? g->ppre.p : nullptr;
     Q.node_cell = g->pm->d_node_cell.p; Q.cell_node = g->pm->d_cell_node.p; Q.node_flags = g->pm->d_node_flags.p;
     Q.node_run_start = g->node_run_start.p; Q.node_nruns = g->node_nruns.p; Q.pool = g->pool.p;
     const bool corr = g->nspecial > 0;
@@ -1882,6 +1946,8 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[15] = (long long)st[15];                          // runs scanned in phase C
     ctx->last_stats[16] = (long long)st[1];                           // phase-C cells that hit
     ctx->last_stats[17] = (long long)st[14];                          // phase-C cells (regular)
+    ctx->last_stats[35] = (long long)st[30];                          // phase-C partial-tile masks read
+    ctx->last_stats[36] = (long long)st[31];                          // phase-C cells tested by masks
     if (nseeds > 0) return DMX_OK;
     if (!out_on_device && nsrc > 0)
         HIPCHK(copy_sync(ctx->stream, out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
@@ -2307,7 +2373,7 @@ static int stepdepth_batched(dmx_ctx* ctx, dmx_graph* g, const std::vector<uint8
         units += (nr[node] + SDB_UNIT - 1) / SDB_UNIT;
     }
     const unsigned amb_cap = 1u << 16, ent_cap = 1u << 22;
-    DevBuf<int32_t> d_ex, d_uown, d_win, d_ambid, d_touch, d_amb;
+    DevBuf<int32_t> d_ex, d_uown, d_win, d_ambid, d_touch, d_amb, d_ahead, d_enext;
     DevBuf<uint8_t> d_done;
     DevBuf<SdbExp> d_bq;
     DevBuf<unsigned long long> d_best;
@@ -2325,6 +2391,9 @@ static int stepdepth_batched(dmx_ctx* ctx, dmx_graph* g, const std::vector<uint8
     HIPCHK(d_touch.alloc(C));
     HIPCHK(d_amb.alloc(amb_cap));
     HIPCHK(d_ent.alloc(ent_cap));
+    HIPCHK(d_ahead.alloc(amb_cap));
+    HIPCHK(d_enext.alloc(ent_cap));
+    HIPCHK(hipMemsetAsync(d_ahead.p, 0xFF, (size_t)amb_cap * 4, s));
     HIPCHK(d_ctl.alloc(1));
     if (E) HIPCHK(hipMemcpyAsync(d_ex.p, ex.data(), E * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(d_done.p, 0, std::max<int64_t>(E, 1), s));
@@ -2347,7 +2416,7 @@ static int stepdepth_batched(dmx_ctx* ctx, dmx_graph* g, const std::vector<uint8
     P.key = d_key; P.mdist = d_mdist; P.cum = d_cum; P.lastpix = d_last;
     P.ex_cells = d_ex.p; P.ex_done = d_done.p; P.bq = d_bq.p; P.uown = d_uown.p;
     P.best = d_best.p; P.nnear = d_nnear.p; P.win = d_win.p; P.ambid = d_ambid.p; P.touch = d_touch.p;
-    P.amb = d_amb.p; P.ent = d_ent.p; P.ent_cap = ent_cap; P.amb_cap = amb_cap; P.ctl = d_ctl.p;
+    P.amb = d_amb.p; P.ent = d_ent.p; P.ahead = d_ahead.p; P.enext = d_enext.p; P.ent_cap = ent_cap; P.amb_cap = amb_cap; P.ctl = d_ctl.p;
     HIPCHK(hipStreamSynchronize(s));
     HIPCHK(hipEventRecord(ctx->ev0, s));
     hipLaunchKernelGGL(sdb_init_kernel, dim3((unsigned)((sel.size() + 255) / 256)), dim3(256), 0, s, P, d_sel,

@@ -429,6 +429,8 @@ struct SdbParams {
     int32_t* touch;               // [C] cells with a candidate this batch
     int32_t* amb;                 // [amb_cap] ambiguous cells
     int2* ent;                    // [ent_cap] (ambiguous index, batch index)
+    int32_t* ahead;               // [amb_cap] last entry of each ambiguous cell's relaxer list (-1: none)
+    int32_t* enext;               // [ent_cap] previous entry of the same ambiguous cell (-1: none)
     unsigned ent_cap, amb_cap;
     SdbCtl* ctl;
 };
@@ -566,8 +568,13 @@ __global__ void __launch_bounds__(SDB_THREADS) sdb_relax_kernel(SdbParams P) {
             } else {
                 const unsigned pos = sdb_wave_append(&C.nent, cand);
                 if (cand) {
-                    if (pos < P.ent_cap) P.ent[pos] = make_int2(P.ambid[c], b);
-                    else C.error = 1;
+                    if (pos < P.ent_cap) {
+                        const int a = P.ambid[c];
+                        P.ent[pos] = make_int2(a, b);
+                        P.enext[pos] = atomicExch(&P.ahead[a], (int)pos);   // per-cell list: O(entries) fold
+                    } else {
+                        C.error = 1;
+                    }
                 }
             }
         }
@@ -626,37 +633,62 @@ __global__ void sdb_apply_kernel(SdbParams P) {
 // Sequential fold of each ambiguous cell over all its batch relaxers in pop (key) order.
 __global__ void __launch_bounds__(SDB_THREADS) sdb_fold_kernel(SdbParams P) {
     __shared__ int lst[SDB_FOLD_CAP];
-    __shared__ int cnt;
     SdbCtl& C = *P.ctl;
     if (C.error) return;
-    const unsigned na = min(C.namb, P.amb_cap), ne = min(C.nent, P.ent_cap);
+    const unsigned na = min(C.namb, P.amb_cap);
+    // one thread per ambiguous cell walks its relaxer list (built by sdb_relax_kernel<3>), so a batch
+    // costs O(entries) rather than a scan of every entry per ambiguous cell
+    for (unsigned a = blockIdx.x * blockDim.x + threadIdx.x; a < na; a += gridDim.x * blockDim.x) {
+        int n = 0;
+        bool over = false;
+        // relaxers in pop order: insertion sort by the relaxer's key while walking the list
+        int buf[32];
+        int* lp = buf;
+        for (int e = P.ahead[a]; e >= 0; e = P.enext[e]) {
+            if (n == 32) { over = true; break; }
+            const int v = P.ent[e].y;
+            const unsigned long long kv = P.bq[v].ku;
+            int j = n - 1;
+            while (j >= 0 && P.bq[lp[j]].ku > kv) { lp[j + 1] = lp[j]; j--; }
+            lp[j + 1] = v;
+            n++;
+        }
+        if (over) continue;   // long lists: the block pass below
+        const int c = P.amb[a];
+        const uint8_t f = P.flags[c];
+        for (int i = 0; i < n; i++) sdb_update(P, C, c, c / P.rows, c % P.rows, f, P.bq[lp[i]]);
+        P.ambid[c] = -1;
+        P.ahead[a] = -1;
+    }
+    // cells with more than 32 relaxers: one block per cell, the list gathered into LDS, folded by thread
+    // 0.  Which pass folds a cell depends only on its list length (the thread pass clears the head of
+    // the short lists it folds, at any time relative to this loop, and never touches a long one).
     for (unsigned a = blockIdx.x; a < na; a += gridDim.x) {
-        if (threadIdx.x == 0) cnt = 0;
-        __syncthreads();
-        for (unsigned i = threadIdx.x; i < ne; i += SDB_THREADS) {
-            const int2 en = P.ent[i];
-            if (en.x == (int)a) {
-                const int p = atomicAdd(&cnt, 1);
-                if (p < SDB_FOLD_CAP) lst[p] = en.y;
-                else C.error = 1;
+        if (threadIdx.x == 0) {
+            const int h = P.ahead[a];
+            int len = 0;
+            for (int e = h; e >= 0 && len <= 32; e = P.enext[e]) len++;
+            if (len <= 32) continue;
+            int n = 0;
+            for (int e = h; e >= 0; e = P.enext[e]) {
+                if (n == SDB_FOLD_CAP) { C.error = 1; n = -1; break; }
+                lst[n++] = P.ent[e].y;
             }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0 && cnt <= SDB_FOLD_CAP) {
-            const int c = P.amb[a];
-            const int n = cnt;
-            for (int i = 1; i < n; i++) {   // insertion sort by the relaxer's key (pop order)
-                const int v = lst[i];
-                const unsigned long long kv = P.bq[v].ku;
-                int j = i - 1;
-                while (j >= 0 && P.bq[lst[j]].ku > kv) { lst[j + 1] = lst[j]; j--; }
-                lst[j + 1] = v;
+            if (n >= 0) {
+                for (int i = 1; i < n; i++) {   // insertion sort by the relaxer's key (pop order)
+                    const int v = lst[i];
+                    const unsigned long long kv = P.bq[v].ku;
+                    int j = i - 1;
+                    while (j >= 0 && P.bq[lst[j]].ku > kv) { lst[j + 1] = lst[j]; j--; }
+                    lst[j + 1] = v;
+                }
+                const int c = P.amb[a];
+                const uint8_t f = P.flags[c];
+                for (int i = 0; i < n; i++) sdb_update(P, C, c, c / P.rows, c % P.rows, f, P.bq[lst[i]]);
+                P.ambid[c] = -1;
             }
-            const uint8_t f = P.flags[c];
-            for (int i = 0; i < n; i++) sdb_update(P, C, c, c / P.rows, c % P.rows, f, P.bq[lst[i]]);
-            P.ambid[c] = -1;
+            P.ahead[a] = -1;
         }
-        __syncthreads();
     }
 }
 

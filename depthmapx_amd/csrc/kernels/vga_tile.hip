@@ -42,6 +42,10 @@ struct VgaTileParams {
     const unsigned long long* ftvis;          // [nt*64][tvw] tiles whose every non-seed cell the cell sees (null: off)
     const unsigned long long* ttvis;          // [nt][tvw] AND of ftvis over the tile's regular cells (null: off)
     const unsigned long long* ttany;          // [nt][tvw] OR of tvis over the tile's regular cells
+    const unsigned long long* pmask;          // partial-tile masks: per cell, the seen cells of each tile in
+                                              // tvis & ~ftvis, in row-word then bit order (null: off)
+    const int64_t* poff;                      // [nt*64 + 1] start of each cell's masks in pmask
+    const uint16_t* ppre;                     // [nt*64][tvw] partial tiles of the cell before each row word
     int tvw;                                  // th * ceil(tw / 64)
     const int32_t* node_cell;
     const int32_t* cell_node;
@@ -63,7 +67,8 @@ struct VgaTileParams {
     int nwork;
     DmxCtl* ctl;              // host-mapped progress / cancel block (nullptr: none)
     int chunk;                // consecutive sources per work grab (neighbouring sources share hints)
-    uint16_t* hint;           // [nt*64] scan position of the run that last hit for a recent source (0xFFFF:
+    uint32_t* hint;           // [nt*64] what last hit for a recent source: the scan position of a run, or
+                              // (bit 31) a partial-tile mask: tile << 16 | its slot in the cell's list (~0u:
                               // none); shared by all workgroups: a stale value only costs one test
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
@@ -379,6 +384,81 @@ __device__ __forceinline__ bool special_hit(const VgaTileParams& P, const FView&
     return false;
 }
 
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int u = __shfl_up(v, off, 64);
+        if (lane >= off) v += u;
+    }
+    return v;
+}
+
+// Exact bottom-up test of a regular cell from its tile-visibility rows and partial-tile masks (whole
+// wave): the cell sees a frontier cell iff a frontier tile lies under its full-visibility row, or the
+// frontier word of one of its partially seen tiles meets that tile's mask.  The cell's visible set is
+// its out-set; a regular cell's in-set is the same set, so this is the bottom-up test with no run
+// scan.  Phase C calls it only for cells whose rows left the answer open (no frontier tile under the
+// full row, some under the any row), so only the partial tiles holding a frontier cell are tested.
+// Lane `lane` owns row words lane + 64k and reads them only under a frontier tile row (Fsr), as the
+// row test before it did (L2 hits); a mask's position is the word's partial-tile prefix (ppre) plus
+// the partial bits before it in the word (the order tile_pmask_kernel writes them in).  Up to 4 masks
+// a lane are in flight per round.
+__device__ __forceinline__ bool pmask_hit(const VgaTileParams& P, const unsigned long long* F,
+                                          const unsigned long long* Fsr, int id, unsigned& nload, uint32_t* Hn) {
+    const int lane = threadIdx.x & 63;
+    const int tvw = P.tvw, tw = P.tw, wr = (P.tw + 63) / 64;
+    const size_t row = (size_t)id * tvw;
+    const unsigned long long* pm = P.pmask + P.poff[id];
+#pragma unroll 1
+    for (int k = 0; k * 64 < tvw; k++) {
+        const int w = k * 64 + lane;
+        const unsigned long long fs = w < tvw ? Fsr[w] : 0ull;
+        unsigned long long pw = 0ull, cw = 0ull;
+        int base = 0;
+        if (fs) {
+            pw = P.tvis[row + w] & ~P.ftvis[row + w];
+            cw = pw & fs;
+            if (cw) base = P.ppre[row + w];
+        }
+        const int trow = (w / wr) * tw + (w % wr) * 64;
+        while (__ballot(cw != 0ull) != 0ull) {
+            unsigned long long mk[4];
+            int tl[4], sl[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                tl[j] = -1;
+                if (cw) {
+                    const int b = __ffsll((long long)cw) - 1;
+                    cw &= cw - 1;
+                    tl[j] = trow + b;
+                    sl[j] = base + __popcll(pw & ((1ull << b) - 1ull));
+                    mk[j] = pm[sl[j]];
+                    nload++;
+                }
+            }
+            int hj = -1;
+#pragma unroll
+            for (int j = 3; j >= 0; j--)
+                if (tl[j] >= 0 && (F[tl[j]] & mk[j])) hj = j;
+            const unsigned long long hb = __ballot(hj >= 0);
+            if (hb != 0ull) {
+                // the next source's phase B tests this tile's mask first (a hint, like a run position)
+                if (lane == __ffsll((long long)hb) - 1) {
+                    const int j = hj;
+                    int t = tl[0], q = sl[0];
+                    if (j == 1) { t = tl[1]; q = sl[1]; }
+                    if (j == 2) { t = tl[2]; q = sl[2]; }
+                    if (j == 3) { t = tl[3]; q = sl[3]; }
+                    Hn[id] = 0x80000000u | ((uint32_t)t << 16) | (uint32_t)q;
+                }
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
 // V (visited) and X (next level) are per-workgroup bitmaps in HBM (they stay in the L2/MALL; a
 // source touches each word a few times), F (frontier, read by every run test) is in LDS.
 // SPECIAL = false: the graph has no asymmetric nodes (every U_f cell is regular), no exact path.
@@ -416,7 +496,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
     unsigned long long tmark = 0;     // leader-thread phase clock
     for (int i = tid; i < 32; i += NT) SC[i] = 0ull;
 
-    uint16_t* Hn = P.hint;
+    uint32_t* Hn = P.hint;
     if (tid == 0) {
         S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.cnt = 0; S.mass = 0; S.src = -1;
         S.grp = blockIdx.x & 7; S.grp_tries = 0;
@@ -575,13 +655,16 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const bool lreg = !SPECIAL || ((reg >> lane) & 1ull);
                     const bool cand = ((mask >> lane) & 1ull) && lreg;
                     int64_t ss = 0;
-                    int nr = 0, hp = 0xFFFF;
+                    int nr = 0;
+                    uint32_t hp = 0xFFFFFFFFu;
+                    int64_t pof = 0;
                     constexpr int KH0 = 4;
                     Run hd[KH0];
                     if (cand) {
                         ss = P.tscan_start[id];
                         nr = P.tnruns[id];
                         hp = Hn[id];
+                        if (P.pmask) pof = P.poff[id];
 #pragma unroll
                         for (int r = 0; r < KH0; r++) hd[r] = P.heads[r * hstride + id];
                     }
@@ -619,7 +702,12 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         to_hard = true;
                         hard_val = -1 - id;   // special node: exact path
                     } else if (mine) {
-                        if (hp >= KH && hp < nr) {   // the run that hit for a recent source
+                        if (hp != 0xFFFFFFFFu && (hp >> 31)) {   // the partial tile that hit for a recent source
+                            if (P.pmask) {
+                                rt++;
+                                hit = (F[(hp >> 16) & 0x7FFFu] & P.pmask[pof + (hp & 0xFFFFu)]) != 0ull;
+                            }
+                        } else if (hp >= KH && hp < (uint32_t)nr) {   // the run that hit for a recent source
                             rt++;
                             hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
                         }
@@ -627,7 +715,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         for (int r = 0; r < KH0; r++)
                             if (!hit && r < nr) {
                                 rt++;
-                                if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != r) Hn[id] = (uint16_t)r; }
+                                if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != (uint32_t)r) Hn[id] = (uint32_t)r; }
                             }
                         const int lim = min(nr, KH + P.bext);
                         if (!hit) ST(29, 1);
@@ -648,7 +736,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             for (int j = 3; j >= 0; j--)
                                 if (h4[j]) fj = j;
                             rt += (unsigned)min(4, lim - base);
-                            if (fj >= 0) { hit = true; if (hp != base + fj) Hn[id] = (uint16_t)(base + fj); }
+                            if (fj >= 0) { hit = true; if (hp != (uint32_t)(base + fj)) Hn[id] = (uint32_t)(base + fj); }
                         }
                         if (!hit) {
                             if (nr > KH + P.bext) { to_hard = true; hard_val = id; }
@@ -747,6 +835,18 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             found = special_hit(P, FV, id, x, y, &nr);
                             if (lane == 0) { ST(23, __builtin_amdgcn_s_memtime() - sp_t0); ST(24, 1); }
                             if (lane == 0) rt += (unsigned)nr;
+                        } else if (P.pmask) {
+                            const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
+                            unsigned nl = 0;
+                            found = pmask_hit(P, F, Fsr, id, nl, Hn);
+                            nl += __shfl_xor(nl, 32); nl += __shfl_xor(nl, 16); nl += __shfl_xor(nl, 8);
+                            nl += __shfl_xor(nl, 4); nl += __shfl_xor(nl, 2); nl += __shfl_xor(nl, 1);
+                            if (lane == 0) {
+                                ST(22, __builtin_amdgcn_s_memtime() - s_t0);
+                                ST(30, nl);
+                                ST(31, 1);
+                                if (found) ST(1, 1);
+                            }
                         } else {
                             const int64_t rs = P.tscan_start[id];
                             nr = P.tnruns[id];
@@ -772,7 +872,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                     if (hmk) fpos = base + k * 64 + __ffsll((long long)hmk) - 1;
                                 }
                                 found = fpos >= 0;
-                                if (found && lane == 0) Hn[id] = (uint16_t)min(fpos, 0xFFFE);
+                                if (found && lane == 0) Hn[id] = (uint32_t)fpos;
                             }
                             if (lane == 0) {
                                 ST(22, __builtin_amdgcn_s_memtime() - s_t0);
@@ -1055,6 +1155,112 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_vis_kernel(int rows, int t
                 fout[w] = f;
             }
         }
+    }
+}
+
+// Partial tiles per cell: popcount of tvis & ~ftvis over its row, and the exclusive prefix of the
+// per-word counts (ppre: the masks of word w start at ppre[w] within the cell's list).  One wave per
+// cell, lane over words (tvw <= 256, so a cell has at most 16,384 partial tiles: u16).
+__global__ void tile_pcount_kernel(int64_t Ct, int tvw, const unsigned long long* tvis, const unsigned long long* ftvis,
+                                   int64_t* pcount, uint16_t* ppre) {
+    const int lane = threadIdx.x & 63;
+    const int64_t id = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (id >= Ct) return;
+    int run = 0;
+    for (int k = 0; k * 64 < tvw; k++) {
+        const int w = k * 64 + lane;
+        const int c = w < tvw ? __popcll(tvis[id * tvw + w] & ~ftvis[id * tvw + w]) : 0;
+        const int incl = wave_incl_scan(c);
+        if (w < tvw) ppre[id * tvw + w] = (uint16_t)(run + incl - c);
+        run += __builtin_amdgcn_readlane(incl, 63);
+    }
+    if (lane == 0) pcount[id] = run;
+}
+
+// Partial-tile masks: for every tile a cell sees only in part (tvis & ~ftvis), the 64-bit mask of the
+// tile's cells it sees, stored at pmask[poff[id] + rank] with rank = partial bits before the tile in
+// row-word then bit order.  One workgroup per node walks the node's runs as tile_vis_kernel does and
+// ORs the per-tile masks into LDS slots (global atomics for a node with more than PM_CAP partial
+// tiles; pmask is zeroed beforehand).  A node's runs are disjoint, so every seen cell is one bit.
+constexpr int PM_CAP = 4096;
+__global__ void __launch_bounds__(64 * TV_WAVES) tile_pmask_kernel(int rows, int tw, int th, const int32_t* node_cell,
+                                                                   int64_t n, const int64_t* node_run_start,
+                                                                   const int32_t* node_nruns, const Run* pool,
+                                                                   const unsigned long long* tvis,
+                                                                   const unsigned long long* ftvis, const int64_t* poff,
+                                                                   unsigned long long* pmask) {
+    __shared__ unsigned long long part[256];
+    __shared__ int pre[256];
+    __shared__ unsigned long long lm[PM_CAP];
+    __shared__ int ptotal;
+    const int wr = (tw + 63) / 64, tvw = th * wr;
+    constexpr int TB = 64 * TV_WAVES;
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
+        const int c = node_cell[k];
+        const int id = tile_id_of(c / rows, c % rows, tw);
+        __syncthreads();   // the previous node's masks are written out
+        if (tid < 64) {
+            // partial words and their exclusive popcount prefix (tvw <= 256: 4 words a lane)
+            int run = 0;
+            for (int kk = 0; kk < 4; kk++) {
+                const int w = kk * 64 + lane;
+                const unsigned long long p = w < tvw ? (tvis[(size_t)id * tvw + w] & ~ftvis[(size_t)id * tvw + w]) : 0ull;
+                const int cnt = __popcll(p);
+                const int incl = wave_incl_scan(cnt);
+                part[w] = p;
+                pre[w] = run + incl - cnt;
+                run += __builtin_amdgcn_readlane(incl, 63);
+            }
+            if (lane == 0) ptotal = run;
+        }
+        __syncthreads();
+        const int P = ptotal;
+        const bool in_lds = P <= PM_CAP;
+        unsigned long long* gout = pmask + poff[id];
+        if (in_lds)
+            for (int i = tid; i < P; i += TB) lm[i] = 0ull;
+        __syncthreads();
+        auto put = [&](int tx, int ty, unsigned long long m) {
+            const int w = ty * wr + (tx >> 6), b = tx & 63;
+            const unsigned long long pwv = part[w];
+            if (!((pwv >> b) & 1ull)) return;
+            const int slot = pre[w] + __popcll(pwv & ((1ull << b) - 1ull));
+            if (in_lds) atomicOr(&lm[slot], m);
+            else atomicOr(&gout[slot], m);
+        };
+        const int64_t rs = node_run_start[k];
+        const int nr = node_nruns[k];
+        for (int r = tid; r < nr; r += TB) {
+            const Run ru = pool[rs + r];
+            if (ru.y0 == ru.y1) {
+                const int y = ru.y0, ty = y >> 3;
+                for (int tx = ru.x0 >> 3; tx <= (ru.x1 >> 3); tx++) {
+                    const int a = max((int)ru.x0, tx * 8) & 7, b = min((int)ru.x1, tx * 8 + 7) & 7;
+                    put(tx, ty, (unsigned long long)((0xFFu >> (7 - b)) & (0xFFu << a) & 0xFFu) << ((y & 7) * 8));
+                }
+            } else if (ru.x0 == ru.x1) {
+                const int x = ru.x0, tx = x >> 3;
+                const unsigned long long colm = 0x0101010101010101ull << (x & 7);
+                for (int ty = ru.y0 >> 3; ty <= (ru.y1 >> 3); ty++) {
+                    const int a = max((int)ru.y0, ty * 8) & 7, b = min((int)ru.y1, ty * 8 + 7) & 7;
+                    put(tx, ty, colm & (~0ull >> (8 * (7 - b))) & (~0ull << (8 * a)));
+                }
+            } else {
+                const int dy = (ru.y1 > ru.y0) ? 1 : -1;
+                int x = ru.x0, y = ru.y0;
+                while (x <= ru.x1) {
+                    int nn;
+                    const unsigned long long m = diag_tile_mask(x, y, dy, ru.x1, nn);
+                    put(x >> 3, y >> 3, m);
+                    x += nn;
+                    y += dy * nn;
+                }
+            }
+        }
+        __syncthreads();
+        if (in_lds)
+            for (int i = tid; i < P; i += TB) gout[i] = lm[i];
     }
 }
 

@@ -104,19 +104,49 @@ def test_1000_vga_blocks_match_oracle(big1000):
         assert (want[:, 5] > 0.5 * N).all()
 
 
+def _spread_blocks(N, n, size, seed):
+    rng = np.random.default_rng(seed)
+    starts = sorted(set([0, N - size] + [int(v) for v in rng.integers(0, N - size, size=n - 2)]))
+    return [(b, b + size) for b in starts]
+
+
 def test_1000_vga_kernels_agree_at_size(big1000, ctx, monkeypatch):
-    """The tile-resolved BFS with its line summaries (default above ~1010^2 the coarser per-tile
-    summary) against the direction-optimising kernel, bit-for-bit, on a block of 256 sources."""
+    """The tile-resolved BFS (line summaries, tile-visibility rows, partial-tile masks) against the
+    direction-optimising kernel, which shares none of those certificates, bit-for-bit on 4 blocks of
+    256 sources spread over the map (the direction-optimising kernel keeps its bitmaps in HBM at this
+    size: ~100 sources/s, so the wide sample is the run-scan comparison below)."""
     pm, g, om = big1000
     N = g.info()["nnodes"]
-    b, e = N // 3, N // 3 + 256
-    a = g.vga_visual_global(src_begin=b, src_end=e)
-    assert ctx.last_stats()["vga_kernel"] == "tile-resolved"
+    blocks = _spread_blocks(N, 4, 256, seed=31)
+    a = [g.vga_visual_global(src_begin=b, src_end=e) for (b, e) in blocks]
+    st = ctx.last_stats()
+    assert st["vga_kernel"] == "tile-resolved"
     monkeypatch.setenv("DMX_VGA_KERNEL", "do")
     g2 = pm.make_graph(ctx)
-    c = g2.vga_visual_global(src_begin=b, src_end=e)
+    for (b, e), ai in zip(blocks, a):
+        c = g2.vga_visual_global(src_begin=b, src_end=e)
+        np.testing.assert_array_equal(ai[b:e].view(np.uint32), c[b:e].view(np.uint32), err_msg="sources [%d,%d)" % (b, e))
     _release(ctx, g2)
-    np.testing.assert_array_equal(a[b:e].view(np.uint32), c[b:e].view(np.uint32))
+
+
+def test_1000_vga_partial_tile_masks_agree_with_run_scan(big1000, ctx, monkeypatch):
+    """Phase C's exact partial-tile-mask test (default) against its run scan (DMX_VGA_PMASK=0, a
+    launch-time switch on the same graph), bit-for-bit on 16 blocks of 8192 sources (131,072 sources,
+    13 % of the map: the rare-cell cases the certificates could hide show up here before they show up
+    in a 32-source oracle block); the masks must have decided cells on these blocks."""
+    pm, g, om = big1000
+    N = g.info()["nnodes"]
+    blocks = _spread_blocks(N, 16, 8192, seed=32)
+    a, used = [], 0
+    for (b, e) in blocks:
+        a.append(g.vga_visual_global(src_begin=b, src_end=e))
+        used += ctx.last_stats()["vga_pmask_cells"]
+    assert used > 0
+    monkeypatch.setenv("DMX_VGA_PMASK", "0")
+    for (b, e), ai in zip(blocks, a):
+        c = g.vga_visual_global(src_begin=b, src_end=e)
+        assert ctx.last_stats()["vga_pmask_cells"] == 0
+        np.testing.assert_array_equal(ai[b:e].view(np.uint32), c[b:e].view(np.uint32), err_msg="sources [%d,%d)" % (b, e))
 
 
 def test_1000_vga_per_tile_summary_path_agrees(big1000, ctx, monkeypatch):
