@@ -414,7 +414,8 @@ def main():
         # phase C (tvis and ftvis) and phase B (tile-to-tile rows)
         tvw = th * ((tw + 63) // 64)
         vga_bytes = (8 * stats.get("vga_runs_expanded", 0) + 16 * tw * th * nsrc + 32 * tw * th * levels +
-                     2 * stats.get("vga_tvis_bytes", 0) + 8 * tvw * stats.get("vga_b_tiles", 0))
+                     2 * stats.get("vga_tvis_bytes", 0) + 8 * tvw * stats.get("vga_b_tiles", 0) +
+                     8 * stats.get("vga_pmask_loads", 0))
         second = "vga_tile_kernel"
         if stepdepth:
             # expanders' run records (average runs per node: the per-expander counts are not exported)
@@ -457,7 +458,8 @@ def main():
             roof["b_vga_reference_work"] = b_vga
             roof["b_vga_rate_GBs"] = b_vga / vga_s / 1e9 if vga_s else None
             roof["work_model"] = ("8 B x run records tested + 16 B x tiles x sources (V/X reset) + 32 B x tiles x "
-                                  "levels + tile-visibility rows read (DESIGN.md section 3)")
+                                  "levels + tile-visibility rows read + 8 B x partial-tile masks read (DESIGN.md "
+                                  "section 3)")
         # issue-rate roofline (VALU) for the two hot kernels, and makeGraph's FP64 rate
         issue = {}
         for kname in ("makegraph_kernel", "vga_tile_kernel", "stepdepth_kernel"):
@@ -502,6 +504,9 @@ def main():
                         "vga_hard_cells_rejected_by_tile_visibility": stats.get("vga_pruned_cells"),
                         "vga_levels_bottom_up": stats.get("vga_bottom_up_levels"),
                         "vga_levels_top_down": stats.get("vga_top_down_levels"),
+                        "vga_cells_decided_by_partial_tile_masks": stats.get("vga_pmask_cells"),
+                        "vga_partial_tile_mask_loads": stats.get("vga_pmask_loads"),
+                        "vga_partial_tile_mask_bytes": stats.get("vga_pmask_bytes"),
                         "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc,
                         "makegraph_algorithmic_bytes": mk_bytes, "vga_algorithmic_bytes": vga_bytes},
             "roofline": roof,

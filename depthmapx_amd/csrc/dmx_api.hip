@@ -1774,6 +1774,8 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     HIPCHK(xg.alloc((size_t)blocks * 2 * nt));
     HIPCHK(queue.alloc((size_t)blocks * nt));
     HIPCHK(list.alloc((size_t)blocks * nt * 64 * 2));
+    DevBuf<int32_t> tlist;   // per workgroup: the two unvisited-tile lists
+    HIPCHK(tlist.alloc((size_t)blocks * nt * 2));
     DevBuf<uint32_t> hint;
     HIPCHK(hint.alloc((size_t)nt * 64));
     HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
@@ -1781,6 +1783,7 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     P.xg = xg.p;
     P.queue = queue.p;
     P.list = list.p;
+    P.tlist = tlist.p;
     P.hint = hint.p;
     // chunks of consecutive sources per workgroup, small enough to balance the tail
     P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
@@ -1948,6 +1951,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[17] = (long long)st[14];                          // phase-C cells (regular)
     ctx->last_stats[35] = (long long)st[30];                          // phase-C partial-tile masks read
     ctx->last_stats[36] = (long long)st[31];                          // phase-C cells tested by masks
+    ctx->last_stats[37] = (long long)(g->pmask.p ? g->pmask.n * 8 : 0);  // bytes of partial-tile masks held
     if (nseeds > 0) return DMX_OK;
     if (!out_on_device && nsrc > 0)
         HIPCHK(copy_sync(ctx->stream, out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));

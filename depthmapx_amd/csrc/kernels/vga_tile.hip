@@ -73,6 +73,8 @@ struct VgaTileParams {
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
     int32_t* list;            // per workgroup [2][nt*64]: hard cells / frontier cells, then phase-B2 cells
+    int32_t* tlist;           // per workgroup [2][nt]: tiles holding an unvisited cell (built by one level's
+                              // bookkeeping for the next level: phase A and the bookkeeping walk only them)
     int maxlev;
     // seed mode (visual step depth, vgavisualglobaldepth.cpp:23-77): one BFS from nseeds seed nodes
     // (level 0, always expanded); contextfilled odd cells are never expanded at later levels;
@@ -278,6 +280,7 @@ __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
 
 struct TileShared {
     int src, qn, hn, item, bn;
+    int tn[2];            // entries of the two unvisited-tile lists (level parity)
     int grp, grp_tries;   // XCD-grouped work: the group being drained, groups found empty
     int mpart;            // merge partner cell of the source (-1: none)
     unsigned long long cnt, mass;
@@ -487,6 +490,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
     unsigned long long* Xg = Vg + nt;
     int4* Q = P.queue + (size_t)blockIdx.x * nt;
     int32_t* L = P.list + (size_t)blockIdx.x * nt * 64 * 2;
+    int32_t* TL = P.tlist + (size_t)blockIdx.x * nt * 2;
     const size_t hstride = (size_t)nt * 64;
     // work counters live in LDS (flushed to P.stats at exit) so they cost no registers: a 1024-thread
     // workgroup has 128 VGPRs a lane and every spill is a scratch round trip
@@ -578,6 +582,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
         long long m_f = seeded ? P.nseeds : (spart >= 0 ? 2 : 1), m_u = target, discovered = 0;
         int level = 0, nlev = 1;
         bool overflow = false;
+        if (tid == 0) { S.tn[0] = 0; S.tn[1] = 0; }
         __syncthreads();
         if (tid == 0) hist[0] = seeded ? P.nseeds : 1;
         for (;;) {
@@ -599,8 +604,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(8, n - tmark); tmark = n; }
             } else if (bottom_up) {
                 // ---- A: tile-common runs
-                for (int t0 = 0; t0 < nt; t0 += NT) {
-                    const int t = t0 + tid;
+                // only the tiles the previous level's bookkeeping listed can hold an unvisited cell
+                const int32_t* TLc = TL + (level & 1) * nt;
+                const int ntl = S.tn[level & 1];
+                for (int t0 = 0; t0 < ntl; t0 += NT) {
+                    const int t = t0 + tid < ntl ? TLc[t0 + tid] : nt;
                     unsigned long long U = 0ull;
                     if (t < nt) {
                         // V, the regular mask and the CRK common runs in one round trip
@@ -936,14 +944,29 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 tmark = n;
             }
             // ---- level bookkeeping: count X, publish the expandable part as the next frontier
+            // Walk the tiles listed for this level (all tiles after level 0: no list yet) -- X only ever
+            // holds cells that were unvisited, so every other tile has none -- and list the tiles that
+            // keep an unvisited cell for the next level.  A cleared frontier first: unlisted tiles
+            // publish nothing (the merge pass may have set bits anywhere).
+            const bool have_list = level > 0;
             for (int i = tid; i < nfs; i += NT) Fsr[i] = 0ull;
+            if (have_list)
+                for (int t = tid; t < nt; t += NT) F[t] = 0ull;
             __syncthreads();
             unsigned long long c_loc = 0, m_loc = 0;
-            for (int t = tid; t < nt; t += NT) {
+            const int32_t* TLc = TL + (level & 1) * nt;
+            int32_t* TLn = TL + ((level + 1) & 1) * nt;
+            const int nwalk = have_list ? S.tn[level & 1] : nt;
+            for (int i0 = 0; i0 < nwalk; i0 += NT) {
+                const int t = i0 + tid < nwalk ? (have_list ? TLc[i0 + tid] : i0 + tid) : -1;
+                bool open = false;
+                if (t >= 0) {
                 unsigned long long x = ld_wg(&Xg[t]);
+                const unsigned long long v0 = Vg[t];
+                open = ~(v0 | x) != 0ull;
                 if (x) {
                     c_loc += (unsigned long long)__popcll(x);
-                    Vg[t] |= x;
+                    Vg[t] = v0 | x;
                     Xg[t] = 0ull;
                     if (P.cell_level)
                         for (unsigned long long m = x; m; m &= m - 1) P.cell_level[t * 64 + __ffsll((long long)m) - 1] = level + 1;
@@ -958,6 +981,14 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     }
                 }
                 F[t] = x;
+                }
+                const unsigned long long om = __ballot(open);
+                if (om) {
+                    int base = 0;
+                    if (lane == 0) base = atomicAdd(&S.tn[(level + 1) & 1], __popcll(om));
+                    base = __shfl(base, 0);
+                    if (open) TLn[base + __popcll(om & ((1ull << lane) - 1ull))] = t;
+                }
             }
             for (int off = 32; off >= 1; off >>= 1) {
                 c_loc += __shfl_xor(c_loc, off);
@@ -995,7 +1026,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             const long long mcorr = (long long)S.mcorr, mdisc = (long long)S.mdisc;
             if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(12, n - tmark); tmark = n; }
             __syncthreads();
-            if (tid == 0) { S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.mcorr = 0; S.mdisc = 0; }
+            if (tid == 0) {
+                S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.mcorr = 0; S.mdisc = 0;
+                S.tn[level & 1] = 0;   // this level's list is spent; it is the next level's append target
+            }
             if (cnt == 0) break;
             if (level + 1 >= VGA_HMAX) { overflow = true; break; }
             if (tid == 0) hist[level + 1] = (int)(cnt - mcorr);

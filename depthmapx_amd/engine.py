@@ -97,7 +97,7 @@ class Context:
                 "vga_cells_reached", "vga_sources", "vga_fail_cells", "vga_fail_runs", "vga_hbm_bitmaps",
                 "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",
                 "vga_hard_cells", "vga_hard_certain", "vga_topdown_cycles", "vga_b_tiles", "vga_b_cells", "vga_tt_tiles", "vga_c_busy", "vga_c_scan", "vga_c_spec", "vga_n_spec", "vga_tt_pruned", "vga_b_row_cycles", "vga_b_cell_tiles",
-                "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks", "mk_reruns", "vga_pmask_loads", "vga_pmask_cells"]
+                "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks", "mk_reruns", "vga_pmask_loads", "vga_pmask_cells", "vga_pmask_bytes"]
         d = {k: int(v) for k, v in zip(keys, out)}
         lv = d.pop("vga_levels")
         d["vga_bottom_up_levels"], d["vga_top_down_levels"] = lv & 0xFFFFFFFF, lv >> 32
