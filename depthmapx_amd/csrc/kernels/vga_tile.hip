@@ -24,6 +24,11 @@
 namespace dmx {
 
 constexpr int KH = 8;        // head runs per cell (first KH entries of its scan order)
+// HV_FIRST: heads and tile-common runs ordered row / column runs first (1000^2: VGA 7.50 -> 6.11 s, phase A's
+// clocks / 5.7: a diagonal run's test walks its tiles, 8 LDS reads a round trip)
+#ifndef DMX_VGA_HV_FIRST
+#define DMX_VGA_HV_FIRST 1
+#endif
 constexpr int CRK = 4;       // tile-common runs per tile
 constexpr int BEXT_DEFAULT = 4;   // runs after the heads a cell scans on its own lane before going wave-cooperative
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
@@ -618,6 +623,34 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         U = ~Vg[t];
                         const unsigned long long R = U & P.regular_tiles[t];
                         if (R) {
+#ifndef DMX_VGA_CR_PAR
+#define DMX_VGA_CR_PAR 0   // 1: the 4 tests without early exit (measured 2x slower phase A: the first usually hits)
+#endif
+#ifndef DMX_VGA_HEADS_PAR
+#define DMX_VGA_HEADS_PAR 0
+#endif
+// B_ORDER: the hint's operand is loaded before the head tests and tested after them (-0.7 %)
+#ifndef DMX_VGA_B_ORDER
+#define DMX_VGA_B_ORDER 1
+#endif
+// RB_INC: line summaries set per published tile with LDS atomics instead of rebuilt from F (measured
+// slower: bookkeeping clocks x1.9, contention on the summary words of a tile row)
+#ifndef DMX_VGA_RB_INC
+#define DMX_VGA_RB_INC 0
+#endif
+#if DMX_VGA_CR_PAR
+                            // the common runs' tests are independent (no early-out between them), so their
+                            // LDS round trips overlap
+                            bool h[CRK];
+#pragma unroll
+                            for (int j = 0; j < CRK; j++) h[j] = j < P.crk && c[j].x0 >= 0 && run_hits_fs(FV, c[j]);
+                            bool hit = false;
+#pragma unroll
+                            for (int j = 0; j < CRK; j++) {
+                                rt += (j < P.crk && c[j].x0 >= 0) ? 1u : 0u;
+                                hit |= h[j];
+                            }
+#else
                             bool hit = false;
 #pragma unroll 1
                             for (int j = 0; j < CRK; j++)
@@ -625,6 +658,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                     rt++;
                                     hit = run_hits_fs(FV, c[j]);
                                 }
+#endif
                             if (hit) { Xg[t] = R; U &= ~R; ST(7, 1); }
                         }
                     }
@@ -710,6 +744,28 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         to_hard = true;
                         hard_val = -1 - id;   // special node: exact path
                     } else if (mine) {
+#if DMX_VGA_B_ORDER
+                        // The hint's operand (a run of the scan order, or a partial tile's mask) is loaded
+                        // first and tested after the 4 heads, so the load overlaps the heads' LDS tests;
+                        // a head hit leaves the hint alone (heads are tested every time anyway).
+                        Run hr;
+                        hr.x0 = -1;
+                        unsigned long long hmk = 0ull;
+                        int htile = -1;
+                        if (hp != 0xFFFFFFFFu && (hp >> 31)) {
+                            if (P.pmask) { htile = (int)((hp >> 16) & 0x7FFFu); hmk = P.pmask[pof + (hp & 0xFFFFu)]; }
+                        } else if (hp >= KH && hp < (uint32_t)nr) {
+                            hr = P.scan_pool[ss + hp];
+                        }
+#pragma unroll 1
+                        for (int r = 0; r < KH0; r++)
+                            if (!hit && r < nr) {
+                                rt++;
+                                hit = run_hits_fs(FV, hd[r]);
+                            }
+                        if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
+                        else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
+#else
                         if (hp != 0xFFFFFFFFu && (hp >> 31)) {   // the partial tile that hit for a recent source
                             if (P.pmask) {
                                 rt++;
@@ -719,12 +775,28 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             rt++;
                             hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
                         }
+#if DMX_VGA_HEADS_PAR
+                        if (!hit) {
+                            // the heads' tests are independent: their LDS round trips overlap
+                            bool h4[KH0];
+#pragma unroll
+                            for (int r = 0; r < KH0; r++) h4[r] = r < nr && run_hits_fs(FV, hd[r]);
+                            int fr = -1;
+#pragma unroll
+                            for (int r = KH0 - 1; r >= 0; r--)
+                                if (h4[r]) fr = r;
+                            rt += (unsigned)min(nr, KH0);
+                            if (fr >= 0) { hit = true; if (hp != (uint32_t)fr) Hn[id] = (uint32_t)fr; }
+                        }
+#else
 #pragma unroll 1
                         for (int r = 0; r < KH0; r++)
                             if (!hit && r < nr) {
                                 rt++;
                                 if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != (uint32_t)r) Hn[id] = (uint32_t)r; }
                             }
+#endif
+#endif
                         const int lim = min(nr, KH + P.bext);
                         if (!hit) ST(29, 1);
                         for (int base = KH0; base < lim && !hit; base += 4) {
@@ -949,7 +1021,12 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             // keep an unvisited cell for the next level.  A cleared frontier first: unlisted tiles
             // publish nothing (the merge pass may have set bits anywhere).
             const bool have_list = level > 0;
+            // line-resolved summaries set per published tile (no merge links: the merge pass adds single
+            // cells to F afterwards, and then the summaries are rebuilt from F below)
+            const bool rb_inc = RBM && DMX_VGA_RB_INC && P.nmp == 0;
             for (int i = tid; i < nfs; i += NT) Fsr[i] = 0ull;
+            if (rb_inc)
+                for (int i = tid; i < P.th * 8 * wr + P.tw * 8 * wc; i += NT) RB[i] = 0ull;   // RB, then CB
             if (have_list)
                 for (int t = tid; t < nt; t += NT) F[t] = 0ull;
             __syncthreads();
@@ -978,6 +1055,21 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         const int tx = t % tw, ty = t / tw;
                         atomicOr(&Fsr[ty * wr + (tx >> 6)], 1ull << (tx & 63));
                         if (!RBM) atomicOr(&Fsc[tx * wc + (ty >> 6)], 1ull << (ty & 63));
+                        if (rb_inc) {
+                            // rows r (columns c) of the tile holding a frontier cell
+                            unsigned long long yr = x | (x >> 4);
+                            yr |= yr >> 2;
+                            yr |= yr >> 1;
+                            unsigned rows8 = (unsigned)(((yr & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+                            unsigned long long yc = x | (x >> 32);
+                            yc |= yc >> 16;
+                            yc |= yc >> 8;
+                            unsigned cols8 = (unsigned)(yc & 0xFFull);
+                            for (; rows8; rows8 &= rows8 - 1)
+                                atomicOr(&RB[(ty * 8 + __ffs(rows8) - 1) * wr + (tx >> 6)], 1ull << (tx & 63));
+                            for (; cols8; cols8 &= cols8 - 1)
+                                atomicOr(&CB[(tx * 8 + __ffs(cols8) - 1) * wc + (ty >> 6)], 1ull << (ty & 63));
+                        }
                     }
                 }
                 F[t] = x;
@@ -1000,7 +1092,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 merge_level_pass(P.mpairs, P.nmp, rows, tw, NT, F, Vg, false, P.seed_tiles, Fsr, RBM ? nullptr : Fsc, wr,
                                  wc, P.cell_level, level + 1, &S.mcorr, &S.mdisc, &S.mass);
             }
-            if (RBM) {
+            if (RBM && !rb_inc) {
                 // line-resolved summaries from the published frontier (plain stores, no atomics)
                 __syncthreads();
                 const int th = P.th;
@@ -1081,7 +1173,20 @@ __global__ void tile_heads_kernel(int rows, int tw, const int32_t* node_cell, in
     const int nr = node_nruns[k];
     tscan_start[id] = ss;
     tnruns[id] = nr;
+#if DMX_VGA_HV_FIRST
+    // the first KH scan entries with the row / column runs before the diagonal ones (a diagonal run's
+    // test walks its tiles one LDS round trip per 8; a row or column run costs <= 4 reads): the order
+    // only changes which test hits first
+    int o = 0;
+    for (int pass = 0; pass < 2; pass++)
+        for (int h = 0; h < KH && h < nr; h++) {
+            const Run ru = scan_pool[ss + h];
+            const bool diag = ru.x0 != ru.x1 && ru.y0 != ru.y1;
+            if (diag == (pass == 1)) heads[(o++) * hstride + id] = ru;
+        }
+#else
     for (int h = 0; h < KH && h < nr; h++) heads[h * hstride + id] = scan_pool[ss + h];
+#endif
 }
 
 // Tile-visibility rows: bit (ty, tx) of cell id's row is set iff the cell sees some cell of tile
@@ -1438,8 +1543,15 @@ __global__ void __launch_bounds__(CR_THREADS) tile_cr_kernel(int cols, int rows,
             int used = 0;
             for (int j = 0; j < CRK; j++) {
                 int pick = -1;
+#if DMX_VGA_HV_FIRST
+                // row / column runs first (cheap tests), longest first within each kind
+                auto key = [&](int g) { return bestlen[g] + ((cand[g].dx == 0 || cand[g].dy == 0) ? (1 << 20) : 0); };
+                for (int g = 0; g < 8; g++)
+                    if (bestlen[g] > 0 && !((used >> g) & 1) && (pick < 0 || key(g) > key(pick))) pick = g;
+#else
                 for (int g = 0; g < 8; g++)
                     if (bestlen[g] > 0 && !((used >> g) & 1) && (pick < 0 || bestlen[g] > bestlen[pick])) pick = g;
+#endif
                 Run z;
                 z.x0 = z.y0 = z.x1 = z.y1 = -1;
                 if (pick >= 0) {
