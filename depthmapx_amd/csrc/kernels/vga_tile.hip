@@ -638,6 +638,12 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
 #ifndef DMX_VGA_RB_INC
 #define DMX_VGA_RB_INC 0
 #endif
+#ifndef DMX_VGA_HINT_BEFORE_DIAG
+#define DMX_VGA_HINT_BEFORE_DIAG 0
+#endif
+#ifndef DMX_VGA_BEXT_NODIAG
+#define DMX_VGA_BEXT_NODIAG 0
+#endif
 #if DMX_VGA_CR_PAR
                             // the common runs' tests are independent (no early-out between them), so their
                             // LDS round trips overlap
@@ -757,6 +763,24 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (hp >= KH && hp < (uint32_t)nr) {
                             hr = P.scan_pool[ss + hp];
                         }
+#if DMX_VGA_HINT_BEFORE_DIAG
+                        // row / column heads, then the hint, then the diagonal heads (the heads are stored row /
+                        // column runs first, HV_FIRST): a diagonal test walks the run's tiles
+                        int r0 = 0;
+#pragma unroll 1
+                        for (; r0 < KH0 && r0 < nr && !hit; r0++) {
+                            if (hd[r0].x0 != hd[r0].x1 && hd[r0].y0 != hd[r0].y1) break;
+                            rt++;
+                            hit = run_hits_fs(FV, hd[r0]);
+                        }
+                        if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
+                        else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
+#pragma unroll 1
+                        for (; r0 < KH0 && r0 < nr && !hit; r0++) {
+                            rt++;
+                            hit = run_hits_fs(FV, hd[r0]);
+                        }
+#else
 #pragma unroll 1
                         for (int r = 0; r < KH0; r++)
                             if (!hit && r < nr) {
@@ -765,6 +789,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             }
                         if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
                         else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
+#endif
 #else
                         if (hp != 0xFFFFFFFFu && (hp >> 31)) {   // the partial tile that hit for a recent source
                             if (P.pmask) {
@@ -808,6 +833,13 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                 else if (r < lim) rr[j] = P.scan_pool[ss + r];
                                 else rr[j].x0 = -1;
                             }
+#if DMX_VGA_BEXT_NODIAG
+                            // diagonal runs are left to phase C's exact mask test (their test walks the tiles)
+                            if (P.pmask)
+#pragma unroll
+                                for (int j = 0; j < 4; j++)
+                                    if (rr[j].x0 >= 0 && rr[j].x0 != rr[j].x1 && rr[j].y0 != rr[j].y1) rr[j].x0 = -1;
+#endif
                             bool h4[4];
 #pragma unroll
                             for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
