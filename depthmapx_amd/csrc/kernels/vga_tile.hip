@@ -467,6 +467,76 @@ __device__ __forceinline__ bool pmask_hit(const VgaTileParams& P, const unsigned
     return false;
 }
 
+// C_FUSED: the row test and the mask test in one pass per cell (no separate row-test pass over the chunk):
+// the 4 row words of tvis and ftvis a lane owns are loaded together, a frontier tile under the full row is a
+// certain hit, none under the partial bits a certain miss, else the masks of the partial frontier tiles.
+__device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const unsigned long long* F,
+                                                const unsigned long long* Fsr, int id, unsigned& nload, uint32_t* Hn,
+                                                int& how) {
+    const int lane = threadIdx.x & 63;
+    const int tvw = P.tvw, tw = P.tw, wr = (P.tw + 63) / 64;
+    const size_t row = (size_t)id * tvw;
+    unsigned long long pw[4], cw[4];
+    bool cert = false;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int w = k * 64 + lane;
+        const unsigned long long fs = w < tvw ? Fsr[w] : 0ull;
+        unsigned long long t = 0ull, f = 0ull;
+        if (fs) { t = P.tvis[row + w]; f = P.ftvis[row + w]; }
+        cert |= (f & fs) != 0ull;
+        pw[k] = t & ~f;
+        cw[k] = pw[k] & fs;
+    }
+    if (__ballot(cert) != 0ull) { how = 1; return true; }
+    if (__ballot((cw[0] | cw[1] | cw[2] | cw[3]) != 0ull) == 0ull) { how = 2; return false; }
+    how = 0;
+    int base[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) base[k] = cw[k] ? (int)P.ppre[row + k * 64 + lane] : 0;
+    const unsigned long long* pm = P.pmask + P.poff[id];
+#pragma unroll 1
+    for (int k = 0; k < 4; k++) {
+        const int w = k * 64 + lane;
+        const int trow = (w / wr) * tw + (w % wr) * 64;
+        unsigned long long c = cw[k];
+        const unsigned long long p = pw[k];
+        const int bk = base[k];
+        while (__ballot(c != 0ull) != 0ull) {
+            unsigned long long mk[4];
+            int tl[4], sl[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                tl[j] = -1;
+                if (c) {
+                    const int b = __ffsll((long long)c) - 1;
+                    c &= c - 1;
+                    tl[j] = trow + b;
+                    sl[j] = bk + __popcll(p & ((1ull << b) - 1ull));
+                    mk[j] = pm[sl[j]];
+                    nload++;
+                }
+            }
+            int hj = -1;
+#pragma unroll
+            for (int j = 3; j >= 0; j--)
+                if (tl[j] >= 0 && (F[tl[j]] & mk[j])) hj = j;
+            const unsigned long long hb = __ballot(hj >= 0);
+            if (hb != 0ull) {
+                if (lane == __ffsll((long long)hb) - 1) {
+                    int t = tl[0], q = sl[0];
+                    if (hj == 1) { t = tl[1]; q = sl[1]; }
+                    if (hj == 2) { t = tl[2]; q = sl[2]; }
+                    if (hj == 3) { t = tl[3]; q = sl[3]; }
+                    Hn[id] = 0x80000000u | ((uint32_t)t << 16) | (uint32_t)q;
+                }
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
 // V (visited) and X (next level) are per-workgroup bitmaps in HBM (they stay in the L2/MALL; a
 // source touches each word a few times), F (frontier, read by every run test) is in LDS.
 // SPECIAL = false: the graph has no asymmetric nodes (every U_f cell is regular), no exact path.
@@ -648,6 +718,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
 #endif
 #ifndef DMX_VGA_RB8
 #define DMX_VGA_RB8 1
+#endif
+#ifndef DMX_VGA_C_FUSED
+#define DMX_VGA_C_FUSED 0
 #endif
 #if DMX_VGA_CR_PAR
                             // the common runs' tests are independent (no early-out between them), so their
@@ -899,7 +972,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const int cn = min(CCH, hn - it0);
                     const int myv = lane < cn ? L[it0 + lane] : -1;
                     unsigned long long certain_m = 0ull, pruned_m = 0ull;   // bit j: chunk entry j
-                    if (P.tvis) {
+                    if (P.tvis && !(DMX_VGA_C_FUSED && P.pmask)) {
                         for (int j = 0; j < cn; j += 2) {
                             const int v0 = __builtin_amdgcn_readlane(myv, j);
                             const int v1 = __builtin_amdgcn_readlane(myv, j + 1);
@@ -959,7 +1032,17 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (P.pmask) {
                             const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
                             unsigned nl = 0;
+#if DMX_VGA_C_FUSED
+                            int how = 0;
+                            found = pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+                            if (lane == 0) {
+                                ST(14, 1);
+                                if (how == 1) { ST(16, 1); }
+                                if (how == 2) ST(13, 1);
+                            }
+#else
                             found = pmask_hit(P, F, Fsr, id, nl, Hn);
+#endif
                             nl += __shfl_xor(nl, 32); nl += __shfl_xor(nl, 16); nl += __shfl_xor(nl, 8);
                             nl += __shfl_xor(nl, 4); nl += __shfl_xor(nl, 2); nl += __shfl_xor(nl, 1);
                             if (lane == 0) {

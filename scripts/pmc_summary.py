@@ -56,13 +56,20 @@ def counters(root):
 
 
 def durations(root):
+    """{kernel: calls, total and average duration} summed over every row whose name maps to the kernel: the
+    template variants of one kernel (makeGraph's first pass and its capacity re-run) are separate rows of the
+    kernel-trace stats, and the counter passes average over all their launches alike."""
     out = {}
     for p in glob.glob(os.path.join(root, "**", "*kernel_stats.csv"), recursive=True):
         for r in csv.DictReader(open(p)):
             k = kname(r["Name"])
-            if k is not None and k not in out:
-                out[k] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                          "total_ns": float(r["TotalDurationNs"])}
+            if k is None:
+                continue
+            e = out.setdefault(k, {"calls": 0, "total_ns": 0.0})
+            e["calls"] += int(r["Calls"])
+            e["total_ns"] += float(r["TotalDurationNs"])
+    for e in out.values():
+        e["avg_ns"] = e["total_ns"] / max(e["calls"], 1)
     return out
 
 
