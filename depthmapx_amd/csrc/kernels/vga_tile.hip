@@ -719,8 +719,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
 #ifndef DMX_VGA_RB8
 #define DMX_VGA_RB8 1
 #endif
+// C_FUSED: phase C's row test and mask test in one pass per cell (1000^2: VGA 5.57 -> 5.11 s)
 #ifndef DMX_VGA_C_FUSED
-#define DMX_VGA_C_FUSED 0
+#define DMX_VGA_C_FUSED 1
 #endif
 #if DMX_VGA_CR_PAR
                             // the common runs' tests are independent (no early-out between them), so their
