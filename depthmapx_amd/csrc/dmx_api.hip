@@ -1606,10 +1606,11 @@ static int prepare_symmetry(dmx_graph* g) {
 }
 
 // Partial-tile masks for phase C's exact test (vga_tile.hip pmask_hit): counts from the full rows
-// (every rank after the rows' all-reduce), an exclusive scan into per-cell offsets, then the masks over
-// the rank's node range (summed over ranks: a cell's masks come from one node, so ranks never
-// overlap).  ~10 GB at 1000^2 (about 1,300 partial tiles a cell); skipped, with phase C scanning runs
-// instead, when that would take more than a quarter of the free memory.
+// (every rank after the rows' all-reduce), an exclusive scan into per-cell offsets, then the masks of every
+// node.  Each rank builds all of them itself, with no collective: the pass costs ~0.07 s at 1000^2, where
+// all-reducing its ~10 GB over the ranks would cost more, and whether a rank has them does not change
+// its results (phase C scans runs without them), so the ranks need not agree.  Skipped when they would
+// take more than a quarter of the free memory.
 static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_t Ct) {
     dmx_ctx* ctx = g->ctx;
     hipStream_t s = ctx->stream;
@@ -1627,18 +1628,7 @@ static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_
     HIPCHK(copy_sync(s, &total, g->poff.p + Ct, 8, hipMemcpyDeviceToHost));
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    bool build = total > 0 && (size_t)total * 8 <= free_b / 4;
-    if (g->prep_fn) {
-        // the same decision on every rank (the masks are all-reduced)
-        DevBuf<int64_t> veto;
-        HIPCHK(veto.alloc(1));
-        const int64_t v = build ? 0 : 1;
-        HIPCHK(hipMemcpyAsync(veto.p, &v, 8, hipMemcpyHostToDevice, s));
-        if (int rc = prep_allreduce(g, veto.p, 1, DMX_I64)) return rc;
-        int64_t vs = 0;
-        HIPCHK(copy_sync(s, &vs, veto.p, 8, hipMemcpyDeviceToHost));
-        build = vs == 0;
-    }
+    const bool build = total > 0 && (size_t)total * 8 <= free_b / 4;
     if (!build) {
         g->poff.reset();
         g->ppre.reset();
@@ -1646,16 +1636,14 @@ static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_
     }
     HIPCHK(g->pmask.alloc((size_t)total));
     HIPCHK(hipMemsetAsync(g->pmask.p, 0, (size_t)total * 8, s));
-    int64_t pb, pe;
-    prep_range(g, pb, pe);
-    if (pe > pb) {
-        const int64_t nb = std::min<int64_t>(pe - pb, (int64_t)ctx->num_cu * 16);
+    const int64_t N = g->nnodes;
+    if (N > 0) {
+        const int64_t nb = std::min<int64_t>(N, (int64_t)ctx->num_cu * 16);
         hipLaunchKernelGGL(tile_pmask_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), 0, s, rows, tw, th,
-                           g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb, g->pool.p,
-                           g->tvis.p, g->ftvis.p, g->poff.p, g->pmask.p);
+                           g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, g->tvis.p,
+                           g->ftvis.p, g->poff.p, g->pmask.p);
         HIPCHK(hipGetLastError());
     }
-    if (int rc = prep_allreduce(g, g->pmask.p, total, DMX_I64)) return rc;
     return DMX_OK;
 }
 

@@ -29,6 +29,10 @@ constexpr int KH = 8;        // head runs per cell (first KH entries of its scan
 #ifndef DMX_VGA_HV_FIRST
 #define DMX_VGA_HV_FIRST 1
 #endif
+// PPRE_EARLY: phase C loads a row word's partial-tile prefix with the word itself
+#ifndef DMX_VGA_PPRE_EARLY
+#define DMX_VGA_PPRE_EARLY 0
+#endif
 constexpr int CRK = 4;       // tile-common runs per tile
 constexpr int BEXT_DEFAULT = 4;   // runs after the heads a cell scans on its own lane before going wave-cooperative
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
@@ -477,13 +481,21 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
     const int tvw = P.tvw, tw = P.tw, wr = (P.tw + 63) / 64;
     const size_t row = (size_t)id * tvw;
     unsigned long long pw[4], cw[4];
+    int base[4];
     bool cert = false;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int w = k * 64 + lane;
         const unsigned long long fs = w < tvw ? Fsr[w] : 0ull;
         unsigned long long t = 0ull, f = 0ull;
-        if (fs) { t = P.tvis[row + w]; f = P.ftvis[row + w]; }
+        base[k] = 0;
+        if (fs) {
+            t = P.tvis[row + w];
+            f = P.ftvis[row + w];
+#if DMX_VGA_PPRE_EARLY
+            base[k] = (int)P.ppre[row + w];   // with the rows: one round trip fewer for an undecided cell
+#endif
+        }
         cert |= (f & fs) != 0ull;
         pw[k] = t & ~f;
         cw[k] = pw[k] & fs;
@@ -491,9 +503,10 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
     if (__ballot(cert) != 0ull) { how = 1; return true; }
     if (__ballot((cw[0] | cw[1] | cw[2] | cw[3]) != 0ull) == 0ull) { how = 2; return false; }
     how = 0;
-    int base[4];
+#if !DMX_VGA_PPRE_EARLY
 #pragma unroll
     for (int k = 0; k < 4; k++) base[k] = cw[k] ? (int)P.ppre[row + k * 64 + lane] : 0;
+#endif
     const unsigned long long* pm = P.pmask + P.poff[id];
 #pragma unroll 1
     for (int k = 0; k < 4; k++) {

@@ -19,4 +19,10 @@ t1=$(date +%s.%N) && echo "bench wall s: $(python -c "print($t1 - $t0)")" >> $OU
 timeout -k 10 1000 python -u -m pytest tests -x -v -m gpu --timeout 400 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
 rc=$?
 tail -1 $OUT/smoke.log; grep '^{' $OUT/bench.log | cut -c1-250; tail -1 $OUT/bench_progress.txt; tail -2 $OUT/pytest_gpu.log
+# A/B probe of the next variant after the evidence (EXTRA_LIB under depthmapx_amd/_lib_ab/)
+if [ $rc -eq 0 ] && [ -n "$EXTRA_LIB" ]; then
+  timeout -k 10 200 python -u scripts/probe_vga_time.py --reps 1 >> $OUT/ab.log 2>> $OUT/ab.err && \
+  DMX_LIB=depthmapx_amd/_lib_ab/$EXTRA_LIB/libdmx.so timeout -k 10 200 python -u scripts/probe_vga_time.py --reps 1 >> $OUT/ab.log 2>> $OUT/ab.err
+  cut -c1-200 $OUT/ab.log
+fi
 exit $rc
