@@ -34,7 +34,7 @@ constexpr int KH = 8;        // head runs per cell (first KH entries of its scan
 #define DMX_VGA_PPRE_EARLY 0
 #endif
 constexpr int CRK = 4;       // tile-common runs per tile
-constexpr int BEXT_DEFAULT = 4;   // runs after the heads a cell scans on its own lane before going wave-cooperative
+constexpr int BEXT_DEFAULT = 0;   // scan-order runs past the KH heads phase B tests (final build: 0 -1.4 % vs 4, profiles/r3b_vga_env)
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
 
 struct VgaTileParams {

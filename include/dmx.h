@@ -164,7 +164,11 @@ int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const*
  * (dmx_graph_assemble_device for shards).  out: host [N][7] or device (dmx_vga_global_device), rows
  * outside the range untouched, columns in table (alphabetical) order: Visual Entropy, Visual
  * Integration [HH], [P-value], [Tekl], Visual Mean Depth, Visual Node Count, Visual Relativised
- * Entropy.  levels (optional, host [N][3]): total nodes, total depth, BFS levels. */
+ * Entropy.  levels (optional, host [N][3]): total nodes, total depth, BFS levels.
+ * The first call on a graph builds its search structures (scan order, tile-visibility rows and, when
+ * they take at most a quarter of the free device memory, the partial-tile masks: about 50 GB next to
+ * the 36 GB graph at 1000^2); they stay with the graph until dmx_graph_free.  Results do not depend on
+ * which of them fit. */
 int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin, int64_t src_end,
                    float* out, int64_t* levels);
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin,

@@ -4,7 +4,7 @@
 set -o pipefail
 O=gpurun_out/${TAG:-vga_env}
 mkdir -p $O
-export DMX_LIB=depthmapx_amd/_lib_ab/${LIBV:-pmh}/libdmx.so
+if [ -n "$LIBV" ] && [ "$LIBV" != "none" ]; then export DMX_LIB=depthmapx_amd/_lib_ab/$LIBV/libdmx.so; fi
 IFS=';' read -ra SETS <<< "${ENVS:-DMX_VGA_BEXT=4}"
 for e in "${SETS[@]}"; do
   env $e timeout -k 10 200 python -u scripts/probe_vga_time.py --reps 1 >> $O/ab.log 2>> $O/ab.err || exit 1
