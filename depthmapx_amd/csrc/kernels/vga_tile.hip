@@ -33,6 +33,10 @@ constexpr int KH = 8;        // head runs per cell (first KH entries of its scan
 #ifndef DMX_VGA_PPRE_EARLY
 #define DMX_VGA_PPRE_EARLY 0
 #endif
+// HEADS8_EARLY: phase B loads heads 4..7 with the hint's operand instead of after the first 4 head tests
+#ifndef DMX_VGA_HEADS8_EARLY
+#define DMX_VGA_HEADS8_EARLY 0
+#endif
 constexpr int CRK = 4;       // tile-common runs per tile
 constexpr int BEXT_DEFAULT = 0;   // scan-order runs past the KH heads phase B tests (final build: 0 -1.4 % vs 4, profiles/r3b_vga_env)
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
@@ -855,6 +859,16 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (hp >= KH && hp < (uint32_t)nr) {
                             hr = P.scan_pool[ss + hp];
                         }
+#if DMX_VGA_HEADS8_EARLY
+                        // heads 4..7 loaded with the hint's operand (they do not depend on anything): the
+                        // extension tests below need no further round trip
+                        Run h2[4];
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            if (KH0 + r < min(nr, KH)) h2[r] = P.heads[(KH0 + r) * hstride + id];
+                            else h2[r].x0 = -1;
+                        }
+#endif
 #if DMX_VGA_HINT_BEFORE_DIAG
                         // row / column heads, then the hint, then the diagonal heads (the heads are stored row /
                         // column runs first, HV_FIRST): a diagonal test walks the run's tiles
@@ -922,7 +936,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
 #pragma unroll
                             for (int j = 0; j < 4; j++) {
                                 const int r = base + j;
+#if DMX_VGA_HEADS8_EARLY && DMX_VGA_B_ORDER
+                                if (r < KH) rr[j] = (base == KH0) ? h2[j] : P.heads[r * hstride + id];
+#else
                                 if (r < KH) rr[j] = P.heads[r * hstride + id];
+#endif
                                 else if (r < lim) rr[j] = P.scan_pool[ss + r];
                                 else rr[j].x0 = -1;
                             }
