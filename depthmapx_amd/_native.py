@@ -29,6 +29,8 @@ SIGNATURES = {
     "dmx_pointmap_free": (_i32, [_vp]),
     "dmx_pointmap_fill": (_i32, [_vp, _dbl, _dbl, _vp]),
     "dmx_pointmap_fill_device": (_i32, [_vp, _vp, _dbl, _dbl, _vp]),
+    "dmx_pointmap_make_points": (_i32, [_vp, _dbl, _dbl, _i32, _vp]),
+    "dmx_pointmap_make_points_device": (_i32, [_vp, _vp, _dbl, _dbl, _i32, _vp]),
     "dmx_ctx_last_fill": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_pointmap_info": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "dmx_pointmap_state": (_i32, [_vp, _vp]),

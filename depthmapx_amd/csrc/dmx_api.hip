@@ -227,8 +227,9 @@ struct dmx_graph {
     // prepare_merges for the searches that follow them
     std::vector<int32_t> merges;
     bool merges_ready = false;
-    bool merge_ctxfill = false;      // a merge cell is CONTEXTFILLED
     DevBuf<int2> d_mpairs;           // [m] (a, b) cells
+    DevBuf<int2> d_mamb;             // links with exactly one end context-filled at an odd PixelRef: (that end, the other)
+    int nmamb = 0;
     DevBuf<int32_t> d_merge_cell;    // [C] partner cell or -1
     int64_t nnodes = 0, node_begin = 0, node_end = 0;
     int64_t nruns = 0;
@@ -286,46 +287,47 @@ void inherit_merges(dmx_graph* g) {
 }
 
 // Device copies of the merge links for the searches; every linked cell must hold a node (the reference
-// calls getNode() on the partner, vgavisualglobal.cpp:116-118).
+// calls getNode() on the partner, vgavisualglobal.cpp:116-118).  Links with exactly one end CONTEXTFILLED at
+// an odd PixelRef are also listed end-first (d_mamb): where the analysis does not expand that end (a radius,
+// visual step depth) a source that finds both ends at one level gets the reference's result only in one pop
+// order (merge_order_check, vsd_merge_kernel), and such a source is refused rather than guessed.
 int prepare_merges(dmx_graph* g) {
     if (!g || g->merges_ready || g->merges.empty()) return DMX_OK;   // (a NULL graph fails in the caller)
     HIPCHK(hipSetDevice(g->ctx->device));
     const PointMapHost& h = *g->pm->host;
     const int64_t C = h.cells(), m = (int64_t)g->merges.size() / 2;
     const auto& st = h.state();
+    const int rows = h.rows();
+    auto cf_odd = [&](int32_t c) {
+        const int x = c / rows, y = c % rows;
+        return (st[c] & CELL_CONTEXTFILLED) && !((x % 2) == 0 && (y % 2) == 0);
+    };
     std::vector<int32_t> per_cell((size_t)C, -1);
-    std::vector<int2> pairs((size_t)m);
-    g->merge_ctxfill = false;
+    std::vector<int2> pairs((size_t)m), amb;
     for (int64_t i = 0; i < m; i++) {
         const int32_t a = g->merges[2 * i], b = g->merges[2 * i + 1];
         if (!(st[a] & CELL_FILLED) || !(st[b] & CELL_FILLED)) return fail(DMX_ERR_ARG, "merge link to a cell without a node");
-        if ((st[a] | st[b]) & CELL_CONTEXTFILLED) g->merge_ctxfill = true;
         per_cell[a] = b;
         per_cell[b] = a;
         pairs[i] = make_int2(a, b);
+        if (cf_odd(a) != cf_odd(b)) amb.push_back(cf_odd(a) ? make_int2(a, b) : make_int2(b, a));
     }
     HIPCHK(g->d_mpairs.alloc(m));
     HIPCHK(g->d_merge_cell.alloc(C));
     HIPCHK(hipMemcpyAsync(g->d_mpairs.p, pairs.data(), m * sizeof(int2), hipMemcpyHostToDevice, g->ctx->stream));
     HIPCHK(hipMemcpyAsync(g->d_merge_cell.p, per_cell.data(), C * 4, hipMemcpyHostToDevice, g->ctx->stream));
+    g->nmamb = (int)amb.size();
+    if (g->nmamb) {
+        HIPCHK(g->d_mamb.alloc(amb.size()));
+        HIPCHK(hipMemcpyAsync(g->d_mamb.p, amb.data(), amb.size() * sizeof(int2), hipMemcpyHostToDevice, g->ctx->stream));
+    }
     HIPCHK(hipStreamSynchronize(g->ctx->stream));
     g->merges_ready = true;
     return DMX_OK;
 }
 
-// Merge links whose outcome depends on the reference's pop order within a BFS level: a partner that is
-// CONTEXTFILLED at an odd PixelRef is counted/extracted or not depending on which end is popped first
-// when the analysis does not expand such cells (VGA global with a radius, visual step depth:
-// vgavisualglobal.cpp:104-122, vgavisualglobaldepth.cpp:52-63).  Only SEMIFILL (the GUI's context fill)
-// makes such cells; these maps are refused rather than analysed with a guessed order.
-int refuse_ordered_merges(dmx_graph* g, bool contextfill_limits_expansion) {
-    if (!g || g->merges.empty() || !contextfill_limits_expansion) return DMX_OK;
-    if (int rc = prepare_merges(g)) return rc;
-    if (g->merge_ctxfill)
-        return fail(DMX_ERR_UNSUPPORTED, "merge links on context-filled cells make this analysis depend on the "
-                                         "reference's pop order");
-    return DMX_OK;
-}
+const char* const k_order_msg = "merge links on context-filled cells: a search found both ends of such a link at one "
+                                "level, where the reference's result depends on which it pops first";
 
 int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     PointMapHost& h = *pm->host;
@@ -412,9 +414,11 @@ __global__ void gather_runs_kernel(const Run* pool, const int64_t* start, const 
 // m_merge on both points), every cell belongs to at most one pair (PointMap::mergePixels,
 // pointdata.cpp:1653-1680, unlinks a cell's previous partner).  per_cell[c] = partner or -1.
 int normalize_merges(int64_t C, const int32_t* pairs, int64_t n, std::vector<int32_t>& per_cell,
-                     std::vector<int32_t>& uniq) {
+                     std::vector<int32_t>& uniq, bool both_ways = false) {
     per_cell.assign(n ? (size_t)C : 0, -1);
     uniq.clear();
+    std::vector<int32_t> from;   // both_ways: the partner each cell's own entry names
+    if (both_ways && n) from.assign((size_t)C, -1);
     for (int64_t i = 0; i < n; i++) {
         const int32_t a = pairs[2 * i], b = pairs[2 * i + 1];
         if (a < 0 || b < 0 || a >= C || b >= C || a == b) return fail(DMX_ERR_ARG, "merge link outside the grid");
@@ -423,7 +427,15 @@ int normalize_merges(int64_t C, const int32_t* pairs, int64_t n, std::vector<int
         if (per_cell[a] < 0) { uniq.push_back(std::min(a, b)); uniq.push_back(std::max(a, b)); }
         per_cell[a] = b;
         per_cell[b] = a;
+        if (both_ways) from[a] = b;
     }
+    // a saved map stores a link on both points (PointMap::mergePixels sets m_merge on each, pointdata.cpp:
+    // 1653-1680), and the searches follow the merge pixel of the point they pop (vgavisualglobal.cpp:113): a
+    // link stored on one end only would be followed one way by the reference -- refused, not made two-way
+    if (both_ways)
+        for (size_t i = 0; i < uniq.size(); i += 2)
+            if (from[uniq[i]] != uniq[i + 1] || from[uniq[i + 1]] != uniq[i])
+                return fail(DMX_ERR_ARG, "a merge link stored on one of its points only (damaged map)");
     return DMX_OK;
 }
 
@@ -615,13 +627,22 @@ int dmx_pointmap_free(dmx_pointmap* pm) {
     return DMX_OK;
 }
 
-int dmx_pointmap_fill(dmx_pointmap* pm, double x, double y, int* made) {
+int dmx_pointmap_make_points(dmx_pointmap* pm, double x, double y, int fill_type, int* made) {
     if (!pm) return fail(DMX_ERR_ARG, "pointmap is NULL");
-    int r = pm->host->fill(x, y);
+    if (made) *made = 0;
+    if (PointMapHost::fill_state_of(fill_type) < 0) return fail(DMX_ERR_ARG, "fill_type must be 0, 1 or 2");
+    int r = pm->host->fill(x, y, fill_type);
     pm->version++;
     if (made) *made = (r == 0);
     if (r == 1) return fail(DMX_ERR_OUTSIDE, "Point outside of target region");
+    if (r == 3)
+        return fail(DMX_ERR_UNSUPPORTED, "an AUGMENT fill from this seed never ends in the reference (expand re-queues "
+                                         "augmented cells, pointdata.cpp:489)");
     return DMX_OK;
+}
+
+int dmx_pointmap_fill(dmx_pointmap* pm, double x, double y, int* made) {
+    return dmx_pointmap_make_points(pm, x, y, 0, made);
 }
 
 namespace {
@@ -661,9 +682,17 @@ unsigned fill_blocks(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + FIL
 // level-synchronous flood fill.  The host model stays the owner of the results (cell states,
 // cropped pieces), so makeGraph and the .graph writer see exactly what the host fill would leave.
 int dmx_pointmap_fill_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y, int* made) {
+    return dmx_pointmap_make_points_device(ctx, pm, x, y, 0, made);
+}
+
+int dmx_pointmap_make_points_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y, int fill_type, int* made) {
     if (!ctx || !pm) return fail(DMX_ERR_ARG, "bad arguments");
     PointMapHost& h = *pm->host;
     if (made) *made = 0;
+    const int32_t fill_state = PointMapHost::fill_state_of(fill_type);
+    if (fill_state < 0) return fail(DMX_ERR_ARG, "fill_type must be 0, 1 or 2");
+    // AUGMENT changes the seed cell alone or never ends (PointMapHost::fill): nothing to flood
+    if (fill_state == CELL_AUGMENTED) return dmx_pointmap_make_points(pm, x, y, fill_type, made);
     int sx = 0, sy = 0;
     const int r = h.fill_seed(x, y, &sx, &sy);
     if (r == 1) return fail(DMX_ERR_OUTSIDE, "Point outside of target region");
@@ -754,7 +783,8 @@ int dmx_pointmap_fill_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y,
     HIPCHK(children.alloc(C));
     HIPCHK(hipMemsetAsync(owner.p, 0xFF, C * sizeof(uint32_t), st));
     const int64_t c0 = h.index(sx, sy);
-    const int32_t seed_state = CELL_FILLED | (h.state()[c0] & CELL_BLOCKED);
+    G.fill_state = fill_state;
+    const int32_t seed_state = fill_state | (h.state()[c0] & CELL_BLOCKED);
     const int32_t seed_cell = (int32_t)c0;
     HIPCHK(hipMemcpyAsync(d_state.p + c0, &seed_state, sizeof(int32_t), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(layer[0].p, &seed_cell, sizeof(int32_t), hipMemcpyHostToDevice, st));
@@ -849,13 +879,13 @@ int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, i
 typedef void (*mk_kernel_t)(const MakeGraphParams*);
 #define MKK(PROF, FIXED, COUNT, MAXD, FAR) makegraph_kernel<5, PROF, FIXED, COUNT, MAXD, FAR>
 static mk_kernel_t mk_kernel(bool fixed, bool count, bool maxd, bool far) {
+    if (count) {       // the cost sample of dmx_makegraph_balance: always counts (its bounds depend on it)
+        if (!fixed || maxd) return MKK(false, false, true, false, false);
+        return far ? MKK(false, true, true, false, true) : MKK(false, true, true, false, false);
+    }
     if (verbose()) {   // per-phase clocks (maxdist runs take the generic kernel)
         if (!fixed || maxd) return MKK(true, false, false, false, false);
         return far ? MKK(true, true, false, false, true) : MKK(true, true, false, false, false);
-    }
-    if (count) {       // the cost sample of dmx_makegraph_balance
-        if (!fixed || maxd) return MKK(false, false, true, false, false);
-        return far ? MKK(false, true, true, false, true) : MKK(false, true, true, false, false);
     }
     if (!fixed) return MKK(false, false, false, false, false);
     if (maxd) return far ? MKK(false, true, false, true, true) : MKK(false, true, false, true, false);
@@ -1147,6 +1177,7 @@ int dmx_makegraph_balance(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
     for (int64_t j = 0; j < ns; j++) sample[j] = std::min<int64_t>(N - 1, j * stride + stride / 2);
     DevBuf<uint32_t> d_work;
     HIPCHK(d_work.alloc((size_t)N * 2));
+    HIPCHK(hipMemsetAsync(d_work.p, 0xFF, (size_t)N * 2 * 4, ctx->stream));   // unwritten entries stay ~0u
     dmx_graph* g = nullptr;
     rc = makegraph_impl(ctx, pm, maxdist, 0, 0, N, &sample, d_work.p, &g);   // boundary already applied
     if (rc) return rc;
@@ -1157,6 +1188,8 @@ int dmx_makegraph_balance(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
     std::vector<double> cum((size_t)ns + 1, 0.0);
     for (int64_t j = 0; j < ns; j++) {
         const int64_t v = sample[j];
+        if (w2[2 * v] == ~0u || w2[2 * v + 1] == ~0u)
+            return fail(DMX_ERR_STATE, "internal: the makeGraph cost sample did not record every sampled source");
         const double w = kMkSourceCost + (double)w2[2 * v] + kMkChunkCost * (double)w2[2 * v + 1];
         const int64_t cnt = std::min<int64_t>(N, (j + 1) * stride) - j * stride;
         cum[j + 1] = cum[j] + w * (double)cnt;
@@ -1767,7 +1800,13 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     DevBuf<uint32_t> hint;
     HIPCHK(hint.alloc((size_t)nt * 64));
     HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
+    DevBuf<int32_t> mseen;   // per workgroup: merge_order_check stamps
     VgaTileParams P = Q;
+    if (Q.nmamb) {
+        HIPCHK(mseen.alloc((size_t)blocks * Q.nmamb));
+        HIPCHK(hipMemsetAsync(mseen.p, 0, (size_t)blocks * Q.nmamb * 4, ctx->stream));
+        P.mseen = mseen.p;
+    }
     P.xg = xg.p;
     P.queue = queue.p;
     P.list = list.p;
@@ -1845,6 +1884,9 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.seeds = d_seeds; Q.nseeds = nseeds; Q.cell_level = d_cell_level;
     Q.nmp = (int)(g->merges.size() / 2);
     Q.mpairs = Q.nmp ? g->d_mpairs.p : nullptr;
+    Q.nmamb = Q.nmp && radius != -1.0 ? g->nmamb : 0;
+    Q.mamb = Q.nmamb ? g->d_mamb.p : nullptr;
+    Q.mseen = nullptr;
     Q.src_list = d_src_list;   // [sb, se) index this list of source nodes (out must be on the device)
     // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
     Q.alpha = 60;   // top-down costs a frontier cell its whole run list (~R/N runs): keep it rare
@@ -1904,6 +1946,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_vga_s = ms * 1e-3;
     int hc[2];
     HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+    if (hc[1] & KERR_ORDER) return fail(DMX_ERR_UNSUPPORTED, k_order_msg);
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level capacity");
     unsigned long long st[32];
     HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
@@ -2034,6 +2077,14 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     Q.nmp = (int)(g->merges.size() / 2);
     Q.mpairs = Q.nmp ? g->d_mpairs.p : nullptr;
     if (!use_do && Q.nmp) return fail(DMX_ERR_UNSUPPORTED, "the top-down v1 kernel does not follow merge links");
+    Q.nmamb = Q.nmp && radius != -1.0 ? g->nmamb : 0;
+    Q.mamb = Q.nmamb ? g->d_mamb.p : nullptr;
+    DevBuf<int32_t> mseen;
+    if (Q.nmamb) {
+        HIPCHK(mseen.alloc((size_t)blocks * Q.nmamb));
+        HIPCHK(hipMemsetAsync(mseen.p, 0, (size_t)blocks * Q.nmamb * 4, ctx->stream));
+        Q.mseen = mseen.p;
+    }
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (nsrc > 0) {
         if (gbm) hipLaunchKernelGGL(vga_do_kernel<true>, dim3((unsigned)blocks), dim3(DO_THREADS), lds, ctx->stream, Q);
@@ -2050,6 +2101,7 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     ctx->last_vga_s = ms * 1e-3;
     int hc[2];
     HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
+    if (hc[1] & KERR_ORDER) return fail(DMX_ERR_UNSUPPORTED, k_order_msg);
     if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level/frontier capacity");
     unsigned long long st[8];
     HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
@@ -2072,7 +2124,6 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
 int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
                    int64_t* levels) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_ordered_merges(g, radius != -1.0)) return rc;
     if (int rc = prepare_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out, false, levels);
 }
@@ -2080,7 +2131,6 @@ int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, in
 int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se,
                           float* out_device) {
     SAME_DEVICE(ctx, g);
-    if (int rc = refuse_ordered_merges(g, radius != -1.0)) return rc;
     if (int rc = prepare_merges(g)) return rc;
     return vga_impl(ctx, g, radius, gates_only, sb, se, out_device, true, nullptr);
 }
@@ -2092,7 +2142,6 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
                                int64_t n, float* out_device) {
     SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out_device || (n > 0 && !nodes)) return fail(DMX_ERR_ARG, "bad arguments");
-    if (int rc = refuse_ordered_merges(g, radius != -1.0)) return rc;
     if (int rc = prepare_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
@@ -2622,9 +2671,17 @@ static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vecto
     const int64_t C = h.cells(), N = g->nnodes, nt = (int64_t)tw * th;
     hipStream_t s = ctx->stream;
     DevBuf<unsigned long long> vis, cnt;
-    DevBuf<int32_t> level, fr[2];
+    DevBuf<int32_t> level, fr[2], pend[2];
+    DevBuf<int> err;
     HIPCHK(vis.alloc(nt));
-    HIPCHK(cnt.alloc(1));
+    HIPCHK(cnt.alloc(2));   // next frontier, pending extractions
+    HIPCHK(err.alloc(1));
+    HIPCHK(hipMemsetAsync(err.p, 0, sizeof(int), ctx->stream));
+    const int nmp = (int)(g->merges.size() / 2);
+    if (g->nmamb) {
+        HIPCHK(pend[0].alloc(g->nmamb));
+        HIPCHK(pend[1].alloc(g->nmamb));
+    }
     HIPCHK(level.alloc(C));
     HIPCHK(fr[0].alloc(std::max<int64_t>(N, 1)));
     HIPCHK(fr[1].alloc(std::max<int64_t>(N, 1)));
@@ -2639,28 +2696,37 @@ static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vecto
     HIPCHK(hipMemcpyAsync(level.p, lv.data(), C * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipMemcpyAsync(fr[0].p, seeds.data(), seeds.size() * 4, hipMemcpyHostToDevice, s));
     HIPCHK(hipEventRecord(ctx->ev0, s));
-    int64_t nf = (int64_t)seeds.size();
+    int64_t nf = (int64_t)seeds.size(), npend = 0;
     int cur = 0, L = 0;
     while (nf > 0) {
-        HIPCHK(hipMemsetAsync(cnt.p, 0, 8, s));
+        HIPCHK(hipMemsetAsync(cnt.p, 0, 16, s));
         const int64_t blocks = std::min<int64_t>((nf + 3) / 4, (int64_t)ctx->num_cu * 16);
         hipLaunchKernelGGL(vsd_level_kernel, dim3((unsigned)blocks), dim3(VSD_THREADS), 0, s, rows, tw,
                            (const int32_t*)fr[cur].p, nf, g->node_run_start.p, g->node_nruns.p, g->pool.p,
                            g->pm->d_cell_node.p, g->pm->d_node_flags.p, L + 1, vis.p, level.p, fr[cur ^ 1].p, cnt.p);
         HIPCHK(hipGetLastError());
-        if (!g->merges.empty()) {
-            const int nmp = (int)(g->merges.size() / 2);
+        if (nmp) {
             hipLaunchKernelGGL(vsd_merge_kernel, dim3((unsigned)((nmp + 255) / 256)), dim3(256), 0, s, rows, tw,
-                               (const int2*)g->d_mpairs.p, nmp, g->pm->d_cell_node.p, L + 1, vis.p, level.p,
-                               fr[cur ^ 1].p, cnt.p);
+                               (const int2*)g->d_mpairs.p, nmp, g->pm->d_cell_node.p, g->pm->d_node_flags.p, L + 1,
+                               vis.p, level.p, fr[cur ^ 1].p, cnt.p, pend[cur ^ 1].p, cnt.p + 1);
             HIPCHK(hipGetLastError());
         }
-        unsigned long long n_next = 0;
-        HIPCHK(copy_sync(s, &n_next, cnt.p, 8, hipMemcpyDeviceToHost));
+        if (npend) {   // the previous level's pending extractions, now that this level is complete
+            hipLaunchKernelGGL(vsd_pending_kernel, dim3((unsigned)((npend + 3) / 4)), dim3(VSD_THREADS), 0, s, rows, tw,
+                               (const int32_t*)pend[cur].p, npend, g->node_run_start.p, g->node_nruns.p, g->pool.p,
+                               g->pm->d_cell_node.p, (const unsigned long long*)vis.p, err.p);
+            HIPCHK(hipGetLastError());
+        }
+        unsigned long long n_next[2] = {0, 0};
+        HIPCHK(copy_sync(s, n_next, cnt.p, 16, hipMemcpyDeviceToHost));
         cur ^= 1;
-        nf = (int64_t)n_next;
+        nf = (int64_t)n_next[0];
+        npend = (int64_t)n_next[1];
         L++;
     }
+    int herr = 0;
+    HIPCHK(copy_sync(s, &herr, err.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (herr & KERR_ORDER) return fail(DMX_ERR_UNSUPPORTED, k_order_msg);
     HIPCHK(hipEventRecord(ctx->ev1, s));
     HIPCHK(copy_sync(s, lv.data(), level.p, C * 4, hipMemcpyDeviceToHost));
     float ms = 0;
@@ -2677,7 +2743,6 @@ static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vecto
 int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     SAME_DEVICE(ctx, g);
     if (!ctx || !g || !out || (nsel > 0 && !sel_cells)) return fail(DMX_ERR_ARG, "bad arguments");
-    if (int rc = refuse_ordered_merges(g, true)) return rc;
     if (int rc = prepare_merges(g)) return rc;
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "step depth needs the whole graph (assemble the shards first)");
@@ -2722,7 +2787,8 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
         std::sort(seeds.begin() + 1, seeds.end());   // seeds[0] stays the first selected cell
     }
     const int tw = (cols + 7) / 8, th = (rows + 7) / 8, nt = tw * th;
-    bool tile = nt <= 16 * 1024 && !getenv("DMX_VSD_TOPDOWN");
+    // links with a context-filled odd end need the top-down search's pending-extraction check
+    bool tile = nt <= 16 * 1024 && !getenv("DMX_VSD_TOPDOWN") && g->nmamb == 0;
     int rc = DMX_OK;
     if (tile) {
         rc = prepare_uf(g);
@@ -2936,8 +3002,13 @@ int dmx_chunk_load(dmx_ctx* ctx, const dmx_chunk* c, const double* region, dmx_p
                                  p.gridconn.data(), attrs.data(), &g);
     if (rc) return rc;
     std::unique_ptr<dmx_graph> gg(g);
-    rc = dmx_pointmap_set_merges(pm.get(), p.merge_pairs.data(), (int64_t)p.merge_pairs.size() / 2);
-    if (rc) return rc;
+    {
+        std::vector<int32_t> per_cell, uniq;
+        rc = normalize_merges(pm->host->cells(), p.merge_pairs.data(), (int64_t)p.merge_pairs.size() / 2, per_cell, uniq,
+                              true);
+        if (rc) return rc;
+        pm->host->set_merge(std::move(per_cell));
+    }
     inherit_merges(g);
     *pm_out = pm.release();
     *g_out = gg.release();
@@ -2956,6 +3027,9 @@ int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n) {
     if (!g || n < 0 || (n && !cell_pairs)) return fail(DMX_ERR_ARG, "bad arguments");
     std::vector<int32_t> per_cell, uniq;
     if (int rc = normalize_merges(g->pm->host->cells(), cell_pairs, n, per_cell, uniq)) return rc;
+    // the links belong to the points (Point::m_merge): the map gets them too, so a chunk written from it
+    // saves them and a graph made from it again follows them
+    g->pm->host->set_merge(std::move(per_cell));
     g->merges = std::move(uniq);
     g->merges_ready = false;
     return DMX_OK;
@@ -2966,7 +3040,7 @@ int dmx_chunk_merges(const dmx_chunk* c, int32_t* cell_pairs, int64_t* n) {
     std::vector<int32_t> per_cell, uniq;
     const ParsedChunk& p = c->pc;
     if (int rc = normalize_merges((int64_t)p.cols * p.rows, p.merge_pairs.data(), (int64_t)p.merge_pairs.size() / 2,
-                                  per_cell, uniq))
+                                  per_cell, uniq, true))
         return rc;
     const int64_t m = (int64_t)uniq.size() / 2;
     if (cell_pairs) {

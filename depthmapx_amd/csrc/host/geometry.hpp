@@ -125,7 +125,7 @@ DMX_HD int cvt_i32_x86(double v) { return (v >= -2147483648.0 && v < 2147483648.
 // Point::m_state bits (salalib/point.h:32-38).
 enum CellState : int32_t {
     CELL_EMPTY = 0x0001, CELL_FILLED = 0x0002, CELL_BLOCKED = 0x0004, CELL_CONTEXTFILLED = 0x0008,
-    CELL_SELECTED = 0x0010, CELL_EDGE = 0x0020, CELL_MERGED = 0x0040
+    CELL_SELECTED = 0x0010, CELL_EDGE = 0x0020, CELL_MERGED = 0x0040, CELL_AUGMENTED = 0x8000
 };
 
 } // namespace dmx

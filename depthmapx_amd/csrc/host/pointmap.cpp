@@ -136,7 +136,7 @@ void PointMapHost::block_lines() {
 }
 
 // PointMap::expand (pointdata.cpp:483-514): 1 off-grid, 2 already filled, 4 blocked, 8 filled now.
-int PointMapHost::expand(int x1, int y1, int x2, int y2, std::vector<int32_t>& next) {
+int PointMapHost::expand_test(int x1, int y1, int x2, int y2) const {
     if ((short)x2 < 0 || (short)x2 >= (short)cols_ || (short)y2 < 0 || (short)y2 >= (short)rows_) return 1;
     const int64_t c1 = index(x1, y1), c2 = index(x2, y2);
     if (state_[c2] & CELL_FILLED) return 2;
@@ -147,11 +147,38 @@ int PointMapHost::expand(int x1, int y1, int x2, int y2, std::vector<int32_t>& n
             Seg s = seg_at(k);
             if (rects_touch(l.r, s.r, tol) && segs_cross(l, s, tol)) return 4;
         }
-    state_[c2] = CELL_FILLED | (state_[c2] & CELL_BLOCKED); // Point::set keeps BLOCKED
+    return 8;
+}
+
+int PointMapHost::expand(int x1, int y1, int x2, int y2, std::vector<int32_t>& next) {
+    const int r = expand_test(x1, y1, x2, y2);
+    if (r != 8) return r;
+    const int64_t c2 = index(x2, y2);
+    state_[c2] = fill_state_ | (state_[c2] & CELL_BLOCKED); // Point::set keeps BLOCKED
     filled_++;
     next.push_back(x2);
     next.push_back(y2);
     return 8;
+}
+
+int32_t PointMapHost::fill_state_of(int fill_type) {
+    switch (fill_type) {
+    case 0: return CELL_FILLED;                       // FULLFILL
+    case 1: return CELL_FILLED | CELL_CONTEXTFILLED;  // SEMIFILL
+    case 2: return CELL_AUGMENTED;                    // AUGMENT
+    default: return -1;
+    }
+}
+
+// makePoints' expand order (pointdata.cpp:457-464): up, down, left, right, up-left, up-right, down-left,
+// down-right (PixelRef::up() is y+1).
+static const int k_expand_dx[8] = {0, 0, -1, 1, -1, 1, -1, 1};
+static const int k_expand_dy[8] = {1, -1, 0, 0, 1, 1, -1, -1};
+
+bool PointMapHost::seed_can_expand(int sx, int sy) const {
+    for (int k = 0; k < 8; k++)
+        if (expand_test(sx, sy, sx + k_expand_dx[k], sy + k_expand_dy[k]) == 8) return true;
+    return false;
 }
 
 int PointMapHost::fill_seed(double px, double py, int* psx, int* psy) const {
@@ -179,18 +206,38 @@ void PointMapHost::adopt_blocked(std::vector<int32_t>&& seg_off, std::vector<dou
 }
 
 void PointMapHost::adopt_state(std::vector<int32_t>&& state) {
+    // m_filled_point_count counts set() calls, not FILLED bits (an AUGMENT seed counts too): add the
+    // cells the adopted fill filled
+    int64_t before = 0, after = 0;
+    for (int32_t s : state_) before += (s & CELL_FILLED) ? 1 : 0;
+    for (int32_t s : state) after += (s & CELL_FILLED) ? 1 : 0;
     state_ = std::move(state);
-    filled_ = 0;
-    for (int32_t s : state_) filled_ += (s & CELL_FILLED) ? 1 : 0;
+    filled_ += after - before;
 }
 
-int PointMapHost::fill(double px, double py) {
+int PointMapHost::fill(double px, double py, int fill_type) {
+    const int32_t fs = fill_state_of(fill_type);
+    if (fs < 0) return 2;
     int sx = 0, sy = 0;
     const int r = fill_seed(px, py, &sx, &sy);
     if (r) return r;
     block_lines();
     int64_t c0 = index(sx, sy);
-    state_[c0] = CELL_FILLED | (state_[c0] & CELL_BLOCKED);
+    if (fs == CELL_AUGMENTED) {
+        // AUGMENT sets AUGMENTED without FILLED, and expand only stops at FILLED cells
+        // (pointdata.cpp:489): the first neighbour it fills re-queues the seed, which re-queues that
+        // neighbour, and the reference's loop never ends.  It ends only when the seed expands nowhere;
+        // then the seed alone is set (and counted, :444) and gets EDGE like any fill's cell (:466-468).
+        if (seed_can_expand(sx, sy)) return 3;
+        int res = 0;
+        for (int k = 0; k < 8; k++) res |= expand_test(sx, sy, sx + k_expand_dx[k], sy + k_expand_dy[k]);
+        state_[c0] = fs | (state_[c0] & CELL_BLOCKED);
+        filled_++;
+        if ((res & 4) || (state_[c0] & CELL_BLOCKED)) state_[c0] |= CELL_EDGE;
+        return 0;
+    }
+    fill_state_ = fs;
+    state_[c0] = fs | (state_[c0] & CELL_BLOCKED);
     filled_++;
     // pflipper flood fill: pop from the back of the current layer, push into the next layer
     std::vector<int32_t> layer[2];
@@ -200,20 +247,14 @@ int PointMapHost::fill(double px, double py) {
         int x = layer[cur][layer[cur].size() - 2], y = layer[cur].back();
         std::vector<int32_t>& nxt = layer[cur ^ 1];
         int res = 0;
-        res |= expand(x, y, x, y + 1, nxt);
-        res |= expand(x, y, x, y - 1, nxt);
-        res |= expand(x, y, x - 1, y, nxt);
-        res |= expand(x, y, x + 1, y, nxt);
-        res |= expand(x, y, x - 1, y + 1, nxt);
-        res |= expand(x, y, x + 1, y + 1, nxt);
-        res |= expand(x, y, x - 1, y - 1, nxt);
-        res |= expand(x, y, x + 1, y - 1, nxt);
+        for (int k = 0; k < 8; k++) res |= expand(x, y, x + k_expand_dx[k], y + k_expand_dy[k], nxt);
         int64_t c = index(x, y);
         if ((res & 4) || (state_[c] & CELL_BLOCKED)) state_[c] |= CELL_EDGE;
         layer[cur].pop_back();
         layer[cur].pop_back();
         if (layer[cur].empty()) cur ^= 1;
     }
+    fill_state_ = CELL_FILLED;
     return 0;
 }
 

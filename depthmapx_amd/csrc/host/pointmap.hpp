@@ -35,10 +35,18 @@ class PointMapHost {
     }
     Rect cell_rect(int x, int y, double border) const; // PointMap::regionate (pointdata.h:359-367)
 
-    // runmethods.cpp:269-277 fillGraph + PointMap::makePoints(seed, FULLFILL).
+    // runmethods.cpp:269-277 fillGraph + PointMap::makePoints(seed, fill_type) (pointdata.cpp:402-481).
+    // fill_type 0 FULLFILL (FILLED), 1 SEMIFILL (FILLED | CONTEXTFILLED), 2 AUGMENT (AUGMENTED: not
+    // FILLED, so the reference's expand re-queues every augmented neighbour and the fill only ends
+    // when the seed cannot expand at all; see fill()).
     // Returns 0 = filled, 1 = point outside region, 2 = makePoints refused (off-grid, already
-    // filled, or seed hidden from its cell centre).
-    int fill(double x, double y);
+    // filled, or seed hidden from its cell centre), 3 = an AUGMENT fill that would never end in the
+    // reference (nothing changed but the line blocking).
+    int fill(double x, double y, int fill_type = 0);
+    // Point::m_state a fill of this type sets (pointdata.cpp:434-441); -1 for an unknown type.
+    static int32_t fill_state_of(int fill_type);
+    // The AUGMENT pre-check: true if some neighbour of (sx, sy) passes PointMap::expand's tests.
+    bool seed_can_expand(int sx, int sy) const;
     // fill's checks on the seed alone (region, pixelate, already filled, seed hidden from its cell
     // centre once lines are blocked): 0 = a fill may start at cell (*sx, *sy), else fill's code.
     int fill_seed(double x, double y, int* sx, int* sy) const;
@@ -71,6 +79,7 @@ class PointMapHost {
   private:
     void rasterise(const Seg& l, std::vector<int32_t>& out) const;
     int expand(int x1, int y1, int x2, int y2, std::vector<int32_t>& next);
+    int expand_test(int x1, int y1, int x2, int y2) const;   // expand's result without filling
     Seg seg_at(int64_t k) const {
         return make_seg(Vec2{segs_[4 * k], segs_[4 * k + 1]}, Vec2{segs_[4 * k + 2], segs_[4 * k + 3]});
     }
@@ -86,6 +95,7 @@ class PointMapHost {
     std::vector<double> segs_;
     bool blocked_ = false;
     int64_t filled_ = 0;
+    int32_t fill_state_ = CELL_FILLED;   // the state the running fill sets
     std::vector<int32_t> merge_;
 };
 

@@ -18,6 +18,7 @@ enum KernelError : int {
     KERR_BIN_MISMATCH = 16,    // whichbin produced a bin outside the octant (should never happen)
     KERR_LEVELS = 32,          // BFS depth exceeded the level histogram
     KERR_FRONTIER = 64,        // BFS frontier buffer overflow
+    KERR_ORDER = 128,          // a merge-link outcome depends on the reference's pop order (merge_order_check)
 };
 
 // Per-cell word uploaded to HBM: bit 0 FILLED, bits 1..7 cropped-segment count (<=127),
@@ -101,6 +102,36 @@ __device__ __forceinline__ void merge_level_pass(const int2* mpairs, int nmp, in
                 atomicAdd(mass, 1ull);
             }
         }
+    }
+}
+
+// Merge links with one end context-filled at an odd PixelRef (a, not expanded under a radius) and the
+// other end b expandable.  When a source discovers both at the same level L (< radius), the reference's
+// outcome depends on which it pops first (vgavisualglobal.cpp:99-122): b first extracts a (a is not
+// counted, its runs feed L + 1); a first counts a and leaves it unexpanded.  The level-synchronous BFS
+// cannot tell, so such a source raises KERR_ORDER.  In every other case the merge pass above is exact: a
+// new at L is not in F (not expanded) and so extracts nothing, and b extracts an unvisited a into F.
+// Called after the merge pass of level L (F: the expandable cells new at L; V includes every cell new at
+// L).  mamb[k] = (a, b); mseen[k] (per workgroup, thread k's own slot across levels) holds the stamp of the
+// source for which a was found, so "a in V and not yet seen" means a is new at this level (the check runs
+// at every level from 1; a cell in V at level 0 -- a merge partner of the source -- has its partner at
+// level 0, not in F).  A cell never discoverable by runs (seed) is only ever reached through its link.
+__device__ __forceinline__ void merge_order_check(const int2* mamb, int nmamb, int rows, int tw, int ntpb,
+                                                  const unsigned long long* F, const unsigned long long* V,
+                                                  bool v_lds, const unsigned long long* seed_tiles, int32_t* mseen,
+                                                  int32_t stamp, int* error) {
+    for (int k = threadIdx.x; k < nmamb; k += ntpb) {
+        if (mseen[k] == stamp) continue;
+        const int2 pr = mamb[k];
+        const int ax = pr.x / rows, ay = pr.x % rows, bx = pr.y / rows, by = pr.y % rows;
+        const int at = (ay >> 3) * tw + (ax >> 3), bt = (by >> 3) * tw + (bx >> 3);
+        const unsigned long long ab = 1ull << ((ay & 7) * 8 + (ax & 7)), bb = 1ull << ((by & 7) * 8 + (bx & 7));
+        if (seed_tiles[at] & ab) continue;
+        const unsigned long long vw =
+            v_lds ? V[at] : __hip_atomic_load(&V[at], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!(vw & ab)) continue;
+        mseen[k] = stamp;
+        if ((F[bt] & bb) && !(F[at] & ab)) atomicOr(error, (int)KERR_ORDER);
     }
 }
 

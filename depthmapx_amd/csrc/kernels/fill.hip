@@ -40,6 +40,7 @@ struct FillGrid {
     double spacing;
     double blx, bly;   // bottom-left cell centre (m_bottom_left)
     Rect region;       // the grid region (m_region), for PixelBase::pixelateLineTouching's normalScale
+    int32_t fill_state = CELL_FILLED;   // Point::set's state for this fill: FILLED [| CONTEXTFILLED] (:434-441)
 };
 
 __device__ __forceinline__ Seg drawing_seg(const double* draw, int64_t k) {
@@ -237,7 +238,7 @@ __device__ __forceinline__ void fill_push_one(const FillGrid& G, int32_t* state,
     for (int k = 0; k < 8; k++) {
         if (!((ch >> k) & 1)) continue;
         const int64_t c2 = (int64_t)(x + c_fill_dx[k]) * G.rows + (y + c_fill_dy[k]);
-        state[c2] = CELL_FILLED | (state[c2] & CELL_BLOCKED);   // Point::set keeps BLOCKED
+        state[c2] = G.fill_state | (state[c2] & CELL_BLOCKED);   // Point::set keeps BLOCKED
         next[n_next - 1 - q] = (int32_t)c2;
         q++;
     }

@@ -55,6 +55,9 @@ struct VgaDoParams {
     unsigned long long* gbm;    // GBM variant: per workgroup 3*tw*th words (V, F, X) in HBM
     const int2* mpairs;         // [nmp] merge links (cell a, cell b), x-major (nullptr: none)
     int nmp;
+    const int2* mamb;           // [nmamb] links with a context-filled odd end (merge_order_check)
+    int nmamb = 0;
+    int32_t* mseen = nullptr;   // per workgroup [nmamb]
 };
 
 constexpr int DO_THREADS = 256;
@@ -401,6 +404,11 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                 __syncthreads();   // the new level is in F and V
                 merge_level_pass(P.mpairs, P.nmp, rows, tw, DO_THREADS, F, V, !GBM, P.seed_tiles, nullptr, nullptr, 0, 0,
                                  nullptr, level + 1, &S->mcorr, &S->mdisc, &S->mass);
+                if (P.nmamb) {
+                    __syncthreads();
+                    merge_order_check(P.mamb, P.nmamb, rows, tw, DO_THREADS, F, V, !GBM, P.seed_tiles,
+                                      P.mseen + (size_t)blockIdx.x * P.nmamb, (int32_t)src + 1, P.error);
+                }
             }
             __syncthreads();
             const long long cnt = (long long)S->cnt, mass = (long long)S->mass;

@@ -100,6 +100,9 @@ struct VgaTileParams {
     int crk;                  // tile-common runs tested in phase A (<= CRK)
     const int2* mpairs;       // [nmp] merge links (cell a, cell b), x-major (Point::m_merge; nullptr: none)
     int nmp;
+    const int2* mamb;         // [nmamb] links with a context-filled odd end (that end first; merge_order_check)
+    int nmamb;
+    int32_t* mseen;           // per workgroup [nmamb] (merge_order_check)
     int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
     int32_t* nlev_out;        // [N] levels (0: source skipped)
     int* error;
@@ -1247,6 +1250,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 __syncthreads();   // the new level is in F and V
                 merge_level_pass(P.mpairs, P.nmp, rows, tw, NT, F, Vg, false, P.seed_tiles, Fsr, RBM ? nullptr : Fsc, wr,
                                  wc, P.cell_level, level + 1, &S.mcorr, &S.mdisc, &S.mass);
+                if (P.nmamb && !seeded) {
+                    __syncthreads();
+                    merge_order_check(P.mamb, P.nmamb, rows, tw, NT, F, Vg, false, P.seed_tiles,
+                                      P.mseen + (size_t)blockIdx.x * P.nmamb, (int32_t)node + 1, P.error);
+                }
             }
             if (RBM && !rb_inc) {
                 // line-resolved summaries from the published frontier (plain stores, no atomics)

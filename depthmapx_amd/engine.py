@@ -141,15 +141,20 @@ class PointMap:
     def rows(self):
         return self.info()["rows"]
 
-    def make_points(self, x, y, ctx=None):
-        """runmethods fillGraph + PointMap::makePoints; raises DmxError(DMX_ERR_OUTSIDE) like the CLI's
-        'Point outside of target region'; returns False where makePoints returns false.  With a
-        Context the rasterisation and the flood fill run on its GPU (dmx_pointmap_fill_device)."""
+    FULLFILL, SEMIFILL, AUGMENT = 0, 1, 2   # QDepthmapView fill modes (depthmapview.h:75)
+
+    def make_points(self, x, y, ctx=None, fill_type=0):
+        """runmethods fillGraph + PointMap::makePoints(p, fill_type) (pointdata.cpp:402-481); raises
+        DmxError(DMX_ERR_OUTSIDE) like the CLI's 'Point outside of target region'; returns False where
+        makePoints returns false.  fill_type 1 (SEMIFILL) marks the cells CONTEXTFILLED; 2 (AUGMENT)
+        raises DMX_ERR_UNSUPPORTED where the reference's fill would never end.  With a Context the
+        rasterisation and the flood fill run on its GPU (dmx_pointmap_make_points_device)."""
         made = ctypes.c_int()
         if ctx is None:
-            N.check(N.lib().dmx_pointmap_fill(self.h, float(x), float(y), ctypes.byref(made)))
+            N.check(N.lib().dmx_pointmap_make_points(self.h, float(x), float(y), int(fill_type), ctypes.byref(made)))
         else:
-            N.check(N.lib().dmx_pointmap_fill_device(ctx.h, self.h, float(x), float(y), ctypes.byref(made)))
+            N.check(N.lib().dmx_pointmap_make_points_device(ctx.h, self.h, float(x), float(y), int(fill_type),
+                                                            ctypes.byref(made)))
         return bool(made.value)
 
     def state(self):

@@ -108,6 +108,17 @@ int dmx_pointmap_fill_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y,
 /* Seconds of the last dmx_pointmap_fill_device: blockLines (0 when lines were already blocked),
  * flood fill, and the number of fill levels. */
 int dmx_ctx_last_fill(dmx_ctx* ctx, double* block_s, double* fill_s, int64_t* levels);
+/* PointMap::makePoints(seed, fill_type) (salalib/pointdata.cpp:402-481; MetaGraph::makePoints,
+ * mgraph.cpp:237-247), the GUI's three fill modes (depthmapX/views/depthmapview/depthmapview.h:75):
+ * 0 FULLFILL (Point::FILLED, what the CLI uses), 1 SEMIFILL (FILLED | CONTEXTFILLED: such cells at odd
+ * PixelRefs are skipped as VGA sources and not expanded under a radius or in visual step depth), 2 AUGMENT
+ * (Point::AUGMENTED without FILLED).  The reference's AUGMENT fill only ends when the seed expands nowhere
+ * (expand stops at FILLED cells only, pointdata.cpp:489, so augmented neighbours re-queue each other
+ * forever): that case sets the seed alone, any other returns DMX_ERR_UNSUPPORTED with no cell filled
+ * (the occluders are blocked, as before any fill).
+ * The _device form runs FULLFILL / SEMIFILL on the context's GPU as dmx_pointmap_fill_device does. */
+int dmx_pointmap_make_points(dmx_pointmap* pm, double x, double y, int fill_type, int* made);
+int dmx_pointmap_make_points_device(dmx_ctx* ctx, dmx_pointmap* pm, double x, double y, int fill_type, int* made);
 /* Restore the FILLED / EDGE / CONTEXTFILLED cell states of a map saved earlier (e.g. the state
  * array of a PointMap chunk of the same grid), as PointMap::read does before makeGraph. */
 int dmx_pointmap_set_state(dmx_pointmap* pm, const int32_t* state);
@@ -166,7 +177,7 @@ int dmx_graph_assemble_device(dmx_ctx* ctx, dmx_pointmap* pm, const void* const*
  * Integration [HH], [P-value], [Tekl], Visual Mean Depth, Visual Node Count, Visual Relativised
  * Entropy.  levels (optional, host [N][3]): total nodes, total depth, BFS levels.
  * The first call on a graph builds its search structures (scan order, tile-visibility rows and, when
- * they take at most a quarter of the free device memory, the partial-tile masks: about 50 GB next to
+ * they take at most a quarter of the free device memory, the partial-tile masks: about 10 GB next to
  * the 36 GB graph at 1000^2); they stay with the graph until dmx_graph_free.  Results do not depend on
  * which of them fit. */
 int dmx_vga_global(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t src_begin, int64_t src_end,
@@ -280,9 +291,12 @@ int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const in
  * 113-122), visual step depth (vgavisualglobaldepth.cpp:55-63), metric / angular all sources
  * (vgametric.cpp:97-105, vgaangular.cpp:95-104) and metric / angular step depth (vgametricdepth.cpp:68-83,
  * vgaangulardepth.cpp:57-67).  Both ends must be filled cells of the graph (DMX_ERR_ARG at the analysis).
- * Links on CONTEXTFILLED cells make VGA global with a radius and visual step depth depend on the
- * reference's pop order inside a level; those two analyses return DMX_ERR_UNSUPPORTED on such maps.
- * VGA visual local has no merge logic. */
+ * A link with one end CONTEXTFILLED at an odd PixelRef is followed exactly, except where the reference's
+ * result depends on its pop order inside a level: VGA global with a radius where a source finds both ends
+ * at one level, and visual step depth where extracting the unexpanded end would reach a new cell -- those
+ * calls return DMX_ERR_UNSUPPORTED.  VGA visual local has no merge logic.  The links are set on the
+ * graph's point map as well (they belong to the points: a chunk written from it saves them).  A chunk
+ * (dmx_chunk_merges, dmx_chunk_load) must store every link on both of its points (DMX_ERR_ARG otherwise). */
 int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n);
 /* The same links on a point map: written into its PointMap chunk (Point::write, point.cpp:51-73) and
  * followed by the graphs made from it (dmx_makegraph, dmx_graph_assemble_device, dmx_graph_from_runs). */

@@ -18,7 +18,13 @@
 #define M_PI_ 3.14159265358979323846
 
 /* Point::m_state bits (salalib/point.h:32-38) */
-enum { ST_EMPTY = 0x1, ST_FILLED = 0x2, ST_BLOCKED = 0x4, ST_CONTEXTFILLED = 0x8, ST_EDGE = 0x20 };
+/* Test knob (dmxo_set_pop_forward): walk each BFS level front to back instead of the reference's back
+ * to front (rbegin, vgavisualglobal.cpp:99, vgavisualglobaldepth.cpp:46).  Used only to show which
+ * results depend on the pop order inside a level; 0 (the reference's order) by default. */
+static int g_pop_forward = 0;
+void dmxo_set_pop_forward(int forward) { g_pop_forward = forward; }
+
+enum { ST_EMPTY = 0x1, ST_FILLED = 0x2, ST_BLOCKED = 0x4, ST_CONTEXTFILLED = 0x8, ST_EDGE = 0x20, ST_AUGMENTED = 0x8000 };
 /* PixelRef directions (salalib/pixelref.h:46) */
 enum { D_NODIR = 0, D_H = 1, D_V = 2, D_PD = 4, D_ND = 8, D_DIAG = 12, D_NH = 16, D_NV = 32 };
 
@@ -385,8 +391,8 @@ static void block_lines(dmxo_map* m) {
     m->blocked_lines = 1;
 }
 
-/* PointMap::expand (pointdata.cpp:483-514) */
-static int expand(dmxo_map* m, int x1, int y1, int x2, int y2, Vec* list) {
+/* PointMap::expand (pointdata.cpp:483-514); fill_state is makePoints' filltype (:434-441) */
+static int expand(dmxo_map* m, int x1, int y1, int x2, int y2, Vec* list, int32_t fill_state) {
     if ((short)x2 < 0 || (short)x2 >= (short)m->cols || (short)y2 < 0 || (short)y2 >= (short)m->rows) return 1;
     int64_t c2 = cidx(m, x2, y2), c1 = cidx(m, x1, y1);
     if (m->state[c2] & ST_FILLED) return 2;
@@ -396,13 +402,20 @@ static int expand(dmxo_map* m, int x1, int y1, int x2, int y2, Vec* list) {
         if (intersect_region(&l.r, &m->cl[i].r, tol) && intersect_line(&l, &m->cl[i], tol)) return 4;
     for (int64_t i = m->cl_off[c2]; i < m->cl_off[c2 + 1]; i++)
         if (intersect_region(&l.r, &m->cl[i].r, tol) && intersect_line(&l, &m->cl[i], tol)) return 4;
-    m->state[c2] = ST_FILLED | (m->state[c2] & ST_BLOCKED); /* Point::set (point.h:121-125) */
+    m->state[c2] = fill_state | (m->state[c2] & ST_BLOCKED); /* Point::set (point.h:121-125) */
     int32_t* p = (int32_t*)vec_push(list, 2 * sizeof(int32_t));
     p[0] = x2; p[1] = y2;
     return 8;
 }
 
-int dmxo_fill(dmxo_map* m, double sx, double sy) {
+int dmxo_fill(dmxo_map* m, double sx, double sy) { return dmxo_fill_type(m, sx, sy, 0); }
+
+/* PointMap::makePoints(seed, fill_type) (pointdata.cpp:402-481): 0 FULLFILL, 1 SEMIFILL, 2 AUGMENT.
+ * The loop is the reference's literal pflipper loop.  An AUGMENT fill sets AUGMENTED without FILLED,
+ * which expand does not stop at (:489), so it can run forever: the loop is cut after 64 pops per cell
+ * and -1 returned (the state is then garbage; callers discard the map). */
+int dmxo_fill_type(dmxo_map* m, double sx, double sy, int fill_type) {
+    int32_t fill_state = fill_type == 0 ? ST_FILLED : fill_type == 1 ? (ST_FILLED | ST_CONTEXTFILLED) : ST_AUGMENTED;
     /* runmethods.cpp:269-277 fillGraph: region.contains(point) */
     if (!(sx > m->parent.blx && sx < m->parent.trx && sy > m->parent.bly && sy < m->parent.try_)) return 0;
     /* PointMap::pixelate(p, false) (pointdata.cpp:283-305) */
@@ -420,8 +433,10 @@ int dmxo_fill(dmxo_map* m, double sx, double sy) {
     }
     block_lines(m);
     int64_t c0 = cidx(m, px, py);
-    m->state[c0] = ST_FILLED | (m->state[c0] & ST_BLOCKED);
+    m->state[c0] = fill_state | (m->state[c0] & ST_BLOCKED);
     Vec lists[2] = {{0}, {0}};
+    const int64_t max_pops = 64 * (int64_t)m->cols * m->rows + 64;
+    int64_t pops = 0;
     int par = 0;
     int32_t* p0 = (int32_t*)vec_push(&lists[0], 2 * sizeof(int32_t));
     p0[0] = px; p0[1] = py;
@@ -430,18 +445,22 @@ int dmxo_fill(dmxo_map* m, double sx, double sy) {
         int x = cur[0], y = cur[1];
         Vec* b = &lists[par ^ 1];
         int res = 0;
-        res |= expand(m, x, y, x, y + 1, b);          /* up */
-        res |= expand(m, x, y, x, y - 1, b);          /* down */
-        res |= expand(m, x, y, x - 1, y, b);          /* left */
-        res |= expand(m, x, y, x + 1, y, b);          /* right */
-        res |= expand(m, x, y, x - 1, y + 1, b);      /* up-left */
-        res |= expand(m, x, y, x + 1, y + 1, b);      /* up-right */
-        res |= expand(m, x, y, x - 1, y - 1, b);      /* down-left */
-        res |= expand(m, x, y, x + 1, y - 1, b);      /* down-right */
+        res |= expand(m, x, y, x, y + 1, b, fill_state);          /* up */
+        res |= expand(m, x, y, x, y - 1, b, fill_state);          /* down */
+        res |= expand(m, x, y, x - 1, y, b, fill_state);          /* left */
+        res |= expand(m, x, y, x + 1, y, b, fill_state);          /* right */
+        res |= expand(m, x, y, x - 1, y + 1, b, fill_state);      /* up-left */
+        res |= expand(m, x, y, x + 1, y + 1, b, fill_state);      /* up-right */
+        res |= expand(m, x, y, x - 1, y - 1, b, fill_state);      /* down-left */
+        res |= expand(m, x, y, x + 1, y - 1, b, fill_state);      /* down-right */
         int64_t c = cidx(m, x, y);
         if ((res & 4) || (m->state[c] & ST_BLOCKED)) m->state[c] |= ST_EDGE;
         lists[par].n--;
         if (lists[par].n == 0) par ^= 1;
+        if (++pops > max_pops) {
+            free(lists[0].p); free(lists[1].p);
+            return -1;
+        }
     }
     free(lists[0].p); free(lists[1].p);
     return 1;
@@ -1044,10 +1063,9 @@ int dmxo_vga_global(dmxo_map* m, double radius, int gates_only, int64_t nb, int6
                 if (nlev_alloc < level + 2) nlev_alloc = level + 2;
                 levels[level + 1].n = 0;
                 dist[nd++] = 0;
-                Pix* lv_ = (Pix*)levels[level].p;
-                for (int64_t i = levels[level].n - 1; i >= 0; i--) {
-                    Pix cur = ((Pix*)levels[level].p)[i];
-                    (void)lv_;
+                const int64_t nl = levels[level].n;
+                for (int64_t i = nl - 1; i >= 0; i--) {
+                    Pix cur = ((Pix*)levels[level].p)[g_pop_forward ? nl - 1 - i : i];
                     int64_t idx = (int64_t)cur.x + (int64_t)cur.y * m->cols;
                     int64_t cc = cidx(m, cur.x, cur.y);
                     if ((m->state[cc] & ST_FILLED) && miscs[idx] != ~0) {
@@ -1526,7 +1544,7 @@ int dmxo_visual_stepdepth(dmxo_map* m, const int32_t* sel_cells, int64_t nsel, f
     while (cur.n) {
         next.n = 0;
         for (int64_t i = cur.n - 1; i >= 0; i--) {
-            const Pix pc = ((Pix*)cur.p)[i];
+            const Pix pc = ((Pix*)cur.p)[g_pop_forward ? cur.n - 1 - i : i];
             const int64_t cc = cidx(m, pc.x, pc.y), idx = (int64_t)pc.x + (int64_t)pc.y * m->cols;
             if ((m->state[cc] & ST_FILLED) && miscs[idx] != ~0) {
                 out[m->node_of_cell[cc]] = (float)level;

@@ -31,6 +31,11 @@ void dmxo_grid_info(const dmxo_map* m, int32_t* cols, int32_t* rows, double* bl_
 /* PointMap::makePoints(seed, FULLFILL) (pointdata.cpp:402-481). Returns 1 on success, 0 if the
  * reference would return false. */
 int dmxo_fill(dmxo_map* m, double x, double y);
+/* makePoints with fill_type 0/1/2 (pointdata.cpp:402-481); -1: an AUGMENT fill that does not end. */
+int dmxo_fill_type(dmxo_map* m, double x, double y, int fill_type);
+/* Test knob: VGA global / visual step depth walk each level front to back (1) or, as the reference, back
+ * to front (0, the default).  Shows which results depend on the pop order inside a level. */
+void dmxo_set_pop_forward(int forward);
 
 /* Per-cell state (x-major, cols*rows) and cropped cell lines (after blockLines). */
 void dmxo_get_state(const dmxo_map* m, int32_t* out);

@@ -31,6 +31,10 @@ def lib():
         L.dmxo_grid_info.argtypes = [vp, vp, vp, vp, vp]
         L.dmxo_fill.restype = i32
         L.dmxo_fill.argtypes = [vp, dbl, dbl]
+        L.dmxo_fill_type.restype = i32
+        L.dmxo_fill_type.argtypes = [vp, dbl, dbl, i32]
+        L.dmxo_set_pop_forward.restype = None
+        L.dmxo_set_pop_forward.argtypes = [i32]
         L.dmxo_get_state.argtypes = [vp, vp]
         L.dmxo_cell_lines_count.restype = i64
         L.dmxo_cell_lines_count.argtypes = [vp]
@@ -118,8 +122,10 @@ class OracleMap:
             lib().dmxo_free(self.h)
             self.h = None
 
-    def fill(self, x, y):
-        return bool(lib().dmxo_fill(self.h, float(x), float(y)))
+    def fill(self, x, y, fill_type=0):
+        """True if makePoints filled; None for an AUGMENT fill that never ends in the reference."""
+        r = lib().dmxo_fill_type(self.h, float(x), float(y), int(fill_type))
+        return None if r < 0 else bool(r)
 
     def state(self):
         out = np.zeros(self.cols * self.rows, dtype=np.int32)
@@ -235,3 +241,8 @@ class OracleMap:
             raise ValueError("node out of range")
         return out, secs
 
+
+def set_pop_forward(forward):
+    """Test knob: the oracle's BFS walks each level front to back (True) instead of the reference's back
+    to front.  Only to show which results depend on the order inside a level."""
+    lib().dmxo_set_pop_forward(1 if forward else 0)

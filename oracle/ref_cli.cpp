@@ -9,6 +9,11 @@
 //                        makePoints, makeGraph, PointMap::unmake)
 //   runVga               :227-267 (RadiusConverter radiusconverter.cpp:24-61)
 //   runStepDepth         :735-778
+//   linkGraph            :116-190 (LINK mode, point maps, coordinate links: -lnk x1,y1,x2,y2)
+// Fixture-only extensions (not depthmapXcli flags): -pps / -ppa fill a point with makePoints'
+// fill_type 1 (SEMIFILL) / 2 (AUGMENT), the GUI's other fill modes (depthmapview.h:75); -pen / -unpen
+// x,y apply the GUI's pencil tool (PointMap::fillPoint(p, add), pointdata.cpp:375-394); all in the
+// order given together with -pp.
 // and writes the .graph exactly as the CLI does (MetaGraph::write(out, METAGRAPH_VERSION, false)).
 // tests/golden/make_golden_graphfiles.py turns its outputs into fixtures (sha256 + section digests).
 //
@@ -25,6 +30,7 @@
 
 #include "salalib/entityparsing.h"
 #include "salalib/gridproperties.h"
+#include "salalib/linkutils.h"
 #include "salalib/mgraph.h"
 
 static std::vector<Point2f> parse_points(const std::vector<std::string>& pts) {
@@ -43,7 +49,8 @@ int main(int argc, char** argv) {
     std::string in, out, mode, vm, vr, sdt;
     bool simple = false, pm = false, pb = false, pu = false, pl = false, vg = false, vl = false;
     double pg = -1, pr = -1;
-    std::vector<std::string> pp, sdp;
+    std::vector<std::string> sdp, lnk;
+    std::vector<std::pair<int, std::string>> pp;   // (fill_type, point)
     for (int i = 1; i < argc; i++) {
         std::string a = argv[i];
         auto next = [&]() { return std::string(argv[++i]); };
@@ -52,7 +59,12 @@ int main(int argc, char** argv) {
         else if (a == "-m") mode = next();
         else if (a == "-s") simple = true;
         else if (a == "-pg") pg = atof(next().c_str());
-        else if (a == "-pp") pp.push_back(next());
+        else if (a == "-pp") pp.push_back({0, next()});
+        else if (a == "-pps") pp.push_back({1, next()});
+        else if (a == "-ppa") pp.push_back({2, next()});
+        else if (a == "-pen") pp.push_back({10, next()});
+        else if (a == "-unpen") pp.push_back({11, next()});
+        else if (a == "-lnk") lnk.push_back(next());
         else if (a == "-pr") pr = atof(next().c_str());
         else if (a == "-pm") pm = true;
         else if (a == "-pb") pb = true;
@@ -83,9 +95,11 @@ int main(int argc, char** argv) {
             if (!g->getDisplayedPointMap().isProcessed()) return die("Current map has not had its graph made");
             g->getDisplayedPointMap().unmake(pl);
         } else {
-            for (auto& p : parse_points(pp)) {
+            for (auto& tp : pp) {
+                Point2f p = parse_points({tp.second}).at(0);
                 if (!g->getRegion().contains(p)) return die("Point outside of target region");
-                g->makePoints(p, 0, nullptr);
+                if (tp.first >= 10) g->getDisplayedPointMap().fillPoint(p, tp.first == 10);
+                else g->makePoints(p, tp.first, nullptr);
             }
             if (pm) g->makeGraph(nullptr, pb ? 1 : 0, pr);
         }
@@ -105,6 +119,13 @@ int main(int argc, char** argv) {
             return die("unsupported -vm " + vm);
         }
         g->analyseGraph(nullptr, o, simple);
+    } else if (mode == "LINK") {
+        std::stringstream ss;
+        ss << "x1,y1,x2,y2";
+        for (auto& l : lnk) ss << "\n" << l;
+        std::vector<Line> lines = EntityParsing::parseLines(ss, ',');
+        PointMap& map = g->getDisplayedPointMap();
+        depthmapX::mergePixelPairs(depthmapX::pixelateMergeLines(lines, map), map);
     } else if (mode == "STEPDEPTH") {
         for (auto& p : parse_points(sdp)) {
             if (!g->getRegion().contains(p)) return die("Point outside of target region");

@@ -123,7 +123,7 @@ def parse(buf):
             disp = r.get("i")
             cols, rows_at = _skip_table(r)
             out["maps"].append({"name": name, "start": start, "displayed_sorted": disp, "columns": cols,
-                                "rows": rows_at, "grid": (cols_, rows)})
+                                "rows": rows_at, "grid": (cols_, rows), "filled": filled})
             break   # the files under test keep one point map; later maps are not located
     return out
 

@@ -4,11 +4,15 @@ real reference (oracle/_ref/ref_probe) and (b) the C restatement (oracle/) on se
 Bar: bit-exact for everything integer (states, bins, run lists, node counts, grid connections) and
 for the makeGraph float attributes; VGA float measures within 1e-6 relative (north_star), with the
 bit-exact fraction asserted separately to catch silent drift."""
+import os
+
 import numpy as np
 import pytest
 
 import depthmapx_amd as dmx
 from golden_io import case_input_lines, load_case, node_digests
+
+HERE = os.path.dirname(os.path.abspath(__file__))
 
 pytestmark = pytest.mark.gpu
 
@@ -207,6 +211,28 @@ def test_balanced_shard_bounds_assemble_to_whole_graph(ctx, stride):
     torch.cuda.synchronize()
     g = pm.assemble(ctx, [t.data_ptr() for t in blobs], [t.numel() for t in blobs])
     _assert_graph_equal(g.copy(), A, True)
+
+
+def test_balanced_shard_bounds_do_not_depend_on_verbose(ctx, tmp_path):
+    """DMX_VERBOSE=1 selects the makeGraph kernels with per-phase clocks; the cost sample of
+    dmx_makegraph_balance must still count every sampled source, so the bounds are the same (every rank
+    relies on computing identical bounds).  The flag is read once per process: a child process runs it."""
+    import subprocess
+    import sys
+    meta, A = load_case("gallery")
+    pm = _map(meta)
+    want = pm.shard_bounds(ctx, 4, stride=7)
+    code = ("import sys; sys.path[:0] = %r\n"
+            "import depthmapx_amd as dmx\n"
+            "from golden_io import load_case, case_input_lines\n"
+            "meta, A = load_case('gallery')\n"
+            "pm = dmx.PointMap(meta['region'], case_input_lines(meta), meta['spacing'])\n"
+            "[pm.make_points(*f) for f in meta['fills']]\n"
+            "print(pm.shard_bounds(dmx.Context(0), 4, stride=7))\n") % ([os.path.dirname(HERE), HERE],)
+    env = dict(os.environ, DMX_VERBOSE="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.stdout.strip().splitlines()[-1] == str(want)
 
 
 @pytest.mark.parametrize("kernel", ["v1", "topdown", "do"])

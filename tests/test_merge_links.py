@@ -14,7 +14,7 @@ CPU: the C restatement (oracle/) against the columns the real reference wrote fo
 built from source) -- this pins the oracle's merge semantics.  GPU: the HIP kernels against the pinned
 oracle on seeded synthetic maps with random merge links (every kernel family: tile-resolved BFS,
 direction-optimising BFS, top-down visual step depth, the serial metric / angular searches), and the
-refusal of the one order-dependent combination (merge links on context-filled cells)."""
+exact handling of links with a context-filled end, refused only where the reference's pop order decides."""
 import json
 import lzma
 import os
@@ -90,7 +90,6 @@ def test_merge_fixtures_hold_links():
             filled = (pmd["state"] & 2) != 0
             assert filled[pmd["merges"].ravel()].all()
     for name, m in CASES.items():
-        assert "refused" not in m
         if name.startswith("merge_") and m["columns"]:
             assert os.path.exists(os.path.join(GF, name + "_cols.npz")), name
 
@@ -238,22 +237,98 @@ def test_gpu_vga_metric_angular_with_merges_match_oracle(ctx, seed):
     np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.gpu
-def test_gpu_merges_on_contextfilled_cells_are_refused_where_order_matters(ctx):
-    """A merge link on a CONTEXTFILLED cell (SEMIFILL) makes VGA global with a radius and visual step
-    depth depend on the pop order inside a level: refused.  Radius n and the metric searches run."""
+def _contextfilled_links(seed):
+    """A seeded map whose links all have one end context-filled at an odd PixelRef (SEMIFILL)."""
     import depthmapx_amd as dmx
-    pm, om, pairs = _synthetic(3)
+    pm, om, pairs = _synthetic(seed, nlinks=16)
+    rows = pm.rows
     st = np.ascontiguousarray(pm.state(), dtype=np.int32)
-    st[pairs[0, 0]] |= 0x8   # Point::CONTEXTFILLED
+    for a, _ in pairs:
+        x, y = divmod(int(a), rows)
+        if x % 2 or y % 2:
+            st[a] |= 0x8   # Point::CONTEXTFILLED
     N = dmx._native
     N.check(N.lib().dmx_pointmap_set_state(pm.h, N.ptr(st)))
+    from pyoracle import OracleMap
+    om2 = OracleMap.from_grid(pm.cols, rows, 1.0, pm.info()["bottom_left"], st)
+    return pm, om, om2, pairs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 4, 6])
+@pytest.mark.parametrize("kernel", ["tile", "do"])
+def test_gpu_contextfilled_links_exact_or_refused_where_order_matters(ctx, monkeypatch, seed, kernel):
+    """Merge links with a context-filled odd end under a radius: the GPU answers exactly what the reference
+    computes, unless some source finds both ends at one level -- then the reference's count depends on its
+    pop order inside the level (the oracle's two orders differ) and the call is refused (DMX_ERR_UNSUPPORTED).
+    Radius n expands every cell and always runs."""
+    import depthmapx_amd as dmx
+    import pyoracle
+    if kernel == "do":
+        monkeypatch.setenv("DMX_VGA_KERNEL", "do")
+    pm, om, om2, pairs = _contextfilled_links(seed)
     pm.set_merges(pairs)
     g = pm.make_graph(ctx)
-    g.vga_visual_global(radius=-1)
-    g.metric_step_depth(cells=[int(pairs[1, 0])])
-    with pytest.raises(dmx.DmxError) as e:
-        g.vga_visual_global(radius=3)
-    assert e.value.status == -5
-    with pytest.raises(dmx.DmxError):
-        g.visual_step_depth(cells=[int(pairs[1, 0])])
+    om.make_graph()
+    b = om.graph()
+    om2.set_graph(b["bins"], b["runs"])
+    om2.set_merges(pairs)
+    got = g.vga_visual_global(radius=-1)
+    assert np.allclose(got, om2.vga_global(radius=-1, threads=8), rtol=1e-6, atol=1e-6)
+    outcomes = []
+    for radius in (2, 3, 5):
+        ref = om2.vga_global(radius=radius, threads=8)
+        try:
+            pyoracle.set_pop_forward(True)
+            fwd = om2.vga_global(radius=radius, threads=8)
+        finally:
+            pyoracle.set_pop_forward(False)
+        order_free = np.array_equal(ref.view(np.uint32), fwd.view(np.uint32))
+        try:
+            got = g.vga_visual_global(radius=radius)
+        except dmx.DmxError as e:
+            assert e.status == -5
+            assert not order_free, radius
+            outcomes.append("refused")
+            continue
+        np.testing.assert_array_equal(got[:, 5], ref[:, 5])
+        assert np.allclose(got, ref, rtol=1e-6, atol=1e-6)
+        outcomes.append("exact")
+    assert len(outcomes) == 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [3, 4, 6])
+def test_gpu_visual_step_depth_with_contextfilled_links(ctx, seed):
+    """Visual step depth with context-filled odd link ends: exact (bit for bit with the oracle), or refused
+    only where extracting an unexpanded end would reach a new cell -- where the two pop orders differ."""
+    import depthmapx_amd as dmx
+    import pyoracle
+    pm, om, om2, pairs = _contextfilled_links(seed)
+    pm.set_merges(pairs)
+    g = pm.make_graph(ctx)
+    om.make_graph()
+    b = om.graph()
+    om2.set_graph(b["bins"], b["runs"])
+    om2.set_merges(pairs)
+    st = pm.state()
+    cells = [int(pairs[0, 1]), int(pairs[1, 0]), pm.pixelate(20.5, 20.5), int(pairs[5, 1])]
+    ran = 0
+    for c in cells:
+        if not st[c] & 2:
+            continue
+        ref = om2.visual_stepdepth([c])
+        try:
+            pyoracle.set_pop_forward(True)
+            fwd = om2.visual_stepdepth([c])
+        finally:
+            pyoracle.set_pop_forward(False)
+        try:
+            got = g.visual_step_depth(cells=[c])
+        except dmx.DmxError as e:
+            assert e.status == -5
+            assert not np.array_equal(ref.view(np.uint32), fwd.view(np.uint32))
+            continue
+        np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
+        ran += 1
+    assert ran > 0
