@@ -30,6 +30,7 @@ SIGNATURES = {
     "dmx_pointmap_fill": (_i32, [_vp, _dbl, _dbl, _vp]),
     "dmx_pointmap_fill_device": (_i32, [_vp, _vp, _dbl, _dbl, _vp]),
     "dmx_pointmap_make_points": (_i32, [_vp, _dbl, _dbl, _i32, _vp]),
+    "dmx_graph_special_nodes": (_i32, [_vp, _vp, _vp]),
     "dmx_pointmap_make_points_device": (_i32, [_vp, _vp, _dbl, _dbl, _i32, _vp]),
     "dmx_ctx_last_fill": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_pointmap_info": (_i32, [_vp, _vp, _vp, _vp, _vp, _vp]),

@@ -1784,15 +1784,15 @@ static int prepare_tiles(dmx_graph* g) {
     return DMX_OK;
 }
 
-extern "C++" template <int NT, bool SPECIAL, bool RBM>
+extern "C++" template <int NT, bool SPECIAL, bool RBM, bool FG>
 static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_t lds, int64_t* blocks_out,
                        DevBuf<unsigned long long>& xg, DevBuf<int4>& queue, DevBuf<int32_t>& list) {
     int occ = 0;
-    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT, SPECIAL, RBM>, NT, lds));
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT, SPECIAL, RBM, FG>, NT, lds));
     if (occ < 1) occ = 1;
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((int64_t)ctx->num_cu * occ, nsrc));
     const int64_t nt = (int64_t)Q.tw * Q.th;
-    HIPCHK(xg.alloc((size_t)blocks * 2 * nt));
+    HIPCHK(xg.alloc((size_t)blocks * (FG ? 3 : 2) * nt));   // V, X [, F]
     HIPCHK(queue.alloc((size_t)blocks * nt));
     HIPCHK(list.alloc((size_t)blocks * nt * 64 * 2));
     DevBuf<int32_t> tlist;   // per workgroup: the two unvisited-tile lists
@@ -1802,6 +1802,7 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
     DevBuf<int32_t> mseen;   // per workgroup: merge_order_check stamps
     VgaTileParams P = Q;
+    P.fg = FG ? xg.p + (size_t)blocks * 2 * nt : nullptr;   // per workgroup [nt] after every V / X pair
     if (Q.nmamb) {
         HIPCHK(mseen.alloc((size_t)blocks * Q.nmamb));
         HIPCHK(hipMemsetAsync(mseen.p, 0, (size_t)blocks * Q.nmamb * 4, ctx->stream));
@@ -1816,22 +1817,13 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
     if (const char* c = getenv("DMX_VGA_CHUNK")) P.chunk = std::max(1, atoi(c));
     P.nwork = (int)((P.src_end - P.src_begin + P.chunk - 1) / P.chunk);
-    P.xcd_ctr = nullptr;
-    DevBuf<int> xcd;
-    if (const char* xe = getenv("DMX_VGA_XCD")) {
-        if (atoi(xe) > 0) {
-            HIPCHK(xcd.alloc(8));
-            HIPCHK(hipMemsetAsync(xcd.p, 0, 8 * sizeof(int), ctx->stream));
-            P.xcd_ctr = xcd.p;
-        }
-    }
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     P.ctl = ctx->d_ctl;
     ctx->h_ctl->progress = 0;
     DevBuf<VgaTileParams> dP;
     HIPCHK(dP.alloc(1));
     HIPCHK(hipMemcpyAsync(dP.p, &P, sizeof(P), hipMemcpyHostToDevice, ctx->stream));
-    hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL, RBM>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream,
+    hipLaunchKernelGGL((vga_tile_kernel<NT, SPECIAL, RBM, FG>), dim3((unsigned)blocks), dim3(NT), lds, ctx->stream,
                        (const VgaTileParams*)dP.p);
     HIPCHK(hipGetLastError());
     HIPCHK(wait_progress(ctx, DMX_PHASE_VGA, nsrc, P.chunk));   // hint freed on return
@@ -1901,11 +1893,20 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     HIPCHK(d_nlev.alloc(std::max<int64_t>(N, 1)));
     Q.maxlev = maxlev; Q.hist_out = d_hist.p; Q.nlev_out = d_nlev.p; Q.stats = ctx->stats.p;
     const size_t wr_ = (tw + 63) / 64, wc_ = (th + 63) / 64;
-    const size_t lds = (size_t)nt * 8 + (size_t)(th * wr_ + tw * wc_) * 8 + (size_t)VGA_HMAX * 4;
-    // line-resolved summaries when they fit next to the frontier bitmap (~1010^2 cells and below)
-    const size_t lds_rb = (size_t)nt * 8 + (size_t)(th * wr_ + th * 8 * wr_ + tw * 8 * wc_) * 8 + (size_t)VGA_HMAX * 4;
+    // LDS: the frontier bitmap (unless FG), the tile-row summary Fsr, then either the per-tile column summary
+    // Fsc or the line-resolved summaries RB / CB, then the level histogram
+    const size_t lds_f = (size_t)nt * 8, lds_h = (size_t)VGA_HMAX * 4;
+    const size_t lds_sc = (size_t)(th * wr_ + tw * wc_) * 8, lds_rbcb = (size_t)(th * wr_ + th * 8 * wr_ + tw * 8 * wc_) * 8;
+    const size_t lds_cap = (size_t)160 * 1024 - 1024;
     const char* rb_env = getenv("DMX_VGA_RB");
-    const bool rbm = !(rb_env && atoi(rb_env) == 0) && lds_rb + 1024 <= (size_t)160 * 1024;
+    const bool rb_ok = !(rb_env && atoi(rb_env) == 0);
+    bool fg = false, rbm = false;
+    size_t L = 0;
+    if (rb_ok && lds_f + lds_rbcb + lds_h <= lds_cap) { rbm = true; L = lds_f + lds_rbcb + lds_h; }
+    else if (lds_f + lds_sc + lds_h <= lds_cap) { L = lds_f + lds_sc + lds_h; }
+    else if (rb_ok && lds_rbcb + lds_h <= lds_cap) { fg = true; rbm = true; L = lds_rbcb + lds_h; }
+    else if (lds_sc + lds_h <= lds_cap) { fg = true; L = lds_sc + lds_h; }
+    else return fail(DMX_ERR_CAPACITY, "grid too large for the tile BFS's LDS summaries");
     DevBuf<unsigned long long> xg;
     DevBuf<int4> queue;
     DevBuf<int32_t> list;
@@ -1914,18 +1915,23 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     (void)kt;
     if (nsrc > 0) {
         const bool sp = g->nspecial > 0;
-        const size_t L = rbm ? lds_rb : lds;
-        if (nt <= 4096) {
-            rc = sp ? (rbm ? launch_tile<256, true, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
-                           : launch_tile<256, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
-                    : (rbm ? launch_tile<256, false, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
-                           : launch_tile<256, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
+        if (fg) {
+            rc = sp ? (rbm ? launch_tile<1024, true, true, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<1024, true, false, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
+                    : (rbm ? launch_tile<1024, false, true, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<1024, false, false, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
+            ntpb = 1024;
+        } else if (nt <= 4096) {
+            rc = sp ? (rbm ? launch_tile<256, true, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<256, true, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
+                    : (rbm ? launch_tile<256, false, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<256, false, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
             ntpb = 256;
         } else {
-            rc = sp ? (rbm ? launch_tile<1024, true, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
-                           : launch_tile<1024, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
-                    : (rbm ? launch_tile<1024, false, true>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
-                           : launch_tile<1024, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
+            rc = sp ? (rbm ? launch_tile<1024, true, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<1024, true, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
+                    : (rbm ? launch_tile<1024, false, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<1024, false, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
             ntpb = 1024;
         }
         if (rc) return rc;
@@ -1974,7 +1980,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[9] = (long long)st[6];
     ctx->last_stats[10] = 0;
     ctx->last_stats[11] = (long long)st[7];
-    ctx->last_stats[12] = blocks | ((long long)kt << 32) | ((long long)ntpb << 40);
+    ctx->last_stats[12] = blocks | ((long long)kt << 32) | ((long long)ntpb << 40) | ((long long)fg << 56);
     ctx->last_stats[13] = (long long)st[13];
     ctx->last_stats[14] = (long long)st[14] * g->tvw * 8;   // bytes of tile-visibility rows read
     ctx->last_stats[15] = (long long)st[15];                          // runs scanned in phase C
@@ -2011,7 +2017,7 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
         const char* fk = getenv("DMX_VGA_KERNEL");
         const bool forced_other = fk && (std::string(fk) == "v1" || std::string(fk) == "do" || std::string(fk) == "topdown");
         const int nt = tw * th;
-        if (!forced_other && g->symmetric == 1 && nt <= 16 * 1024 && !ctx->tile_disabled) {
+        if (!forced_other && g->symmetric == 1 && !ctx->tile_disabled) {
             int rc2 = vga_tile_impl(ctx, g, radius, gates_only, sb, se, out, out_on_device, levels, tw, th);
             if (rc2 != DMX_ERR_CAPACITY) return rc2;   // capacity (level histogram): retry with vga_do
         }
@@ -2158,7 +2164,7 @@ int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int ga
     if (rc) return rc;
     PointMapHost& h = *g->pm->host;
     const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
-    if (g->symmetric == 1 && tw * th <= 16 * 1024 && !ctx->tile_disabled) {
+    if (g->symmetric == 1 && !ctx->tile_disabled) {
         DevBuf<int32_t> d_list;
         HIPCHK(d_list.alloc(lst.size()));
         HIPCHK(hipMemcpyAsync(d_list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, ctx->stream));
@@ -2648,6 +2654,23 @@ int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
     SAME_DEVICE(ctx, g);
     if (int rc = prepare_merges(g)) return rc;
     return stepdepth_impl<true>(ctx, g, sel_cells, nsel, out);
+}
+
+// The nodes the symmetry pass found asymmetric (their in-set differs from their run-length out-set; the
+// BFS kernels route them through exact Extra / Missing lists).  Runs the VGA preparation if needed.
+int dmx_graph_special_nodes(dmx_graph* g, int32_t* nodes, int64_t* n) {
+    if (!g || !n) return fail(DMX_ERR_ARG, "bad arguments");
+    if (g->node_begin != 0 || g->node_end != g->nnodes) return fail(DMX_ERR_STATE, "needs the whole graph");
+    HIPCHK(hipSetDevice(g->ctx->device));
+    if (int rc = prepare_uf(g)) return rc;
+    if (int rc = prepare_symmetry(g)) return rc;
+    const int64_t m = (int64_t)g->special_nodes.size();
+    if (nodes) {
+        if (*n < m) return fail(DMX_ERR_ARG, "buffer too small");
+        std::memcpy(nodes, g->special_nodes.data(), (size_t)m * 4);
+    }
+    *n = m;
+    return DMX_OK;
 }
 
 int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {

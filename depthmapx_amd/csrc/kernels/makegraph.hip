@@ -28,9 +28,6 @@ constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capa
 // cells, and a full-length LDS array would cost a 2000^2 grid a quarter of its waves
 constexpr int MK_OPEN_LDS = 1024;
 // BIN_BALLOT: the per-bin count and far distance updated once per ratio class of a candidate chunk
-#ifndef DMX_MK_BIN_BALLOT
-#define DMX_MK_BIN_BALLOT 0
-#endif
 
 struct MakeGraphParams {
     int cols, rows;
@@ -699,9 +696,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     if (am) {
                         int bin = -1;
                         double this_dist = 0.0;
-#if DMX_MK_BIN_BALLOT
-                        int kcls = 6;   // ratio class of this lane's visible cell (5: the FP64 fallback, 6: none)
-#endif
                         if (add) {
                             // whichbin(depixelate(c) - centre) (pointdata.h:432-520) decided on the exact
                             // ratio ind/depth: 0 and 1 are the axis / diagonal; tan15 and tan30 are
@@ -724,36 +718,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             }
                             const double dx = (double)(hx - cx), dy = (double)(hy - cy);
                             this_dist = sqrt(dx * dx + dy * dy) * sp;
-#if DMX_MK_BIN_BALLOT
-                            kcls = k >= 0 ? k : 5;
-                            if (k < 0) {
-#endif
                             atomicAdd(&L.binc[bin], 1u);
                             atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
-#if DMX_MK_BIN_BALLOT
-                            }
-#endif
                         }
-#if DMX_MK_BIN_BALLOT
-                        {
-                            // one LDS update per ratio class instead of one per cell: the chunk's cells share
-                            // the depth and their ind grows with the lane, so the farthest cell of a class is
-                            // its highest lane
-                            const uint32_t db = __float_as_uint((float)this_dist);
-#pragma unroll
-                            for (int c = 0; c < 5; c++) {
-                                const unsigned long long m = ballot(kcls == c);
-                                if (m) {
-                                    const int hl = 63 - __clzll((long long)m);
-                                    const uint32_t far = __builtin_amdgcn_readlane(db, hl);
-                                    if (lane == 0) {
-                                        atomicAdd(&L.binc[obin[c]], (unsigned)__popcll(m));
-                                        atomicMax(&L.bfar[obin[c]], far);
-                                    }
-                                }
-                            }
-                        }
-#endif
                         MK_T(3);
                         if (exact) {
                             // serial sums in lane order = reference addlist order

@@ -4,8 +4,8 @@
 // semantics as in vga.hip / vga_do.hip), organised so that one source costs O(tiles) rather than
 // O(cells) of memory traffic on open plans:
 //   * one workgroup per source (persistent grid); the frontier F is an LDS bitmap in 8x8-cell
-//     tiles (fits 1024x1024-cell grids), while the visited set V and the next level X live in the
-//     registers of the thread that owns each tile (thread tid owns tiles tid + k*NT);
+//     tiles (fits 1024x1024-cell grids), while the visited set V and the next level X live in
+//     per-workgroup HBM scratch (xg), touched only for the tiles that still hold an unvisited cell;
 //   * level 1 is top-down: the source's runs are rasterised into F with LDS atomic ORs;
 //   * later levels are bottom-up (valid because visibility is symmetric; the few asymmetric nodes
 //     are routed through exact in-set corrections, see vga_do.hip):
@@ -26,17 +26,8 @@ namespace dmx {
 constexpr int KH = 8;        // head runs per cell (first KH entries of its scan order)
 // HV_FIRST: heads and tile-common runs ordered row / column runs first (1000^2: VGA 7.50 -> 6.11 s, phase A's
 // clocks / 5.7: a diagonal run's test walks its tiles, 8 LDS reads a round trip)
-#ifndef DMX_VGA_HV_FIRST
-#define DMX_VGA_HV_FIRST 1
-#endif
 // PPRE_EARLY: phase C loads a row word's partial-tile prefix with the word itself
-#ifndef DMX_VGA_PPRE_EARLY
-#define DMX_VGA_PPRE_EARLY 0
-#endif
 // HEADS8_EARLY: phase B loads heads 4..7 with the hint's operand instead of after the first 4 head tests
-#ifndef DMX_VGA_HEADS8_EARLY
-#define DMX_VGA_HEADS8_EARLY 0
-#endif
 constexpr int CRK = 4;       // tile-common runs per tile
 constexpr int BEXT_DEFAULT = 0;   // scan-order runs past the KH heads phase B tests (final build: 0 -1.4 % vs 4, profiles/r3b_vga_env)
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
@@ -76,14 +67,14 @@ struct VgaTileParams {
     int64_t uf_count;
     int alpha;
     int* work_counter;
-    int* xcd_ctr;             // optional: 8 group counters (grab_work); nwork = work items (chunks)
-    int nwork;
+    int nwork;                // work items (chunks)
     DmxCtl* ctl;              // host-mapped progress / cancel block (nullptr: none)
     int chunk;                // consecutive sources per work grab (neighbouring sources share hints)
     uint32_t* hint;           // [nt*64] what last hit for a recent source: the scan position of a run, or
                               // (bit 31) a partial-tile mask: tile << 16 | its slot in the cell's list (~0u:
                               // none); shared by all workgroups: a stale value only costs one test
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
+    unsigned long long* fg;   // per workgroup [nt]: the frontier F (vga_tile_kernel<..., FG = true> only)
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
     int32_t* list;            // per workgroup [2][nt*64]: hard cells / frontier cells, then phase-B2 cells
     int32_t* tlist;           // per workgroup [2][nt]: tiles holding an unvisited cell (built by one level's
@@ -251,7 +242,8 @@ __device__ __forceinline__ bool diag_hits(const FView& V, Run ru) {
 
 // Line-resolved summaries (RB / CB): a run along one row (column) covers every cell of its interior
 // tiles in that row (column), so a summary bit there is a hit; only the two end tiles need their
-// frontier word.  At most 2 summary reads + 2 frontier reads per run (grids <= 1024 a side).
+// frontier word.  At most 2 summary reads + 2 frontier reads per run on grids <= 1024 a side; wider lines
+// (frontier in HBM, vga_tile_kernel<..., FG>) read the summary words between the ends as well.
 __device__ __forceinline__ bool line_hits_rb(const unsigned long long* F, const unsigned long long* sum, int fbase, int fstride,
                                              int t0, int t1, unsigned long long m_first, unsigned long long m_last) {
     const int w0 = t0 >> 6, w1 = t1 >> 6;
@@ -259,13 +251,15 @@ __device__ __forceinline__ bool line_hits_rb(const unsigned long long* F, const 
     unsigned long long b = 0ull;
     if (w1 == w0) a &= ~0ull >> (63 - (t1 & 63));
     else b = sum[w1] & (~0ull >> (63 - (t1 & 63)));
-    if (!(a | b)) return false;
     const bool f0 = (a >> (t0 & 63)) & 1ull;
     const bool f1 = ((w1 == w0 ? a : b) >> (t1 & 63)) & 1ull;
     unsigned long long ia = a & ~(1ull << (t0 & 63)), ib = b;
     if (w1 == w0) ia &= ~(1ull << (t1 & 63));
     else ib &= ~(1ull << (t1 & 63));
     if (ia | ib) return true;   // an interior tile: its whole row (column) segment is on the run
+    for (int w = w0 + 1; w < w1; w++)
+        if (sum[w]) return true;
+    if (!(f0 | f1)) return false;
     if (t0 == t1) return f0 && (F[fbase + t0 * fstride] & m_first & m_last);
     return (f0 && (F[fbase + t0 * fstride] & m_first)) || (f1 && (F[fbase + t1 * fstride] & m_last));
 }
@@ -297,29 +291,15 @@ __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
 struct TileShared {
     int src, qn, hn, item, bn;
     int tn[2];            // entries of the two unvisited-tile lists (level parity)
-    int grp, grp_tries;   // XCD-grouped work: the group being drained, groups found empty
     int mpart;            // merge partner cell of the source (-1: none)
     unsigned long long cnt, mass;
     unsigned long long mcorr, mdisc;   // merge pass: pairs discovered together, partners of U_f joined
 };
 
-// Next work item.  xcd_ctr == nullptr: one counter for the whole grid.  Otherwise the items are split
-// into 8 contiguous ranges, one per group of blocks sharing an XCD (blockIdx % 8: a label, not an XCD
-// id; placement only changes speed), so the ~32 workgroups of an XCD work on neighbouring sources and
-// share its L2; a group whose range is drained moves on to the next group's range.  The grid counter
-// still counts grabs, for progress.
-__device__ __forceinline__ int grab_work(DmxCtl* ctl, int* work_counter, int* xcd_ctr, int nwork, TileShared& S) {
-    const int w = ctl_poll(ctl, atomicAdd(work_counter, 1));   // progress and cancel on the grab count
-    if (!xcd_ctr || w == CTL_STOP) return w;
-    while (S.grp_tries < 8) {
-        const int g = S.grp;
-        const int b = (int)((long long)nwork * g / 8), e = (int)((long long)nwork * (g + 1) / 8);
-        const int i = atomicAdd(&xcd_ctr[g], 1);
-        if (b + i < e) return b + i;
-        S.grp = (g + 1) & 7;
-        S.grp_tries++;
-    }
-    return nwork;   // past the end: the workgroup leaves
+// Next work item: one grid counter (progress and cancel ride on it).  Contiguous per-XCD ranges, so that an
+// XCD's workgroups share their L2 on neighbouring sources, measured 1.1 % slower.
+__device__ __forceinline__ int grab_work(DmxCtl* ctl, int* work_counter) {
+    return ctl_poll(ctl, atomicAdd(work_counter, 1));
 }
 
 // Frontier cells on run `ru` (rare path: exact count for the asymmetric nodes).
@@ -499,9 +479,6 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
         if (fs) {
             t = P.tvis[row + w];
             f = P.ftvis[row + w];
-#if DMX_VGA_PPRE_EARLY
-            base[k] = (int)P.ppre[row + w];   // with the rows: one round trip fewer for an undecided cell
-#endif
         }
         cert |= (f & fs) != 0ull;
         pw[k] = t & ~f;
@@ -510,10 +487,8 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
     if (__ballot(cert) != 0ull) { how = 1; return true; }
     if (__ballot((cw[0] | cw[1] | cw[2] | cw[3]) != 0ull) == 0ull) { how = 2; return false; }
     how = 0;
-#if !DMX_VGA_PPRE_EARLY
 #pragma unroll
     for (int k = 0; k < 4; k++) base[k] = cw[k] ? (int)P.ppre[row + k * 64 + lane] : 0;
-#endif
     const unsigned long long* pm = P.pmask + P.poff[id];
 #pragma unroll 1
     for (int k = 0; k < 4; k++) {
@@ -561,16 +536,20 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
 // source touches each word a few times), F (frontier, read by every run test) is in LDS.
 // SPECIAL = false: the graph has no asymmetric nodes (every U_f cell is regular), no exact path.
 // RBM: line-resolved summaries RB / CB in LDS (replace Fsc; need ~32 KB more LDS, grids <= ~1010^2).
-template <int NT, bool SPECIAL, bool RBM>
+// FG: grids whose frontier bitmap does not fit the LDS (above 1024 cells a side): F is a per-workgroup
+// bitmap in HBM like V and X, and the LDS holds only its summaries (Fsr and RB / CB: 136 KB at 2000^2),
+// so a row or column run still costs its summary words plus at most 2 frontier words.
+template <int NT, bool SPECIAL, bool RBM, bool FG>
 __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __restrict__ PP) {
     const VgaTileParams& P = *PP;
-    extern __shared__ __attribute__((aligned(16))) unsigned long long F[];
+    extern __shared__ __attribute__((aligned(16))) unsigned long long tile_smem[];
     __shared__ TileShared S;
     constexpr int NW = NT / 64;
     const int nt = P.tw * P.th;
     const int wr = (P.tw + 63) / 64, wc = (P.th + 63) / 64;
     const int nfs = RBM ? P.th * wr : P.th * wr + P.tw * wc;   // summary words rebuilt by atomics per level
-    unsigned long long* Fsr = F + nt;           // [th][wr]
+    unsigned long long* F = FG ? P.fg + (size_t)blockIdx.x * nt : tile_smem;
+    unsigned long long* Fsr = FG ? tile_smem : F + nt;   // [th][wr]
     unsigned long long* Fsc = Fsr + P.th * wr;  // [tw][wc] (!RBM)
     unsigned long long* RB = Fsr + P.th * wr;   // [th*8][wr] (RBM)
     unsigned long long* CB = RB + P.th * 8 * wr; // [tw*8][wc] (RBM)
@@ -598,7 +577,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
     uint32_t* Hn = P.hint;
     if (tid == 0) {
         S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.cnt = 0; S.mass = 0; S.src = -1;
-        S.grp = blockIdx.x & 7; S.grp_tries = 0;
         S.mpart = -1; S.mcorr = 0; S.mdisc = 0;
     }
     int64_t chunk_end = 0;
@@ -608,7 +586,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
         // through the same runs: the hint array carries that knowledge from one source to the next
         if (src + 1 >= chunk_end) {
             __syncthreads();
-            if (tid == 0) S.src = grab_work(P.ctl, P.work_counter, P.xcd_ctr, P.nwork, S);
+            if (tid == 0) S.src = grab_work(P.ctl, P.work_counter);
             __syncthreads();
             src = P.src_begin + (int64_t)S.src * P.chunk;
             chunk_end = min(src + (int64_t)P.chunk, P.src_end);
@@ -713,49 +691,12 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         U = ~Vg[t];
                         const unsigned long long R = U & P.regular_tiles[t];
                         if (R) {
-#ifndef DMX_VGA_CR_PAR
-#define DMX_VGA_CR_PAR 0   // 1: the 4 tests without early exit (measured 2x slower phase A: the first usually hits)
-#endif
-#ifndef DMX_VGA_HEADS_PAR
-#define DMX_VGA_HEADS_PAR 0
-#endif
 // B_ORDER: the hint's operand is loaded before the head tests and tested after them (-0.7 %)
-#ifndef DMX_VGA_B_ORDER
-#define DMX_VGA_B_ORDER 1
-#endif
 // RB_INC: line summaries set per published tile with LDS atomics instead of rebuilt from F (measured
 // slower: bookkeeping clocks x1.9, contention on the summary words of a tile row)
-#ifndef DMX_VGA_RB_INC
-#define DMX_VGA_RB_INC 0
-#endif
-#ifndef DMX_VGA_HINT_BEFORE_DIAG
-#define DMX_VGA_HINT_BEFORE_DIAG 0
-#endif
 // BEXT_NODIAG: phase B's extra run tests skip diagonal runs (a cell that misses then goes to phase C's exact
 // mask test): 6.10 -> 5.62 s at 1000^2.  RB8: the line summaries rebuilt one F word read per tile (-0.05 s)
-#ifndef DMX_VGA_BEXT_NODIAG
-#define DMX_VGA_BEXT_NODIAG 1
-#endif
-#ifndef DMX_VGA_RB8
-#define DMX_VGA_RB8 1
-#endif
 // C_FUSED: phase C's row test and mask test in one pass per cell (1000^2: VGA 5.57 -> 5.11 s)
-#ifndef DMX_VGA_C_FUSED
-#define DMX_VGA_C_FUSED 1
-#endif
-#if DMX_VGA_CR_PAR
-                            // the common runs' tests are independent (no early-out between them), so their
-                            // LDS round trips overlap
-                            bool h[CRK];
-#pragma unroll
-                            for (int j = 0; j < CRK; j++) h[j] = j < P.crk && c[j].x0 >= 0 && run_hits_fs(FV, c[j]);
-                            bool hit = false;
-#pragma unroll
-                            for (int j = 0; j < CRK; j++) {
-                                rt += (j < P.crk && c[j].x0 >= 0) ? 1u : 0u;
-                                hit |= h[j];
-                            }
-#else
                             bool hit = false;
 #pragma unroll 1
                             for (int j = 0; j < CRK; j++)
@@ -763,7 +704,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                     rt++;
                                     hit = run_hits_fs(FV, c[j]);
                                 }
-#endif
                             if (hit) { Xg[t] = R; U &= ~R; ST(7, 1); }
                         }
                     }
@@ -849,7 +789,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         to_hard = true;
                         hard_val = -1 - id;   // special node: exact path
                     } else if (mine) {
-#if DMX_VGA_B_ORDER
                         // The hint's operand (a run of the scan order, or a partial tile's mask) is loaded
                         // first and tested after the 4 heads, so the load overlaps the heads' LDS tests;
                         // a head hit leaves the hint alone (heads are tested every time anyway).
@@ -862,34 +801,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (hp >= KH && hp < (uint32_t)nr) {
                             hr = P.scan_pool[ss + hp];
                         }
-#if DMX_VGA_HEADS8_EARLY
-                        // heads 4..7 loaded with the hint's operand (they do not depend on anything): the
-                        // extension tests below need no further round trip
-                        Run h2[4];
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            if (KH0 + r < min(nr, KH)) h2[r] = P.heads[(KH0 + r) * hstride + id];
-                            else h2[r].x0 = -1;
-                        }
-#endif
-#if DMX_VGA_HINT_BEFORE_DIAG
-                        // row / column heads, then the hint, then the diagonal heads (the heads are stored row /
-                        // column runs first, HV_FIRST): a diagonal test walks the run's tiles
-                        int r0 = 0;
-#pragma unroll 1
-                        for (; r0 < KH0 && r0 < nr && !hit; r0++) {
-                            if (hd[r0].x0 != hd[r0].x1 && hd[r0].y0 != hd[r0].y1) break;
-                            rt++;
-                            hit = run_hits_fs(FV, hd[r0]);
-                        }
-                        if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
-                        else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
-#pragma unroll 1
-                        for (; r0 < KH0 && r0 < nr && !hit; r0++) {
-                            rt++;
-                            hit = run_hits_fs(FV, hd[r0]);
-                        }
-#else
 #pragma unroll 1
                         for (int r = 0; r < KH0; r++)
                             if (!hit && r < nr) {
@@ -898,39 +809,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             }
                         if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
                         else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
-#endif
-#else
-                        if (hp != 0xFFFFFFFFu && (hp >> 31)) {   // the partial tile that hit for a recent source
-                            if (P.pmask) {
-                                rt++;
-                                hit = (F[(hp >> 16) & 0x7FFFu] & P.pmask[pof + (hp & 0xFFFFu)]) != 0ull;
-                            }
-                        } else if (hp >= KH && hp < (uint32_t)nr) {   // the run that hit for a recent source
-                            rt++;
-                            hit = run_hits_fs(FV, P.scan_pool[ss + hp]);
-                        }
-#if DMX_VGA_HEADS_PAR
-                        if (!hit) {
-                            // the heads' tests are independent: their LDS round trips overlap
-                            bool h4[KH0];
-#pragma unroll
-                            for (int r = 0; r < KH0; r++) h4[r] = r < nr && run_hits_fs(FV, hd[r]);
-                            int fr = -1;
-#pragma unroll
-                            for (int r = KH0 - 1; r >= 0; r--)
-                                if (h4[r]) fr = r;
-                            rt += (unsigned)min(nr, KH0);
-                            if (fr >= 0) { hit = true; if (hp != (uint32_t)fr) Hn[id] = (uint32_t)fr; }
-                        }
-#else
-#pragma unroll 1
-                        for (int r = 0; r < KH0; r++)
-                            if (!hit && r < nr) {
-                                rt++;
-                                if (run_hits_fs(FV, hd[r])) { hit = true; if (hp != (uint32_t)r) Hn[id] = (uint32_t)r; }
-                            }
-#endif
-#endif
                         const int lim = min(nr, KH + P.bext);
                         if (!hit) ST(29, 1);
                         bool skipped = false;
@@ -939,15 +817,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
 #pragma unroll
                             for (int j = 0; j < 4; j++) {
                                 const int r = base + j;
-#if DMX_VGA_HEADS8_EARLY && DMX_VGA_B_ORDER
-                                if (r < KH) rr[j] = (base == KH0) ? h2[j] : P.heads[r * hstride + id];
-#else
                                 if (r < KH) rr[j] = P.heads[r * hstride + id];
-#endif
                                 else if (r < lim) rr[j] = P.scan_pool[ss + r];
                                 else rr[j].x0 = -1;
                             }
-#if DMX_VGA_BEXT_NODIAG
                             // diagonal runs are left to phase C's exact mask test (their test walks the tiles)
                             if (P.pmask)
 #pragma unroll
@@ -956,7 +829,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                         rr[j].x0 = -1;
                                         skipped = true;   // not a full test: a miss goes to phase C
                                     }
-#endif
                             bool h4[4];
 #pragma unroll
                             for (int j = 0; j < 4; j++) h4[j] = rr[j].x0 >= 0 && run_hits_fs(FV, rr[j]);
@@ -994,10 +866,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 constexpr int CCH = 16;
                 // runs a lane loads per scan step (1000^2: 4 -> 9.61 s, 8 -> 9.71 s, 16 -> 14.6 s: more loads
                 // in flight per round trip do not pay for the registers and the over-read past the first hit)
-#ifndef DMX_VGA_CSTEP
-#define DMX_VGA_CSTEP 4
-#endif
-                constexpr int CSTEP = DMX_VGA_CSTEP;
+                constexpr int CSTEP = 4;
                 const unsigned long long c_t0 = __builtin_amdgcn_s_memtime();
                 for (;;) {
                     int it0 = 0;
@@ -1007,7 +876,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const int cn = min(CCH, hn - it0);
                     const int myv = lane < cn ? L[it0 + lane] : -1;
                     unsigned long long certain_m = 0ull, pruned_m = 0ull;   // bit j: chunk entry j
-                    if (P.tvis && !(DMX_VGA_C_FUSED && P.pmask)) {
+                    if (P.tvis && !P.pmask) {
                         for (int j = 0; j < cn; j += 2) {
                             const int v0 = __builtin_amdgcn_readlane(myv, j);
                             const int v1 = __builtin_amdgcn_readlane(myv, j + 1);
@@ -1067,7 +936,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (P.pmask) {
                             const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
                             unsigned nl = 0;
-#if DMX_VGA_C_FUSED
                             int how = 0;
                             found = pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
                             if (lane == 0) {
@@ -1075,9 +943,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                 if (how == 1) { ST(16, 1); }
                                 if (how == 2) ST(13, 1);
                             }
-#else
-                            found = pmask_hit(P, F, Fsr, id, nl, Hn);
-#endif
                             nl += __shfl_xor(nl, 32); nl += __shfl_xor(nl, 16); nl += __shfl_xor(nl, 8);
                             nl += __shfl_xor(nl, 4); nl += __shfl_xor(nl, 2); nl += __shfl_xor(nl, 1);
                             if (lane == 0) {
@@ -1180,12 +1045,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             // keep an unvisited cell for the next level.  A cleared frontier first: unlisted tiles
             // publish nothing (the merge pass may have set bits anywhere).
             const bool have_list = level > 0;
-            // line-resolved summaries set per published tile (no merge links: the merge pass adds single
-            // cells to F afterwards, and then the summaries are rebuilt from F below)
-            const bool rb_inc = RBM && DMX_VGA_RB_INC && P.nmp == 0;
             for (int i = tid; i < nfs; i += NT) Fsr[i] = 0ull;
-            if (rb_inc)
-                for (int i = tid; i < P.th * 8 * wr + P.tw * 8 * wc; i += NT) RB[i] = 0ull;   // RB, then CB
             if (have_list)
                 for (int t = tid; t < nt; t += NT) F[t] = 0ull;
             __syncthreads();
@@ -1214,21 +1074,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         const int tx = t % tw, ty = t / tw;
                         atomicOr(&Fsr[ty * wr + (tx >> 6)], 1ull << (tx & 63));
                         if (!RBM) atomicOr(&Fsc[tx * wc + (ty >> 6)], 1ull << (ty & 63));
-                        if (rb_inc) {
-                            // rows r (columns c) of the tile holding a frontier cell
-                            unsigned long long yr = x | (x >> 4);
-                            yr |= yr >> 2;
-                            yr |= yr >> 1;
-                            unsigned rows8 = (unsigned)(((yr & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
-                            unsigned long long yc = x | (x >> 32);
-                            yc |= yc >> 16;
-                            yc |= yc >> 8;
-                            unsigned cols8 = (unsigned)(yc & 0xFFull);
-                            for (; rows8; rows8 &= rows8 - 1)
-                                atomicOr(&RB[(ty * 8 + __ffs(rows8) - 1) * wr + (tx >> 6)], 1ull << (tx & 63));
-                            for (; cols8; cols8 &= cols8 - 1)
-                                atomicOr(&CB[(tx * 8 + __ffs(cols8) - 1) * wc + (ty >> 6)], 1ull << (ty & 63));
-                        }
                     }
                 }
                 F[t] = x;
@@ -1256,11 +1101,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                       P.mseen + (size_t)blockIdx.x * P.nmamb, (int32_t)node + 1, P.error);
                 }
             }
-            if (RBM && !rb_inc) {
+            if (RBM) {
                 // line-resolved summaries from the published frontier (plain stores, no atomics)
                 __syncthreads();
                 const int th = P.th;
-#if DMX_VGA_RB8
                 // one thread per (tile row, word) builds that word's 8 row summaries from the frontier tiles
                 // Fsr lists, one per (tile column, word) its 8 column summaries: each F word read once
                 for (int i = tid; i < th * wr + tw * wc; i += NT) {
@@ -1293,24 +1137,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         for (int k = 0; k < 8; k++) CB[(tx * 8 + k) * wc + w] = b[k];
                     }
                 }
-#else
-                for (int i = tid; i < th * 8 * wr; i += NT) {
-                    const int w = i % wr, r = (i / wr) & 7, ty = i / (8 * wr);
-                    const unsigned long long* fr = F + ty * tw + w * 64;
-                    const int n = min(64, tw - w * 64);
-                    unsigned long long bits = 0ull;
-                    for (int j = 0; j < n; j++) bits |= (unsigned long long)(((fr[j] >> (8 * r)) & 0xFFull) != 0ull) << j;
-                    RB[(ty * 8 + r) * wr + w] = bits;
-                }
-                for (int i = tid; i < tw * 8 * wc; i += NT) {
-                    const int w = i % wc, c = (i / wc) & 7, tx = i / (8 * wc);
-                    const unsigned long long cm = 0x0101010101010101ull << c;
-                    const int n = min(64, th - w * 64);
-                    unsigned long long bits = 0ull;
-                    for (int j = 0; j < n; j++) bits |= (unsigned long long)((F[(w * 64 + j) * tw + tx] & cm) != 0ull) << j;
-                    CB[(tx * 8 + c) * wc + w] = bits;
-                }
-#endif
             }
             sync_global();
             const long long cnt = (long long)S.cnt, mass = (long long)S.mass;
@@ -1372,7 +1198,6 @@ __global__ void tile_heads_kernel(int rows, int tw, const int32_t* node_cell, in
     const int nr = node_nruns[k];
     tscan_start[id] = ss;
     tnruns[id] = nr;
-#if DMX_VGA_HV_FIRST
     // the first KH scan entries with the row / column runs before the diagonal ones (a diagonal run's
     // test walks its tiles one LDS round trip per 8; a row or column run costs <= 4 reads): the order
     // only changes which test hits first
@@ -1383,9 +1208,6 @@ __global__ void tile_heads_kernel(int rows, int tw, const int32_t* node_cell, in
             const bool diag = ru.x0 != ru.x1 && ru.y0 != ru.y1;
             if (diag == (pass == 1)) heads[(o++) * hstride + id] = ru;
         }
-#else
-    for (int h = 0; h < KH && h < nr; h++) heads[h * hstride + id] = scan_pool[ss + h];
-#endif
 }
 
 // Tile-visibility rows: bit (ty, tx) of cell id's row is set iff the cell sees some cell of tile
@@ -1742,15 +1564,10 @@ __global__ void __launch_bounds__(CR_THREADS) tile_cr_kernel(int cols, int rows,
             int used = 0;
             for (int j = 0; j < CRK; j++) {
                 int pick = -1;
-#if DMX_VGA_HV_FIRST
                 // row / column runs first (cheap tests), longest first within each kind
                 auto key = [&](int g) { return bestlen[g] + ((cand[g].dx == 0 || cand[g].dy == 0) ? (1 << 20) : 0); };
                 for (int g = 0; g < 8; g++)
                     if (bestlen[g] > 0 && !((used >> g) & 1) && (pick < 0 || key(g) > key(pick))) pick = g;
-#else
-                for (int g = 0; g < 8; g++)
-                    if (bestlen[g] > 0 && !((used >> g) & 1) && (pick < 0 || bestlen[g] > bestlen[pick])) pick = g;
-#endif
                 Run z;
                 z.x0 = z.y0 = z.x1 = z.y1 = -1;
                 if (pick >= 0) {

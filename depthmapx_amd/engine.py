@@ -102,6 +102,8 @@ class Context:
         lv = d.pop("vga_levels")
         d["vga_bottom_up_levels"], d["vga_top_down_levels"] = lv & 0xFFFFFFFF, lv >> 32
         d["vga_special_nodes"] = d["vga_kernel"] >> 8
+        d["vga_frontier_hbm"] = (d["vga_launch"] >> 56) & 1   # tile BFS with its frontier in HBM (grids > 1024^2)
+        d["vga_launch"] &= (1 << 56) - 1
         d["vga_kernel"] = ["topdown-v1", "direction-optimizing(top-down only)",
                            "direction-optimizing", "tile-resolved"][d["vga_kernel"] & 0xFF]
         return d
@@ -233,6 +235,14 @@ class Graph:
         n, b, e, r = (ctypes.c_int64() for _ in range(4))
         N.check(N.lib().dmx_graph_info(self.h, ctypes.byref(n), ctypes.byref(b), ctypes.byref(e), ctypes.byref(r)))
         return dict(nnodes=n.value, node_begin=b.value, node_end=e.value, nruns=r.value)
+
+    def special_nodes(self):
+        """Nodes with an asymmetric visible set (dmx_graph_special_nodes)."""
+        n = ctypes.c_int64(0)
+        N.check(N.lib().dmx_graph_special_nodes(self.h, None, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), dtype=np.int32)
+        N.check(N.lib().dmx_graph_special_nodes(self.h, N.ptr(out), ctypes.byref(n)))
+        return out[:n.value]
 
     def copy(self, runs=True):
         i = self.info()

@@ -188,6 +188,11 @@ int dmx_vga_global_device(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
  * nodes in out_device are left untouched.  Used to interleave multi-GPU shards over the grid. */
 int dmx_vga_global_device_list(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, const int64_t* nodes,
                                int64_t n, float* out_device);
+/* Diagnostics of the VGA preparation (no reference counterpart): the nodes whose visible set is not
+ * symmetric (a cell in the node's runs that does not see the node back), found by 64-bit random-weight
+ * range hashes and routed through exact in-set corrections.  *n in = capacity, out = count; nodes NULL:
+ * only *n.  Builds the preparation on the graph's context if no VGA call has. */
+int dmx_graph_special_nodes(dmx_graph* g, int32_t* nodes, int64_t* n);
 /* ---- VGA metric (GPU) ----------------------------------------------------------------------- */
 /* MetaGraph::analyseGraph(OUTPUT_METRIC) -> VGAMetric(radius, gates_only).run (salalib/mgraph.cpp:
  * 359-361, vgamodules/vgametric.cpp:26-136) for source nodes [src_begin, src_end) (src_end < 0:

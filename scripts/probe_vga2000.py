@@ -21,6 +21,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nsrc", type=int, default=1024)
     ap.add_argument("--blocks", type=int, default=4)
+    ap.add_argument("--check-do", type=int, default=0, help="sources of the first block re-run on vga_do and compared")
     a = ap.parse_args()
     W = 1999
     ctx = dmx.Context(0)
@@ -33,15 +34,31 @@ def main():
     per = a.nsrc // a.blocks
     starts = [int(v) for v in np.linspace(0, N - per, a.blocks)]
     rec = {"grid": "2000x2000", "nodes": N, "makegraph_s": mk, "blocks": []}
+    outs = []
     for i, b in enumerate(starts):
         t1 = time.time()
         out = g.vga_visual_global(src_begin=b, src_end=b + per)
         wall = time.time() - t1
         st = ctx.last_stats()
+        outs.append(out[b:b + per].copy())
         rec["blocks"].append({"begin": b, "n": per, "kernel_s": ctx.last_timing()[1], "wall_s": wall,
                               "vga_kernel": st["vga_kernel"], "hbm_bitmaps": st.get("vga_hbm_bitmaps"),
-                              "mean_count": float(out[b:b + per, 5].mean())})
+                              "frontier_hbm": st.get("vga_frontier_hbm"), "mean_count": float(out[b:b + per, 5].mean()),
+                              "bottom_up_levels": st["vga_bottom_up_levels"], "top_down_levels": st["vga_top_down_levels"],
+                              "runs_tested": st["vga_runs_expanded"], "hard_cells": st["vga_hard_cells"],
+                              "hard_runs": st["vga_hard_runs"], "cr_tiles": st["vga_cr_tiles"]})
         print(json.dumps(rec["blocks"][-1]), file=sys.stderr, flush=True)
+    if a.check_do:
+        os.environ["DMX_VGA_KERNEL"] = "do"
+        b = starts[0]
+        n = min(a.check_do, per)
+        t1 = time.time()
+        ref = g.vga_visual_global(src_begin=b, src_end=b + n)
+        os.environ.pop("DMX_VGA_KERNEL")
+        same = bool(np.array_equal(ref[b:b + n].view(np.uint32), outs[0][:n].view(np.uint32)))
+        rec["check_do"] = {"sources": n, "bit_identical": same, "do_kernel_s": ctx.last_timing()[1],
+                           "wall_s": time.time() - t1}
+        print(json.dumps(rec["check_do"]), file=sys.stderr, flush=True)
     ks = sum(x["kernel_s"] for x in rec["blocks"][1:]) / max(1, sum(x["n"] for x in rec["blocks"][1:]))
     rec["kernel_s_per_source"] = ks
     rec["extrapolated_whole_map_s"] = ks * N
