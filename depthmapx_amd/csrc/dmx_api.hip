@@ -1730,9 +1730,15 @@ static int prepare_tiles(dmx_graph* g) {
     const bool tv_on = !(tv_env && atoi(tv_env) == 0);
     const char* ftv_env = getenv("DMX_VGA_FTVIS");
     const bool ftv_on = !(ftv_env && atoi(ftv_env) == 0);
-    // (the tile kernel reads a row as 4 words a lane: tvw <= 256, true for every grid whose frontier
-    // bitmap fits the LDS)
-    bool tv_build = tv_on && N && tvw <= 256 && tv_bytes * (ftv_on ? 2 : 1) <= free_b / 4 && tv_bytes <= (32ull << 30);
+    // Grids up to 1024 cells a side (tvw <= 256: the masks' row test reads 4 words a lane): tvis, ftvis, the
+    // tile rows and the partial-tile masks when they take at most a quarter of the free memory.  Wider grids
+    // (2000^2: 8 KB a row, 32 GB) keep tvis alone, as the phase-C miss certificate in front of the run scan,
+    // when it takes at most a third of what is free next to the graph and its scan order.
+    const bool wide = tvw > 256;
+    const size_t free_all = free_b + cached_bytes();
+    const bool ftv = ftv_on && !wide;
+    bool tv_build = tv_on && N && tv_bytes <= (32ull << 30) &&
+                    (wide ? tv_bytes <= free_all / 3 : tv_bytes * (ftv ? 2 : 1) <= free_b / 4);
     if (g->prep_fn) {
         // every rank must take the same branch (the rows are all-reduced): build only if all can
         DevBuf<int64_t> veto;
@@ -1747,7 +1753,7 @@ static int prepare_tiles(dmx_graph* g) {
     if (tv_build) {
         HIPCHK(g->tvis.alloc(Ct * tvw));
         HIPCHK(hipMemsetAsync(g->tvis.p, 0, tv_bytes, s));
-        if (ftv_on) {
+        if (ftv) {
             HIPCHK(g->ftvis.alloc(Ct * tvw));
             HIPCHK(hipMemsetAsync(g->ftvis.p, 0, tv_bytes, s));
         }
@@ -1760,22 +1766,22 @@ static int prepare_tiles(dmx_graph* g) {
             const int64_t nb = std::min<int64_t>(pe - pb, (int64_t)ctx->num_cu * 16);
             hipLaunchKernelGGL(tile_vis_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), tv_lds, s, rows, tw, th,
                                g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb,
-                               g->pool.p, g->notuf_tiles.p, g->tvis.p, ftv_on ? g->ftvis.p : nullptr);
+                               g->pool.p, g->notuf_tiles.p, g->tvis.p, ftv ? g->ftvis.p : nullptr);
             HIPCHK(hipGetLastError());
         }
         // rows of distinct nodes are disjoint: the sum over ranks is their union
         if (int rc = prep_allreduce(g, g->tvis.p, Ct * tvw, DMX_I64)) return rc;
-        if (ftv_on)
+        if (ftv)
             if (int rc = prep_allreduce(g, g->ftvis.p, Ct * tvw, DMX_I64)) return rc;
         const char* tt_env = getenv("DMX_VGA_TTVIS");
-        if (ftv_on && !(tt_env && atoi(tt_env) == 0)) {
+        if (ftv && !(tt_env && atoi(tt_env) == 0)) {
             HIPCHK(g->ttvis.alloc((size_t)2 * nt * tvw));   // ttvis, then ttany
             hipLaunchKernelGGL(tile_tt_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, nt, tvw, g->regular_tiles.p,
                                g->ftvis.p, g->tvis.p, g->ttvis.p, g->ttvis.p + (size_t)nt * tvw);
             HIPCHK(hipGetLastError());
         }
         const char* pm_env = getenv("DMX_VGA_PMASK");
-        if (ftv_on && !(pm_env && atoi(pm_env) == 0))
+        if (ftv && !(pm_env && atoi(pm_env) == 0))
             if (int rc = prepare_pmask(g, rows, tw, th, tvw, Ct)) return rc;
         g->tvw = tvw;
     }

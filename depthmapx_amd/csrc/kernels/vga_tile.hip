@@ -357,8 +357,7 @@ __device__ __forceinline__ bool special_hit(const VgaTileParams& P, const FView&
     if (P.tvis) {
         const unsigned long long* tv = P.tvis + (size_t)id * P.tvw;
         unsigned long long ta = 0ull;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
+        for (int j = 0; j * 64 < P.tvw; j++) {
             const int w = j * 64 + lane;
             if (w < P.tvw) ta |= tv[w] & FV.Fsr[w];
         }
@@ -886,8 +885,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             const unsigned long long* fv0 = P.ftvis ? P.ftvis + (size_t)(r0 ? v0 : 0) * P.tvw : nullptr;
                             const unsigned long long* fv1 = P.ftvis ? P.ftvis + (size_t)(r1 ? v1 : 0) * P.tvw : nullptr;
                             unsigned long long fa0 = 0ull, ta0 = 0ull, fa1 = 0ull, ta1 = 0ull;
-#pragma unroll
-                            for (int k = 0; k < 4; k++) {
+                            // 4 row words a lane up to 1024 cells a side, more on wider grids (tvis alone)
+#pragma unroll 4
+                            for (int k = 0; k * 64 < P.tvw; k++) {
                                 const int w = k * 64 + lane;
                                 const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
                                 if (fs) {   // rows are read only under frontier tile rows

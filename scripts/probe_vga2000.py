@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--nsrc", type=int, default=1024)
     ap.add_argument("--blocks", type=int, default=4)
     ap.add_argument("--check-do", type=int, default=0, help="sources of the first block re-run on vga_do and compared")
+    ap.add_argument("--alphas", default="", help="comma list: re-time the first block with DMX_VGA_ALPHA set to each")
     a = ap.parse_args()
     W = 1999
     ctx = dmx.Context(0)
@@ -46,8 +47,22 @@ def main():
                               "frontier_hbm": st.get("vga_frontier_hbm"), "mean_count": float(out[b:b + per, 5].mean()),
                               "bottom_up_levels": st["vga_bottom_up_levels"], "top_down_levels": st["vga_top_down_levels"],
                               "runs_tested": st["vga_runs_expanded"], "hard_cells": st["vga_hard_cells"],
-                              "hard_runs": st["vga_hard_runs"], "cr_tiles": st["vga_cr_tiles"]})
+                              "hard_runs": st["vga_hard_runs"], "cr_tiles": st["vga_cr_tiles"],
+                              "b_cells": st["vga_b_cells"], "phase_cycles": ctx.last_phase_cycles()})
         print(json.dumps(rec["blocks"][-1]), file=sys.stderr, flush=True)
+    for al in [x for x in a.alphas.split(",") if x]:
+        os.environ["DMX_VGA_ALPHA"] = al
+        b = starts[0]
+        out = g.vga_visual_global(src_begin=b, src_end=b + per)
+        st = ctx.last_stats()
+        same = bool(np.array_equal(out[b:b + per].view(np.uint32), outs[0].view(np.uint32)))
+        rec.setdefault("alpha_sweep", []).append({"alpha": int(al), "kernel_s": ctx.last_timing()[1], "identical": same,
+                                                  "bottom_up_levels": st["vga_bottom_up_levels"],
+                                                  "top_down_levels": st["vga_top_down_levels"],
+                                                  "runs_tested": st["vga_runs_expanded"],
+                                                  "phase_cycles": ctx.last_phase_cycles()})
+        print(json.dumps(rec["alpha_sweep"][-1]), file=sys.stderr, flush=True)
+        os.environ.pop("DMX_VGA_ALPHA")
     if a.check_do:
         os.environ["DMX_VGA_KERNEL"] = "do"
         b = starts[0]
