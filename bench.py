@@ -508,7 +508,10 @@ def main():
                         "vga_partial_tile_mask_loads": stats.get("vga_pmask_loads"),
                         "vga_partial_tile_mask_bytes": stats.get("vga_pmask_bytes"),
                         "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc,
-                        "makegraph_algorithmic_bytes": mk_bytes, "vga_algorithmic_bytes": vga_bytes},
+                        "makegraph_algorithmic_bytes": mk_bytes, "vga_algorithmic_bytes": vga_bytes,
+                        # the bottom-up BFS's symmetry test and early-exit universe rest on 64-bit random-weight
+                        # sums (prep): a node misclassified with probability 2^-64 each
+                        "vga_certificate_failure_bound": 2.0 * N / 2.0 ** 64 if not stepdepth else None},
             "roofline": roof,
         }
         if kt["exchange_s"] or mk_auto:

@@ -263,6 +263,7 @@ struct dmx_graph {
     DevBuf<unsigned long long> tvis;   // tile-visibility rows (empty: not built / too large)
     DevBuf<unsigned long long> ftvis;  // full-visibility rows (every non-seed cell of the tile seen)
     DevBuf<unsigned long long> ttvis;  // tile-to-tile full visibility (AND of ftvis over regular cells)
+    DevBuf<unsigned long long> tvsum;  // wide grids: per cell, one bit per non-zero tvis row word
     DevBuf<unsigned long long> pmask;  // partial-tile masks (the cells of each partly seen tile a cell sees)
     DevBuf<int64_t> poff;              // [Ct + 1] start of each cell's masks
     DevBuf<uint16_t> ppre;             // [Ct][tvw] partial tiles of a cell before each row word
@@ -877,7 +878,13 @@ int dmx_pointmap_cell_lines(dmx_pointmap* pm, int32_t* counts, double* pieces, i
 // 6.9 s, 4: 5.4 s, 5: 4.9 s (96 VGPRs, some cold spills), 6: 5.4 s.  fixed: the first pass (LDS
 // capacities, certified moment sums and the maxdist test compiled in); count: the cost-sample counters.
 typedef void (*mk_kernel_t)(const MakeGraphParams*);
-#define MKK(PROF, FIXED, COUNT, MAXD, FAR) makegraph_kernel<5, PROF, FIXED, COUNT, MAXD, FAR>
+// waves per SIMD the makeGraph register allocation targets (A/B builds: -DDMX_MK_WPE=n).  Measured round 4
+// (profiles/r4_makegraph_wpe_ab.jsonl, configs[2] / configs[4]): 5 -> 4.62 / 10.65 s, 6 -> 5.20 / 11.99 s,
+// 8 -> 9.10 / 19.31 s: fewer registers spill more than the extra waves hide
+#ifndef DMX_MK_WPE
+#define DMX_MK_WPE 5
+#endif
+#define MKK(PROF, FIXED, COUNT, MAXD, FAR) makegraph_kernel<DMX_MK_WPE, PROF, FIXED, COUNT, MAXD, FAR>
 static mk_kernel_t mk_kernel(bool fixed, bool count, bool maxd, bool far) {
     if (count) {       // the cost sample of dmx_makegraph_balance: always counts (its bounds depend on it)
         if (!fixed || maxd) return MKK(false, false, true, false, false);
@@ -1783,6 +1790,12 @@ static int prepare_tiles(dmx_graph* g) {
         const char* pm_env = getenv("DMX_VGA_PMASK");
         if (ftv && !(pm_env && atoi(pm_env) == 0))
             if (int rc = prepare_pmask(g, rows, tw, th, tvw, Ct)) return rc;
+        if (wide) {
+            HIPCHK(g->tvsum.alloc((size_t)Ct * ((tvw + 63) / 64)));
+            hipLaunchKernelGGL(tile_vsum_kernel, dim3((unsigned)((Ct + 3) / 4)), dim3(256), 0, s, Ct, tvw, g->tvis.p,
+                               g->tvsum.p);
+            HIPCHK(hipGetLastError());
+        }
         g->tvw = tvw;
     }
     HIPCHK(hipStreamSynchronize(s));
@@ -1862,6 +1875,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.cr = g->cr.p; Q.heads = g->heads.p; Q.tscan_start = g->tscan_start.p; Q.tnruns = g->tnruns.p;
     Q.scan_pool = g->scan_pool.p;
     Q.tvis = g->tvw ? g->tvis.p : nullptr; Q.tvw = g->tvw;
+    Q.tvsum = (g->tvw && g->tvsum.p) ? g->tvsum.p : nullptr;
     Q.ftvis = (g->tvw && g->ftvis.p) ? g->ftvis.p : nullptr;
     Q.ttvis = (g->tvw && g->ttvis.p) ? g->ttvis.p : nullptr;
     Q.ttany = Q.ttvis ? g->ttvis.p + (size_t)tw * th * g->tvw : nullptr;

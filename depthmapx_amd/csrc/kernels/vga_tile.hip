@@ -51,6 +51,7 @@ struct VgaTileParams {
     const int64_t* poff;                      // [nt*64 + 1] start of each cell's masks in pmask
     const uint16_t* ppre;                     // [nt*64][tvw] partial tiles of the cell before each row word
     int tvw;                                  // th * ceil(tw / 64)
+    const unsigned long long* tvsum;          // [nt*64][ceil(tvw / 64)] non-zero row words (wide grids; null: off)
     const int32_t* node_cell;
     const int32_t* cell_node;
     const uint8_t* node_flags;
@@ -885,19 +886,45 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             const unsigned long long* fv0 = P.ftvis ? P.ftvis + (size_t)(r0 ? v0 : 0) * P.tvw : nullptr;
                             const unsigned long long* fv1 = P.ftvis ? P.ftvis + (size_t)(r1 ? v1 : 0) * P.tvw : nullptr;
                             unsigned long long fa0 = 0ull, ta0 = 0ull, fa1 = 0ull, ta1 = 0ull;
-                            // 4 row words a lane up to 1024 cells a side, more on wider grids (tvis alone)
+                            if (!P.tvsum) {
+                                // 4 row words a lane up to 1024 cells a side
 #pragma unroll 4
-                            for (int k = 0; k * 64 < P.tvw; k++) {
-                                const int w = k * 64 + lane;
-                                const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
-                                if (fs) {   // rows are read only under frontier tile rows
-                                    if (r0) {
-                                        ta0 |= tv0[w] & fs;
-                                        if (fv0) fa0 |= fv0[w] & fs;
+                                for (int k = 0; k * 64 < P.tvw; k++) {
+                                    const int w = k * 64 + lane;
+                                    const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
+                                    if (fs) {   // rows are read only under frontier tile rows
+                                        if (r0) {
+                                            ta0 |= tv0[w] & fs;
+                                            if (fv0) fa0 |= fv0[w] & fs;
+                                        }
+                                        if (r1) {
+                                            ta1 |= tv1[w] & fs;
+                                            if (fv1) fa1 |= fv1[w] & fs;
+                                        }
                                     }
-                                    if (r1) {
-                                        ta1 |= tv1[w] & fs;
-                                        if (fv1) fa1 |= fv1[w] & fs;
+                                }
+                            } else {
+                                // wider grids (tvis alone): the row summaries leave out the words that are
+                                // zero for the cell; summary word k (lane k) holds bit `lane` for row word w
+                                const int tvsw = (P.tvw + 63) / 64;
+                                unsigned long long sm0 = 0ull, sm1 = 0ull;
+                                if (lane < tvsw) {
+                                    sm0 = r0 ? P.tvsum[(size_t)v0 * tvsw + lane] : 0ull;
+                                    sm1 = r1 ? P.tvsum[(size_t)v1 * tvsw + lane] : 0ull;
+                                }
+                                for (int k = 0; k < tvsw; k++) {
+                                    const int w = k * 64 + lane;
+                                    const unsigned long long s0 =
+                                        (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)sm0, k) |
+                                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(sm0 >> 32), k) << 32);
+                                    const unsigned long long s1 =
+                                        (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)sm1, k) |
+                                        ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(sm1 >> 32), k) << 32);
+                                    if (!((s0 | s1) >> lane & 1ull)) continue;
+                                    const unsigned long long fs = Fsr[w];   // w < tvw: its summary bit is set
+                                    if (fs) {
+                                        if ((s0 >> lane) & 1ull) ta0 |= tv0[w] & fs;
+                                        if ((s1 >> lane) & 1ull) ta1 |= tv1[w] & fs;
                                     }
                                 }
                             }
@@ -1147,6 +1174,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.mcorr = 0; S.mdisc = 0;
                 S.tn[level & 1] = 0;   // this level's list is spent; it is the next level's append target
             }
+            // the next level's first appends (phase A's queue, the top-down frontier list) must not race
+            // the resets above: a wave that appended before them lost its entries
+            __syncthreads();
             if (cnt == 0) break;
             if (level + 1 >= VGA_HMAX) { overflow = true; break; }
             if (tid == 0) hist[level + 1] = (int)(cnt - mcorr);
@@ -1443,6 +1473,23 @@ __global__ void tile_tt_kernel(int nt, int tvw, const unsigned long long* regula
         }
         ttvis[(size_t)t * tvw + w] = acc;
         ttany[(size_t)t * tvw + w] = any;
+    }
+}
+
+// Row summary of the tile-visibility rows on wide grids (tvw > 256 words, no masks): bit w of a cell's
+// summary is set iff its row word w is non-zero, so phase C's miss certificate reads only the words the
+// cell has (a dense map's cell sees a few % of the tiles) instead of every word under a frontier tile row.
+// One wave per cell: summary word j is the ballot of row words 64j .. 64j + 63 being non-zero.
+__global__ void tile_vsum_kernel(int64_t Ct, int tvw, const unsigned long long* tvis, unsigned long long* tvsum) {
+    const int lane = threadIdx.x & 63;
+    const int64_t c = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (c >= Ct) return;
+    const int tvsw = (tvw + 63) / 64;
+    const unsigned long long* row = tvis + (size_t)c * tvw;
+    for (int j = 0; j < tvsw; j++) {
+        const int w = j * 64 + lane;
+        const unsigned long long bits = __ballot(w < tvw && row[w] != 0ull);
+        if (lane == 0) tvsum[(size_t)c * tvsw + j] = bits;
     }
 }
 

@@ -48,7 +48,9 @@ def main():
                               "bottom_up_levels": st["vga_bottom_up_levels"], "top_down_levels": st["vga_top_down_levels"],
                               "runs_tested": st["vga_runs_expanded"], "hard_cells": st["vga_hard_cells"],
                               "hard_runs": st["vga_hard_runs"], "cr_tiles": st["vga_cr_tiles"],
-                              "b_cells": st["vga_b_cells"], "phase_cycles": ctx.last_phase_cycles()})
+                              "b_cells": st["vga_b_cells"], "pruned_cells": st["vga_pruned_cells"],
+                              "certain_hits": st["vga_hard_certain"], "c_busy_cycles": st["vga_c_busy"],
+                              "c_scan_cycles": st["vga_c_scan"], "phase_cycles": ctx.last_phase_cycles()})
         print(json.dumps(rec["blocks"][-1]), file=sys.stderr, flush=True)
     for al in [x for x in a.alphas.split(",") if x]:
         os.environ["DMX_VGA_ALPHA"] = al
