@@ -72,13 +72,15 @@ def nearest_filled(pm, x, y):
     raise RuntimeError("no filled cell")
 
 
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r3_pmc.json")
+# the newest round's PMC summary of the shipped build (scripts/gpu_r4_evidence.sh writes r4)
+PMC_SUMMARY = next((p for p in (os.path.join(REPO, "profiles", "r%d_pmc.json" % r) for r in (4, 3)) if os.path.exists(p)),
+                   os.path.join(REPO, "profiles", "r4_pmc.json"))
 FP64_PEAK_TF = 78.6    # MI355X FP64 vector (MI355X_MICROARCH.md)
 
 
 def load_pmc(workload):
     """Per-kernel PMC summary of the same workload and build (scripts/gpu_pmc.sh -> scripts/pmc_summary.py ->
-    profiles/r3_pmc.json): HBM bytes raw and 2x-FETCH corrected, L2 hit rate, VALU issue, FP64 instruction
+    profiles/r4_pmc.json): HBM bytes raw and 2x-FETCH corrected, L2 hit rate, VALU issue, FP64 instruction
     counts."""
     if not os.path.exists(PMC_SUMMARY):
         return {}

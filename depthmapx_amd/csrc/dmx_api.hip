@@ -1983,13 +1983,13 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[21] = (long long)st[19];                          // phase-B cells
     ctx->last_stats[22] = (long long)st[20];                          // phase-B tiles resolved by ttvis
     ctx->last_stats[27] = (long long)st[25];                          // phase-B tiles pruned by ttany
-    ctx->last_stats[28] = (long long)st[26];                          // phase-B row-test clocks (wave)
+    ctx->last_stats[28] = (long long)st[26];                          // phase-B row-test clocks (not collected: 0)
     ctx->last_stats[29] = (long long)st[27];                          // phase-B tiles with cell tests
-    ctx->last_stats[30] = (long long)st[28];                          // phase-B cell-test clocks (wave)
+    ctx->last_stats[30] = (long long)st[28];                          // phase-B cell-test clocks (not collected: 0)
     ctx->last_stats[31] = (long long)st[29];                          // phase-B cells past hint + 4 heads
     ctx->last_stats[23] = (long long)st[21];                          // phase-C busy clocks summed over waves
-    ctx->last_stats[24] = (long long)st[22];                          // phase-C run-scan clocks summed over waves
-    ctx->last_stats[25] = (long long)st[23];                          // phase-C special-node clocks
+    ctx->last_stats[24] = (long long)st[22];                          // phase-C per-cell clocks (not collected: 0)
+    ctx->last_stats[25] = (long long)st[23];                          // phase-C special-node clocks (not collected: 0)
     ctx->last_stats[26] = (long long)st[24];                          // phase-C special-node tests
     ctx->last_stats[3] = 3 | ((long long)g->nspecial << 8);
     ctx->last_stats[4] = (long long)st[0];

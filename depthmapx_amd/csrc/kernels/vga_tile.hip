@@ -383,6 +383,34 @@ __device__ __forceinline__ bool special_hit(const VgaTileParams& P, const FView&
     return false;
 }
 
+// The in-set corrections of an asymmetric node v (whole wave): whether a frontier cell is in Extra(v) (an
+// in-neighbour outside cells(v): a hit), and how many frontier cells are in Missing(v) (cells of v that are not
+// in-neighbours; Missing(v) is a subset of cells(v), built in prepare_symmetry).  With none of the latter,
+// v's in-set meets F iff cells(v) does, which the partial-tile masks decide as for a regular cell.
+__device__ __forceinline__ bool special_extra_hit(const VgaTileParams& P, const unsigned long long* F, int node,
+                                                  int* nmiss_f) {
+    const int lane = threadIdx.x & 63;
+    const int tw = P.tw, rows = P.rows;
+    const int si = P.spec_index[node];
+    const int e0 = P.extra_off[si], e1 = P.extra_off[si + 1];
+    const int m0 = P.missing_off[si], m1 = P.missing_off[si + 1];
+    bool h = false;
+    int nm = 0;
+    for (int j = e0 + lane; j < e1; j += 64) {
+        const int uc = P.node_cell[P.extra[j]];
+        const int ux = uc / rows, uy = uc % rows;
+        if (F[(uy >> 3) * tw + (ux >> 3)] & (1ull << ((uy & 7) * 8 + (ux & 7)))) h = true;
+    }
+    for (int j = m0 + lane; j < m1; j += 64) {
+        const int mc = P.node_cell[P.missing[j]];
+        const int mx = mc / rows, my = mc % rows;
+        if ((F[(my >> 3) * tw + (mx >> 3)] >> ((my & 7) * 8 + (mx & 7))) & 1ull) nm++;
+    }
+    for (int off = 32; off >= 1; off >>= 1) nm += __shfl_xor(nm, off);
+    *nmiss_f = nm;
+    return __ballot(h) != 0ull;
+}
+
 __device__ __forceinline__ int wave_incl_scan(int v) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
@@ -682,14 +710,15 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 const int ntl = S.tn[level & 1];
                 for (int t0 = 0; t0 < ntl; t0 += NT) {
                     const int t = t0 + tid < ntl ? TLc[t0 + tid] : nt;
-                    unsigned long long U = 0ull;
+                    unsigned long long U = 0ull, rg = ~0ull;
                     if (t < nt) {
                         // V, the regular mask and the CRK common runs in one round trip
                         Run c[CRK];
 #pragma unroll
                         for (int j = 0; j < CRK; j++) c[j] = P.cr[CRK * t + j];
                         U = ~Vg[t];
-                        const unsigned long long R = U & P.regular_tiles[t];
+                        rg = P.regular_tiles[t];
+                        const unsigned long long R = U & rg;
                         if (R) {
 // B_ORDER: the hint's operand is loaded before the head tests and tested after them (-0.7 %)
 // RB_INC: line summaries set per published tile with LDS atomics instead of rebuilt from F (measured
@@ -714,7 +743,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         base = __shfl(base, 0);
                         if (U) {
                             const int pos = base + __popcll(want & ((1ull << lane) - 1ull));
-                            Q[pos] = make_int4(t, 0, (int)(unsigned)(U & 0xFFFFFFFFull), (int)(unsigned)(U >> 32));
+                            // .y: the tile still holds an asymmetric cell (phase B then loads the regular mask)
+                            Q[pos] = make_int4(t, (U & ~rg) ? 1 : 0, (int)(unsigned)(U & 0xFFFFFFFFull),
+                                               (int)(unsigned)(U >> 32));
                         }
                     }
                 }
@@ -729,7 +760,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 // leave open then test the hint run, the heads and the next bext runs of their scan
                 // order.  Misses go to the hard list.
                 for (;;) {
-                    // dynamic: the few tiles that need cell tests cost ~100x a row-resolved one
+                    // dynamic: the few tiles that need cell tests cost ~100x a row-resolved one; the regular
+                    // mask is loaded only for tiles that hold an asymmetric cell (flagged in the entry), so
+                    // the cell loads follow the entry without a round trip of their own
                     int it = 0;
                     if (lane == 0) it = atomicAdd(&S.bn, 1);
                     it = __shfl(it, 0);
@@ -738,7 +771,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const int t = e.x;
                     unsigned long long mask = (unsigned long long)(unsigned)e.z | ((unsigned long long)(unsigned)e.w << 32);
                     const int id = (t << 6) | lane;
-                    const unsigned long long reg = P.regular_tiles[t];
+                    const unsigned long long reg = (SPECIAL && e.y) ? P.regular_tiles[t] : ~0ull;
                     const bool lreg = !SPECIAL || ((reg >> lane) & 1ull);
                     const bool cand = ((mask >> lane) & 1ull) && lreg;
                     int64_t ss = 0;
@@ -769,7 +802,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         }
                     }
                     if (lane == 0) { ST(18, 1); ST(19, __popcll(mask)); }
-                    const unsigned long long bt0 = __builtin_amdgcn_s_memtime();
                     if (__ballot(acc != 0ull) != 0ull) {
                         // a frontier tile every regular cell of t sees completely
                         const unsigned long long R = mask & reg;
@@ -781,8 +813,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         mask &= ~reg;
                     }
                     const bool mine = (mask >> lane) & 1ull;
-                    const unsigned long long bt1 = __builtin_amdgcn_s_memtime();
-                    if (lane == 0) { ST(26, bt1 - bt0); if (__ballot(mine)) ST(27, 1); }
+                    if (__ballot(mine) && lane == 0) ST(27, 1);
                     bool hit = false, to_hard = false;
                     int hard_val = 0;
                     if (mine && !lreg) {
@@ -845,7 +876,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         }
                     }
                     const unsigned long long hm = __ballot(hit);
-                    if (lane == 0) ST(28, __builtin_amdgcn_s_memtime() - bt1);
                     if (hm && lane == 0) or_wg(&Xg[t], hm);
                     const unsigned long long hw = __ballot(to_hard);
                     if (hw) {
@@ -956,12 +986,19 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         if (SPECIAL && special) {
                             int x, y;
                             xy_of_tile_id(id, tw, x, y);
-                            const unsigned long long sp_t0 = __builtin_amdgcn_s_memtime();
-                            found = special_hit(P, FV, id, x, y, &nr);
-                            if (lane == 0) { ST(23, __builtin_amdgcn_s_memtime() - sp_t0); ST(24, 1); }
-                            if (lane == 0) rt += (unsigned)nr;
+                            int nmiss = 1;
+                            if (P.pmask) found = special_extra_hit(P, F, P.cell_node[x * rows + y], &nmiss);
+                            if (!found && nmiss == 0) {
+                                // no Missing cell in the frontier: in-set meets F iff cells(v) does (the masks)
+                                unsigned nl = 0;
+                                int how = 0;
+                                found = pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+                            } else if (!found) {
+                                found = special_hit(P, FV, id, x, y, &nr);
+                                if (lane == 0) rt += (unsigned)nr;
+                            }
+                            if (lane == 0) ST(24, 1);
                         } else if (P.pmask) {
-                            const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
                             unsigned nl = 0;
                             int how = 0;
                             found = pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
@@ -973,7 +1010,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             nl += __shfl_xor(nl, 32); nl += __shfl_xor(nl, 16); nl += __shfl_xor(nl, 8);
                             nl += __shfl_xor(nl, 4); nl += __shfl_xor(nl, 2); nl += __shfl_xor(nl, 1);
                             if (lane == 0) {
-                                ST(22, __builtin_amdgcn_s_memtime() - s_t0);
                                 ST(30, nl);
                                 ST(31, 1);
                                 if (found) ST(1, 1);
@@ -982,7 +1018,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             const int64_t rs = P.tscan_start[id];
                             nr = P.tnruns[id];
                             int base = KH + P.bext;   // the first KH + bext runs were tested in phase B
-                            const unsigned long long s_t0 = __builtin_amdgcn_s_memtime();
                             for (; base < nr && !found; base += CSTEP * 64) {
                                 Run rr[CSTEP];
 #pragma unroll
@@ -1006,7 +1041,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                 if (found && lane == 0) Hn[id] = (uint32_t)fpos;
                             }
                             if (lane == 0) {
-                                ST(22, __builtin_amdgcn_s_memtime() - s_t0);
                                 const unsigned long long sc = (unsigned long long)max(min(base, nr) - KH - P.bext, 0);
                                 rt += (unsigned)sc;
                                 ST(15, sc);

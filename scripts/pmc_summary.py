@@ -21,6 +21,7 @@ Per kernel (makegraph_kernel, vga_tile_kernel, ...), averaged per launch:
   fp64_flops          = 64 x (ADD + MUL + TRANS + 2 x FMA) F64 wave-instructions (an upper bound: the
                         counters count wave instructions, partially-masked waves count 64 lanes)
   fp64_tflops         = fp64_flops / duration, against the 78.6 TF FP64 vector peak
+  lds_conflict_*      = SQ_LDS_BANK_CONFLICT per SQ_INSTS_LDS, and as a share of SQ_LDS_IDX_ACTIVE
 """
 import collections
 import csv
@@ -105,6 +106,11 @@ def main():
                 e["wave_cycles_split"] = {"active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0) / wc,
                                           "wait_any": c.get("SQ_WAIT_ANY", 0) / wc,
                                           "wait_inst_any": c.get("SQ_WAIT_INST_ANY", 0) / wc}
+        if c.get("SQ_INSTS_LDS"):
+            # conflict cycles per LDS instruction, and their share of the cycles the LDS was busy indexing
+            e["lds_conflict_cycles_per_inst"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_INSTS_LDS"]
+            if c.get("SQ_LDS_IDX_ACTIVE"):
+                e["lds_conflict_frac_of_idx_active"] = c.get("SQ_LDS_BANK_CONFLICT", 0.0) / c["SQ_LDS_IDX_ACTIVE"]
         f64 = [c.get("SQ_INSTS_VALU_%s_F64" % t) for t in ("ADD", "MUL", "FMA", "TRANS")]
         if all(x is not None for x in f64):
             flops = 64.0 * (f64[0] + f64[1] + 2.0 * f64[2] + f64[3])
