@@ -1,6 +1,7 @@
 #!/bin/bash
-# Round-4 evidence in one call (the pool loses boxes often): PMC passes of configs[2] -> profiles/r4_pmc.json,
-# smoke(), the bench (STEPS/WARMUP, CPU leg), then the configs[4] PMC passes and its bench line.
+# Round-4 evidence: PART=2 -- configs[2] PMC passes -> profiles/r4_pmc.json, smoke(), the bench (STEPS/WARMUP,
+# CPU leg) under a kernel-trace + stats profile; PART=5 -- the configs[4] (bench --config 5) PMC passes and its
+# bench line.  The PMC summary is written here on the box and merged back through gpurun_out/.
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$PWD}
@@ -10,18 +11,25 @@ mkdir -p $OUT
 cd $R
 W2="synthetic-1000/50-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + VGA -vm visibility -vg -vr n"
 W5="synthetic-1999/5000-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + STEPDEPTH -sdt metric -sdp 1000,1000 (cell 2001000)"
-rm -f profiles/r4_pmc.json
-TAG=$T/pmc2 bash scripts/gpu_pmc.sh > $OUT/pmc2.log 2>&1 && \
-python3 scripts/pmc_summary.py gpurun_out/$T/pmc2 "$W2" profiles/r4_pmc.json > $OUT/pmc2_summary.log 2>&1 && \
-cp profiles/r4_pmc.json $OUT/ && \
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
-t0=$(date +%s.%N) && \
-timeout -k 10 600 python -u bench.py --gpus 1 --steps ${STEPS:-10} --warmup ${WARMUP:-2} > $OUT/bench.log 2> $OUT/bench_progress.txt && \
-t1=$(date +%s.%N) && echo "bench wall s: $(python -c "print($t1 - $t0)")" >> $OUT/bench_progress.txt && \
-TAG=$T/pmc5 BENCH_ARGS="--config 5" bash scripts/gpu_pmc.sh > $OUT/pmc5.log 2>&1 && \
-python3 scripts/pmc_summary.py gpurun_out/$T/pmc5 "$W5" profiles/r4_pmc.json > $OUT/pmc5_summary.log 2>&1 && \
-cp profiles/r4_pmc.json $OUT/ && \
-timeout -k 10 400 python -u bench.py --gpus 1 --config 5 --steps 2 --warmup 1 > $OUT/bench5.log 2> $OUT/bench5_progress.txt
-rc=$?
-tail -2 $OUT/smoke.log; grep '^{' $OUT/bench.log | cut -c1-300; tail -1 $OUT/bench_progress.txt; grep '^{' $OUT/bench5.log | cut -c1-300
+if [ "${PART:-2}" = 2 ]; then
+  TAG=$T/pmc2 bash scripts/gpu_pmc.sh > $OUT/pmc2.log 2>&1
+  rc=$?
+  python3 scripts/pmc_summary.py gpurun_out/$T/pmc2 "$W2" $OUT/r4_pmc.json > $OUT/pmc2_summary.log 2>&1
+  cp $OUT/r4_pmc.json profiles/r4_pmc.json   # the bench below reads it
+  [ $rc = 0 ] && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
+  t0=$(date +%s.%N) && \
+  timeout -k 10 600 python -u bench.py --gpus 1 --steps ${STEPS:-10} --warmup ${WARMUP:-2} > $OUT/bench.log 2> $OUT/bench_progress.txt && \
+  t1=$(date +%s.%N) && echo "bench wall s: $(python -c "print($t1 - $t0)")" >> $OUT/bench_progress.txt
+  rc=$?
+  tail -5 $OUT/pmc2.log; tail -2 $OUT/smoke.log; grep '^{' $OUT/bench.log | cut -c1-300; tail -1 $OUT/bench_progress.txt
+else
+  cp profiles/r4_pmc.json $OUT/r4_pmc.json 2>/dev/null
+  TAG=$T/pmc5 BENCH_ARGS="--config 5" bash scripts/gpu_pmc.sh > $OUT/pmc5.log 2>&1
+  rc=$?
+  python3 scripts/pmc_summary.py gpurun_out/$T/pmc5 "$W5" $OUT/r4_pmc.json > $OUT/pmc5_summary.log 2>&1
+  cp $OUT/r4_pmc.json profiles/r4_pmc.json
+  [ $rc = 0 ] && timeout -k 10 400 python -u bench.py --gpus 1 --config 5 --steps 2 --warmup 1 > $OUT/bench5.log 2> $OUT/bench5_progress.txt
+  rc=$?
+  tail -5 $OUT/pmc5.log; grep '^{' $OUT/bench5.log | cut -c1-300
+fi
 exit $rc
