@@ -9,6 +9,8 @@ T=${TAG:-r4evidence}
 OUT=$R/gpurun_out/$T
 mkdir -p $OUT
 cd $R
+( while true; do sleep 45; date +%s >> $OUT/heartbeat; done ) > /dev/null 2>&1 &
+HB=$!
 W2="synthetic-1000/50-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + VGA -vm visibility -vg -vr n"
 W5="synthetic-1999/5000-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + STEPDEPTH -sdt metric -sdp 1000,1000 (cell 2001000)"
 if [ "${PART:-2}" = 2 ]; then
@@ -28,8 +30,11 @@ else
   rc=$?
   python3 scripts/pmc_summary.py gpurun_out/$T/pmc5 "$W5" $OUT/r4_pmc.json > $OUT/pmc5_summary.log 2>&1
   cp $OUT/r4_pmc.json profiles/r4_pmc.json
-  [ $rc = 0 ] && timeout -k 10 400 python -u bench.py --gpus 1 --config 5 --steps 2 --warmup 1 > $OUT/bench5.log 2> $OUT/bench5_progress.txt
+  [ $rc = 0 ] && timeout -k 10 400 python -u bench.py --gpus 1 --config 5 --steps 2 --warmup 1 > $OUT/bench5.log 2> $OUT/bench5_progress.txt && \
+  DMX_TEST_WIDE=1 timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread -m gpu \
+    tests/test_gpu_scale.py -k "2000_vga_sources" > $OUT/vga2000_wide_tests.log 2>&1
   rc=$?
-  tail -5 $OUT/pmc5.log; grep '^{' $OUT/bench5.log | cut -c1-300
+  tail -5 $OUT/pmc5.log; grep '^{' $OUT/bench5.log | cut -c1-300; tail -2 $OUT/vga2000_wide_tests.log
 fi
+kill $HB
 exit $rc
