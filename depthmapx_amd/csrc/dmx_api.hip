@@ -255,6 +255,10 @@ struct dmx_graph {
     int nspecial = 0;
     std::vector<int32_t> special_nodes;
     DevBuf<int32_t> spec_index, extra_off, extra, missing_off, missing;
+    // the symmetry scatter done by makeGraph as it published the runs (sym_fused): consumed and freed by
+    // prepare_symmetry
+    DevBuf<unsigned long long> sym_prefix, sym_diff, sym_ho;
+    bool sym_fused = false;
     // tile-resolved BFS (vga_tile.hip)
     bool tiles_ready = false;
     DevBuf<int64_t> tscan_start;
@@ -951,6 +955,21 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         for (int64_t v : *only)
             if (v < node_begin || v >= node_end) return fail(DMX_ERR_ARG, "sample node outside the range");
     int64_t pool_cap = std::max<int64_t>(n_src * std::max<int64_t>(64, 6 * (int64_t)D), 1024);
+    // A whole-graph build does the VGA symmetry certificate's scatter as it publishes each source's runs
+    // (the runs are in the L2 then, and the memory-side atomics overlap the sweep), instead of a later pass
+    // over the 36 GB pool (0.38 s at 1000^2).  Ranges, samples and cost counts leave it to prepare_symmetry.
+    const bool fuse_sym = !only && d_work == nullptr && node_begin == 0 && node_end == N && N > 0 &&
+                          !getenv("DMX_MK_NOSYM");
+    const int64_t Cc = (int64_t)h.cols() * h.rows();
+    if (fuse_sym) {
+        HIPCHK(g->sym_prefix.alloc((size_t)4 * Cc));
+        HIPCHK(g->sym_diff.alloc((size_t)4 * Cc));
+        HIPCHK(g->sym_ho.alloc(N));
+        const int maxlines = h.cols() + h.rows();
+        hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, ctx->stream, h.cols(),
+                           h.rows(), pm->d_cell_node.p, g->sym_prefix.p, 0);
+        HIPCHK(hipGetLastError());
+    }
     ctx->last_mk_s = 0;
     DevBuf<int64_t> fail_list, node_list;
     DevBuf<MakeGraphParams> dP;   // kernel parameters in device memory (see makegraph_kernel)
@@ -979,6 +998,10 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         }
         bool pool_over = false;
         const int64_t pool_cap_full = pool_cap;
+        if (fuse_sym) {   // every pass publishes each source once; a restarted pass starts over
+            HIPCHK(hipMemsetAsync(g->sym_diff.p, 0, (size_t)4 * Cc * 8, ctx->stream));
+            HIPCHK(hipMemsetAsync(g->sym_ho.p, 0, (size_t)N * 8, ctx->stream));
+        }
         if (sampling) {
             std::vector<int64_t> sl((size_t)kSample);
             for (int64_t i = 0; i < kSample; i++) sl[i] = node_begin + (i * n) / kSample + n / (2 * kSample);
@@ -1062,6 +1085,10 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
             P.exact_moments = exact_pass ? 1 : 0;
             P.src_work = d_work;
             P.openh = openh.p; P.openh_n = openh_n;
+            const bool sym_pass = fuse_sym && !sampling;   // the sampling pass's runs are thrown away
+            P.sym_prefix = sym_pass ? g->sym_prefix.p : nullptr;
+            P.sym_diff = sym_pass ? g->sym_diff.p : nullptr;
+            P.sym_ho = sym_pass ? g->sym_ho.p : nullptr;
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
                 HIPCHK(dP.alloc(1));
@@ -1148,6 +1175,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         ctx->last_stats[34] = (long long)reruns;
         ctx->last_mk_s = mk_total_s + kernel_s;   // every pass counted (sample, overflow re-runs)
         g->nruns = (int64_t)used;
+        if (fuse_sym) { g->sym_fused = true; g->sym_prefix.reset(); }   // the prefix sums are no longer needed
         VLOG("makegraph: kernels %.3f s, total %.3f s\n", kernel_s, now_s() - t_start);
         *out = g.release();
         return DMX_OK;
@@ -1520,44 +1548,58 @@ static int prepare_uf(dmx_graph* g) {
 static int prepare_symmetry(dmx_graph* g) {
     if (g->symmetric >= 0) return DMX_OK;
     const char* force = getenv("DMX_VGA_KERNEL");
-    if (force && std::string(force) == "topdown") { g->symmetric = 0; return DMX_OK; }
+    if (force && std::string(force) == "topdown") {
+        g->symmetric = 0;
+        g->sym_diff.reset(); g->sym_ho.reset(); g->sym_fused = false;
+        return DMX_OK;
+    }
     dmx_ctx* ctx = g->ctx;
     hipStream_t s = ctx->stream;
     PointMapHost& h = *g->pm->host;
     const int cols = h.cols(), rows = h.rows();
     const int64_t C = (int64_t)cols * rows, N = g->nnodes;
     const int kSpecLimit = 4096;
-    DevBuf<unsigned long long> prefix, diff, ho;
+    DevBuf<unsigned long long> prefix, diff_own, ho_own;
     DevBuf<int32_t> flist;
     DevBuf<int> fcount;
-    HIPCHK(prefix.alloc((size_t)4 * C));
-    HIPCHK(diff.alloc((size_t)4 * C));
-    HIPCHK(ho.alloc(std::max<int64_t>(N, 1)));
     HIPCHK(flist.alloc(kSpecLimit));
     HIPCHK(fcount.alloc(1));
-    HIPCHK(hipMemsetAsync(diff.p, 0, (size_t)4 * C * 8, s));
-    HIPCHK(hipMemsetAsync(ho.p, 0, (size_t)std::max<int64_t>(N, 1) * 8, s));
     HIPCHK(hipMemsetAsync(fcount.p, 0, 4, s));
     const int maxlines = cols + rows;
-    hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
-                       g->pm->d_cell_node.p, prefix.p, 0);
-    HIPCHK(hipGetLastError());
-    int64_t pb, pe;
-    prep_range(g, pb, pe);
-    if (pe > pb) {
-        hipLaunchKernelGGL(sym_scatter_kernel, dim3((unsigned)std::min<int64_t>(pe - pb, 4096)), dim3(256), 0, s, cols,
-                           rows, g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb, g->node_nruns.p + pb,
-                           g->pool.p, prefix.p, diff.p, ho.p + pb);
+    unsigned long long *diff = nullptr, *ho = nullptr;
+    if (g->sym_fused) {
+        // makeGraph did the scatter over the whole graph as it published the runs: complete on every rank,
+        // so no all-reduce either
+        diff = g->sym_diff.p;
+        ho = g->sym_ho.p;
+    } else {
+        HIPCHK(prefix.alloc((size_t)4 * C));
+        HIPCHK(diff_own.alloc((size_t)4 * C));
+        HIPCHK(ho_own.alloc(std::max<int64_t>(N, 1)));
+        diff = diff_own.p;
+        ho = ho_own.p;
+        HIPCHK(hipMemsetAsync(diff, 0, (size_t)4 * C * 8, s));
+        HIPCHK(hipMemsetAsync(ho, 0, (size_t)std::max<int64_t>(N, 1) * 8, s));
+        hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
+                           g->pm->d_cell_node.p, prefix.p, 0);
         HIPCHK(hipGetLastError());
+        int64_t pb, pe;
+        prep_range(g, pb, pe);
+        if (pe > pb) {
+            hipLaunchKernelGGL(sym_scatter_kernel, dim3((unsigned)std::min<int64_t>(pe - pb, 4096)), dim3(256), 0, s,
+                               cols, rows, g->pm->d_node_cell.p + pb, pe - pb, g->node_run_start.p + pb,
+                               g->node_nruns.p + pb, g->pool.p, prefix.p, diff, ho + pb);
+            HIPCHK(hipGetLastError());
+        }
+        if (int rc = prep_allreduce(g, diff, (int64_t)4 * C, DMX_I64)) return rc;
+        if (int rc = prep_allreduce(g, ho, N, DMX_I64)) return rc;
     }
-    if (int rc = prep_allreduce(g, diff.p, (int64_t)4 * C, DMX_I64)) return rc;
-    if (int rc = prep_allreduce(g, ho.p, N, DMX_I64)) return rc;
     hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
-                       g->pm->d_cell_node.p, diff.p, 1);
+                       g->pm->d_cell_node.p, diff, 1);
     HIPCHK(hipGetLastError());
     if (N) {
         hipLaunchKernelGGL(sym_flag_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, s, rows,
-                           g->pm->d_node_cell.p, N, C, diff.p, ho.p, fcount.p, flist.p, kSpecLimit);
+                           g->pm->d_node_cell.p, N, C, diff, ho, fcount.p, flist.p, kSpecLimit);
         HIPCHK(hipGetLastError());
     }
     // U_f straight from the in-set hashes (uf_hi_tiles_kernel): no separate coverage pass
@@ -1568,13 +1610,14 @@ static int prepare_symmetry(dmx_graph* g) {
     HIPCHK(g->uf_tiles.alloc((size_t)tw * th));
     HIPCHK(g->notuf_tiles.alloc((size_t)tw * th));
     hipLaunchKernelGGL(uf_hi_tiles_kernel, dim3((tw * th + 255) / 256), dim3(256), 0, s, cols, rows, tw, th,
-                       g->pm->d_cell_node.p, diff.p, g->uf_tiles.p, g->notuf_tiles.p, ufcnt.p);
+                       g->pm->d_cell_node.p, diff, g->uf_tiles.p, g->notuf_tiles.p, ufcnt.p);
     HIPCHK(hipGetLastError());
     int nspec = 0;
     unsigned long long ufc = 0;
     HIPCHK(hipMemcpyAsync(&nspec, fcount.p, 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(&ufc, ufcnt.p, 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
+    g->sym_diff.reset(); g->sym_ho.reset(); g->sym_fused = false;   // consumed
     g->uf_count = (int64_t)ufc;
     g->nspecial = nspec;
     if (nspec == 0) { g->symmetric = 1; return DMX_OK; }

@@ -135,4 +135,40 @@ __device__ __forceinline__ void merge_order_check(const int2* mamb, int nmamb, i
     }
 }
 
+__device__ __host__ __forceinline__ unsigned long long cell_weight(unsigned long long c) {
+    unsigned long long z = c * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// direction of a run: 0 along x, 1 along y, 2 along (+1,+1), 3 along (+1,-1); single cells use 0
+__device__ __forceinline__ int run_dir(Run ru) {
+    if (ru.y0 == ru.y1) return 0;
+    if (ru.x0 == ru.x1) return 1;
+    return (ru.y1 > ru.y0) ? 2 : 3;
+}
+__device__ __forceinline__ void dir_step(int dir, int& dx, int& dy) {
+    dx = (dir == 1) ? 0 : 1;
+    dy = (dir == 0) ? 0 : ((dir == 3) ? -1 : 1);
+}
+
+// One run of node u: its share of HO(u) (the prefix-sum difference of the weights along the run's line) and
+// the range add of s(u) over the run's cells into the difference arrays D (memory-side atomics).
+__device__ __forceinline__ unsigned long long sym_run_scatter(Run ru, unsigned long long su, int cols, int rows,
+                                                              const unsigned long long* prefix, unsigned long long* diff) {
+    const int64_t C = (int64_t)cols * rows;
+    const int dir = run_dir(ru);
+    int dx, dy;
+    dir_step(dir, dx, dy);
+    const int px = ru.x0 - dx, py = ru.y0 - dy, ex = ru.x1 + dx, ey = ru.y1 + dy;
+    const unsigned long long* P = prefix + (int64_t)dir * C;
+    unsigned long long acc = P[(int64_t)ru.x1 * rows + ru.y1];
+    if (px >= 0 && px < cols && py >= 0 && py < rows) acc -= P[(int64_t)px * rows + py];
+    unsigned long long* D = diff + (int64_t)dir * C;
+    atomicAdd(&D[(int64_t)ru.x0 * rows + ru.y0], su);
+    if (ex >= 0 && ex < cols && ey >= 0 && ey < rows) atomicAdd(&D[(int64_t)ex * rows + ey], (unsigned long long)(0ull - su));
+    return acc;
+}
+
 } // namespace dmx

@@ -70,6 +70,11 @@ struct MakeGraphParams {
     uint32_t* src_work;        // optional [n][2]: depth steps and candidate chunks of each published source
     uint32_t* openh;           // per wave: open-run state of rows >= MK_OPEN_LDS (zeroed by the host, kept zero)
     int openh_n;               // its length per wave: max(0, dmax + 4 - MK_OPEN_LDS)
+    // the VGA symmetry certificate's scatter, done as each source publishes its runs (null: off; vga_do.hip
+    // prepare_symmetry then scans the pool): HO per node and the range adds of s(u) along each run's line
+    const unsigned long long* sym_prefix;   // [4][C] line prefix sums of the cell weights
+    unsigned long long* sym_diff;           // [4][C] difference arrays (zeroed by the host per pass)
+    unsigned long long* sym_ho;             // [N] (indexed by node - node_begin)
 };
 
 // phase clocks (profile builds of a run only; wave-uniform scalar reads)
@@ -994,12 +999,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             P.node_run_start[k] = -1;
         } else {
             int64_t dst = (int64_t)base;
+            const bool sym = P.sym_diff != nullptr;
+            const unsigned long long su = sym ? cell_weight((unsigned long long)cell) : 0ull;
+            unsigned long long ho = 0ull;   // 64-bit wrap-around: the order of the terms does not matter
             for (int si = 0; si < 8; si++) {
                 int q = c_seg_order[si];
                 const Run* src = stB + L.misc[16 + q];
                 const int len = L.misc[24 + q];
-                for (int i = lane; i < len; i += 64) P.pool[dst + i] = src[i];
+                for (int i = lane; i < len; i += 64) {
+                    const Run r = src[i];
+                    P.pool[dst + i] = r;
+                    if (sym) ho += sym_run_scatter(r, su, P.cols, P.rows, P.sym_prefix, P.sym_diff);
+                }
                 dst += len;
+            }
+            if (sym) {
+                for (int off = 32; off >= 1; off >>= 1) ho += __shfl_xor(ho, off);
+                if (lane == 0) P.sym_ho[k] = ho;
             }
             if (lane == 0) P.node_run_start[k] = (int64_t)base;
         }

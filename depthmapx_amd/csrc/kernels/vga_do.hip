@@ -460,23 +460,7 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
 // Extra (in-neighbours outside cells(v)) / Missing (cells(v) members that are not in-neighbours)
 // lists built from their explicit cell sets.  Range sums / range adds along rows, columns and both
 // diagonals make this O(runs).
-__device__ __host__ __forceinline__ unsigned long long cell_weight(unsigned long long c) {
-    unsigned long long z = c * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
-
-// direction of a run: 0 along x, 1 along y, 2 along (+1,+1), 3 along (+1,-1); single cells use 0
-__device__ __forceinline__ int run_dir(Run ru) {
-    if (ru.y0 == ru.y1) return 0;
-    if (ru.x0 == ru.x1) return 1;
-    return (ru.y1 > ru.y0) ? 2 : 3;
-}
-__device__ __forceinline__ void dir_step(int dir, int& dx, int& dy) {
-    dx = (dir == 1) ? 0 : 1;
-    dy = (dir == 0) ? 0 : ((dir == 3) ? -1 : 1);
-}
+// cell_weight, run_dir, dir_step and sym_run_scatter: common.hpp (makeGraph publishes the same scatter)
 
 // lines along direction `dir`: start cell of line `line`
 __device__ __forceinline__ bool line_start(int dir, int line, int cols, int rows, int& x, int& y) {
@@ -518,19 +502,7 @@ __global__ void sym_scatter_kernel(int cols, int rows, const int32_t* node_cell,
         const int64_t rs = node_run_start[k];
         const int nr = node_nruns[k];
         unsigned long long acc = 0;
-        for (int r = threadIdx.x; r < nr; r += blockDim.x) {
-            const Run ru = pool[rs + r];
-            const int dir = run_dir(ru);
-            int dx, dy;
-            dir_step(dir, dx, dy);
-            const int px = ru.x0 - dx, py = ru.y0 - dy, ex = ru.x1 + dx, ey = ru.y1 + dy;
-            const unsigned long long* P = prefix + (int64_t)dir * C;
-            acc += P[(int64_t)ru.x1 * rows + ru.y1];
-            if (px >= 0 && px < cols && py >= 0 && py < rows) acc -= P[(int64_t)px * rows + py];
-            unsigned long long* D = diff + (int64_t)dir * C;
-            atomicAdd(&D[(int64_t)ru.x0 * rows + ru.y0], su);
-            if (ex >= 0 && ex < cols && ey >= 0 && ey < rows) atomicAdd(&D[(int64_t)ex * rows + ey], (unsigned long long)(0ull - su));
-        }
+        for (int r = threadIdx.x; r < nr; r += blockDim.x) acc += sym_run_scatter(pool[rs + r], su, cols, rows, prefix, diff);
         for (int off = 32; off >= 1; off >>= 1) acc += __shfl_xor(acc, off);
         __shared__ unsigned long long red[16];
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;

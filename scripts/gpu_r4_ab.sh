@@ -17,8 +17,17 @@ run() {
   [ -n "${MK_VARIANTS}" ] && for v in default ${MK_VARIANTS}; do
     lib $v
     timeout -k 10 200 python -u scripts/probe_mk_time.py --config 2 --reps 2 >> $OUT/mk.jsonl 2>> $OUT/mk.err || { tail -5 $OUT/mk.err; return 1; }
+    if [ -n "${MK5}" ]; then
+      timeout -k 10 200 python -u scripts/probe_mk_time.py --config 5 --reps 1 >> $OUT/mk.jsonl 2>> $OUT/mk.err || { tail -5 $OUT/mk.err; return 1; }
+    fi
   done
   [ -n "${MK_VARIANTS}" ] && cut -c1-200 $OUT/mk.jsonl
+  [ -n "${BENCH_VARIANTS}" ] && for v in default ${BENCH_VARIANTS}; do
+    lib $v
+    timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline 2>> $OUT/bench.err | grep '^{' | \
+      python -c "import sys, json; d = json.loads(sys.stdin.read()); print(json.dumps({'lib': '$v', 'ms_per_step': d['ms_per_step'], 'value': d['value'], 'parts': {k: v for k, v in d.get('kernels', {}).items() if k.endswith('_s')}}))" >> $OUT/bench_ab.jsonl || { tail -5 $OUT/bench.err; return 1; }
+  done
+  [ -n "${BENCH_VARIANTS}" ] && cat $OUT/bench_ab.jsonl | cut -c1-400
   [ -n "${NO_TESTS}" ] && return 0
   lib ${TEST_VARIANT:-default}
   timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py \

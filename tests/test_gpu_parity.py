@@ -274,6 +274,28 @@ def test_vga_asymmetric_graph_corrections(ctx, monkeypatch):
         np.testing.assert_array_equal(o[b:e].view(np.uint32), o2[b:e].view(np.uint32))
 
 
+def test_symmetry_scatter_in_makegraph_equals_separate_pass(ctx, monkeypatch):
+    """A whole-graph makeGraph does the symmetry certificate's scatter (per-node out-hash, range adds of the
+    in-hash) as each source publishes its runs; DMX_MK_NOSYM leaves it to the VGA preparation's pass over the
+    pool, as a shard or an assembled graph does.  Same special nodes (syn256: the 4 of its 2 asymmetric
+    pairs) and bit-identical VGA on sources around them."""
+    lines = np.loadtxt(__import__("os").path.join(__import__("golden_io").GOLDEN, "inputs", "syn256.csv"),
+                       delimiter=",", skiprows=1)
+    pm = dmx.PointMap([0.0, 0.0, 256.0, 256.0], lines, 1.0)
+    assert pm.make_points(0.5, 0.5)
+    res = []
+    for nosym in (False, True):
+        if nosym:
+            monkeypatch.setenv("DMX_MK_NOSYM", "1")
+        g = pm.make_graph(ctx)
+        o, lv = g.vga_visual_global(src_begin=21900, src_end=22100, levels=True)
+        res.append((g.special_nodes(), o[21900:22100].copy(), lv[21900:22100].copy()))
+        g.close()
+    assert len(res[0][0]) == 4 and list(res[0][0]) == list(res[1][0])
+    np.testing.assert_array_equal(res[0][1].view(np.uint32), res[1][1].view(np.uint32))
+    np.testing.assert_array_equal(res[0][2], res[1][2])
+
+
 SD_CASES = ["kat", "syn16", "syn32", "syn64", "gallery"]
 
 
@@ -495,26 +517,37 @@ def test_vga_source_list_matches_full_run(ctx):
     assert (got[rest] == -7.0).all()
 
 
-def test_vga_prep_shard_single_rank_identity(ctx):
+def test_vga_prep_shard_single_rank_identity(ctx, monkeypatch):
     """dmx_graph_set_prep_shard with a world of one (the all-reduce is the identity): same columns
     as the unsharded run, and the callback sees the partial buffers in order: the in-set hash
     difference arrays, the out-set hashes, the special-node veto, then the tvis / ftvis rows (each rank
-    builds the partial-tile masks of every node itself: no collective)."""
+    builds the partial-tile masks of every node itself: no collective).  A graph whose makeGraph swept
+    every source did the hash scatter as it published the runs: complete on every rank, so the hashes
+    are not all-reduced (the veto and the rows still are)."""
     import torch
     meta, A = load_case("gallery")
     pm = _map(meta)
     full = pm.make_graph(ctx).vga_visual_global()
-    g = pm.make_graph(ctx)
     n = full.shape[0]
-    calls = []
-    g.set_prep_shard(0, n, lambda ptr, count, dtype: calls.append((count, dtype)) or 0)
-    out = torch.full((n, 7), -1.0, dtype=torch.float32, device="cuda")
-    g.vga_visual_global_device_list(out.data_ptr(), np.arange(n))
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), full.view(np.uint32))
     C = meta["cols"] * meta["rows"]
-    assert calls[:3] == [(4 * C, 1), (n, 1), (1, 1)]
-    assert len(calls) == 5 and calls[3] == calls[4] and calls[3][1] == 1
+    for nosym in (True, False):
+        if nosym:
+            monkeypatch.setenv("DMX_MK_NOSYM", "1")
+        else:
+            monkeypatch.delenv("DMX_MK_NOSYM", raising=False)
+        g = pm.make_graph(ctx)
+        calls = []
+        g.set_prep_shard(0, n, lambda ptr, count, dtype: calls.append((count, dtype)) or 0)
+        out = torch.full((n, 7), -1.0, dtype=torch.float32, device="cuda")
+        g.vga_visual_global_device_list(out.data_ptr(), np.arange(n))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), full.view(np.uint32))
+        if nosym:
+            assert calls[:3] == [(4 * C, 1), (n, 1), (1, 1)]
+            assert len(calls) == 5 and calls[3] == calls[4] and calls[3][1] == 1
+        else:
+            assert calls[0] == (1, 1) and len(calls) == 3 and calls[1] == calls[2] and calls[1][1] == 1
+        g.close()
 
 
 @pytest.mark.parametrize("name", ["gallery", "syn64"])
