@@ -181,11 +181,8 @@ struct FView {
     const unsigned long long* CB;   // [tw*8][wc]: bit ty of column x: tile (x>>3, ty) has one in column x
     int tw, wr, wc;
 };
-// Tiles [t0, t1] of one summary line (bit per tile, <= 2 words: grids up to 1024 cells a side):
+// Tiles [t0, t1] of one summary line (bit per tile, one word per 64 tiles):
 // OR of F[base + tx * stride] & (cell mask of tile tx), 8 frontier tiles per round.
-#ifndef LH_COUNT
-#define LH_COUNT()
-#endif
 template <bool VERT>
 __device__ __forceinline__ bool line_hits(const unsigned long long* F, const unsigned long long* sum, int base, int stride,
                                           int t0, int t1, int a, int b, int sh) {
@@ -195,7 +192,6 @@ __device__ __forceinline__ bool line_hits(const unsigned long long* F, const uns
         if (w == w0) m &= ~0ull << (t0 & 63);
         if (w == w1) m &= ~0ull >> (63 - (t1 & 63));
         while (m) {
-            LH_COUNT();
             const int p = __ffsll((long long)m) - 1;
             unsigned long long acc = 0ull;
 #pragma unroll

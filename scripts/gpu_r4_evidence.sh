@@ -34,7 +34,12 @@ else
   DMX_TEST_WIDE=1 timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread -m gpu \
     tests/test_gpu_scale.py -k "2000_vga_sources" > $OUT/vga2000_wide_tests.log 2>&1
   rc=$?
+  # the 1000^2 step with the symmetry scatter left to the VGA preparation (the round-3 arrangement)
+  [ $rc = 0 ] && DMX_MK_NOSYM=1 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline \
+    > $OUT/bench_nosym.log 2> $OUT/bench_nosym_progress.txt
+  rc=$?
   tail -5 $OUT/pmc5.log; grep '^{' $OUT/bench5.log | cut -c1-300; tail -2 $OUT/vga2000_wide_tests.log
+  grep '^{' $OUT/bench_nosym.log | cut -c1-300
 fi
 kill $HB
 exit $rc
