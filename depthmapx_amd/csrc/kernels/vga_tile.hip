@@ -181,6 +181,9 @@ struct FView {
     const unsigned long long* CB;   // [tw*8][wc]: bit ty of column x: tile (x>>3, ty) has one in column x
     int tw, wr, wc;
 };
+#ifndef VGA_KH0
+#define VGA_KH0 2   // phase B: heads loaded with the cell's first loads (A/B builds: -DVGA_KH0=n)
+#endif
 // Tiles [t0, t1] of one summary line (bit per tile, one word per 64 tiles):
 // OR of F[base + tx * stride] & (cell mask of tile tx), 8 frontier tiles per round.
 template <bool VERT>
@@ -522,10 +525,11 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
         const unsigned long long p = pw[k];
         const int bk = base[k];
         while (__ballot(c != 0ull) != 0ull) {
-            unsigned long long mk[4];
-            int tl[4], sl[4];
+            constexpr int NM = 4;   // masks a lane keeps in flight (2: +1 %, 8: +34 %, round 4)
+            unsigned long long mk[NM];
+            int tl[NM], sl[NM];
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < NM; j++) {
                 tl[j] = -1;
                 if (c) {
                     const int b = __ffsll((long long)c) - 1;
@@ -536,19 +540,13 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
                     nload++;
                 }
             }
-            int hj = -1;
+            int hj = -1, ht = 0, hq = 0;
 #pragma unroll
-            for (int j = 3; j >= 0; j--)
-                if (tl[j] >= 0 && (F[tl[j]] & mk[j])) hj = j;
+            for (int j = NM - 1; j >= 0; j--)
+                if (tl[j] >= 0 && (F[tl[j]] & mk[j])) { hj = j; ht = tl[j]; hq = sl[j]; }
             const unsigned long long hb = __ballot(hj >= 0);
             if (hb != 0ull) {
-                if (lane == __ffsll((long long)hb) - 1) {
-                    int t = tl[0], q = sl[0];
-                    if (hj == 1) { t = tl[1]; q = sl[1]; }
-                    if (hj == 2) { t = tl[2]; q = sl[2]; }
-                    if (hj == 3) { t = tl[3]; q = sl[3]; }
-                    Hn[id] = 0x80000000u | ((uint32_t)t << 16) | (uint32_t)q;
-                }
+                if (lane == __ffsll((long long)hb) - 1) Hn[id] = 0x80000000u | ((uint32_t)ht << 16) | (uint32_t)hq;
                 return true;
             }
         }
@@ -774,7 +772,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     int nr = 0;
                     uint32_t hp = 0xFFFFFFFFu;
                     int64_t pof = 0;
-                    constexpr int KH0 = 4;
+                    // heads loaded with the cell's first loads, the rest of the KH heads in the extension loop
+                    // (round 4 at 1000^2: 4 -> 2 heads 4.67 -> 4.60 s, fewer live registers at the head tests)
+                    constexpr int KH0 = VGA_KH0;
                     Run hd[KH0];
                     if (cand) {
                         ss = P.tscan_start[id];

@@ -31,8 +31,8 @@ run() {
   [ -n "${NO_TESTS}" ] && return 0
   lib ${TEST_VARIANT:-default}
   timeout -k 10 700 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu tests/test_gpu_parity.py \
-    tests/test_gpu_scale.py tests/test_merge_links.py tests/test_semifill.py \
-    -k "${K:-(vga or merge or contextfilled or special or asym or makegraph or random_occluders) and not 2000}" \
+    tests/test_gpu_scale.py tests/test_merge_links.py tests/test_semifill.py tests/test_graphfile.py tests/test_gpu_nocaps.py \
+    -k "${K:-(vga or merge or contextfilled or special or asym or makegraph or random_occluders or graph_regression or topdown or symmetry) and not 2000}" \
     > $OUT/pytest.log 2>&1
   rc=$?
   grep -E "FAILED|ERROR" $OUT/pytest.log | head; tail -3 $OUT/pytest.log
