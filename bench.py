@@ -453,15 +453,29 @@ def main():
                 "algorithmic_bytes": dom_bytes, "work_model_rate": work_rate,
                 "launches_per_step": dpm.get("calls"), "kernel_s_live": dom_s,
                 "kernel_s_rocprof": dps.get("duration_ns", dpm.get("duration_ns", 0)) * 1e-9 if dpm else None}
+        vga_model = ("8 B x run records tested + 16 B x tiles x sources (V/X reset) + 32 B x tiles x levels + "
+                     "tile-visibility rows read + 8 B x partial-tile masks read (DESIGN.md section 3)")
+        mk_model = "B_mk = 8 B x runs written + 4 B x sieve cells examined (DESIGN.md section 2)"
+        roof["work_model"] = mk_model if dominant == "makegraph_kernel" else (vga_model if not stepdepth else
+                                                                              "8 B x expander runs + 8 B x relaxations")
+        # the other hot kernel of the step, the same figures (the two are within a few % of each other at 1000^2)
+        okern, obytes, osecs = ((second, vga_bytes, vga_s) if dominant == "makegraph_kernel" else
+                                ("makegraph_kernel", mk_bytes, mk_s))
+        opm = pmc.get(okern, {})
+        otraffic = opm.get("per_step", {}).get("hbm_bytes_raw", opm.get("hbm_bytes_raw"))
+        if osecs:
+            roof["other_kernel"] = {"kernel": okern, "kernel_s_live": osecs,
+                                    "achieved": otraffic / osecs / 1e9 if otraffic else None,
+                                    "frac": otraffic / osecs / 1e9 / HBM_PEAK_GBS if otraffic else None,
+                                    "traffic": otraffic, "l2_hit_rate": opm.get("l2_hit_rate"),
+                                    "algorithmic_bytes": obytes, "work_model_rate": obytes / osecs / 1e9,
+                                    "work_model": mk_model if okern == "makegraph_kernel" else vga_model}
         if not stepdepth:
             # SURVEY.md section 8(d) B_vga at batch size 1 = the reference's BFS work (every source reads every
             # reached node's run records and touches N cells): the bytes a run-by-run BFS would move
             b_vga = nsrc * (8 * int(g.info()["nruns"]) + 4 * N)
             roof["b_vga_reference_work"] = b_vga
             roof["b_vga_rate_GBs"] = b_vga / vga_s / 1e9 if vga_s else None
-            roof["work_model"] = ("8 B x run records tested + 16 B x tiles x sources (V/X reset) + 32 B x tiles x "
-                                  "levels + tile-visibility rows read + 8 B x partial-tile masks read (DESIGN.md "
-                                  "section 3)")
         # issue-rate roofline (VALU) for the two hot kernels, and makeGraph's FP64 rate
         issue = {}
         for kname in ("makegraph_kernel", "vga_tile_kernel", "stepdepth_kernel"):
