@@ -469,7 +469,8 @@ def main():
                                     "frac": otraffic / osecs / 1e9 / HBM_PEAK_GBS if otraffic else None,
                                     "traffic": otraffic, "l2_hit_rate": opm.get("l2_hit_rate"),
                                     "algorithmic_bytes": obytes, "work_model_rate": obytes / osecs / 1e9,
-                                    "work_model": mk_model if okern == "makegraph_kernel" else vga_model}
+                                    "work_model": mk_model if okern == "makegraph_kernel" else (
+                                        vga_model if not stepdepth else "8 B x expander runs + 8 B x relaxations")}
         if not stepdepth:
             # SURVEY.md section 8(d) B_vga at batch size 1 = the reference's BFS work (every source reads every
             # reached node's run records and touches N cells): the bytes a run-by-run BFS would move
