@@ -1,33 +1,34 @@
-// vga_tile.hip -- K3 v3: tile-resolved, direction-optimising VGA global BFS (+ K4 measures).
+// vga_tile.hip -- tile-resolved, direction-optimising VGA global BFS (+ the measures kernel and the
+// preparation kernels it reads).
 //
-// Same result as VGAVisualGlobal::run (salalib/vgamodules/vgavisualglobal.cpp:23-216; set
-// semantics as in vga.hip / vga_do.hip), organised so that one source costs O(tiles) rather than
-// O(cells) of memory traffic on open plans:
-//   * one workgroup per source (persistent grid); the frontier F is an LDS bitmap in 8x8-cell
-//     tiles (fits 1024x1024-cell grids), while the visited set V and the next level X live in
-//     per-workgroup HBM scratch (xg), touched only for the tiles that still hold an unvisited cell;
-//   * level 1 is top-down: the source's runs are rasterised into F with LDS atomic ORs;
-//   * later levels are bottom-up (valid because visibility is symmetric; the few asymmetric nodes
-//     are routed through exact in-set corrections, see vga_do.hip):
-//       A. tile level: the owner tests the tile's precomputed common runs CR(t) -- runs whose cells
-//          are visible from EVERY regular cell of the tile -- against F; one hit discovers all of
-//          the tile's unvisited regular cells at once (64 cells per test);
-//       B. cell level: the remaining cells test their KH "head" runs (the longest run of each of
-//          8 angular groups, longest first), a wave per tile, lane = cell, coalesced loads;
-//       C. hard cells scan their whole run list longest-first, 64 runs per wave step (coalesced),
-//          stopping at the first hit.
-//   * top-down is used again only when Beamer's test on cell counts prefers it (small frontier).
-// Prep kernels below build the tile-ordered per-cell arrays, the head runs and CR(t) from the
-// run-length graph in O(runs).
+// Same result as VGAVisualGlobal::run (salalib/vgamodules/vgavisualglobal.cpp:23-216; set semantics as in
+// vga_do.hip), organised so that one source costs O(tiles) rather than O(cells) of memory traffic:
+//   * one 1024-thread workgroup per source (persistent grid); the frontier F is a bitmap of 8x8-cell tiles,
+//     in LDS up to 1024 cells a side and in per-workgroup HBM above (FG, its line summaries stay in LDS);
+//     the visited set V and the next level X live in per-workgroup HBM scratch, touched only for the tiles
+//     the previous level listed as still holding an unvisited cell;
+//   * level 1 is top-down: the source's runs are rasterised into F;
+//   * later levels are bottom-up while Beamer's test on cell counts allows (valid because visibility is
+//     symmetric; the few asymmetric nodes take exact in-set corrections, vga_do.hip prepare_symmetry):
+//       A. tile level: the tile's common runs CR(t) (visible from every regular cell of the tile) against F;
+//          one hit discovers all of the tile's unvisited regular cells;
+//       B. a wave per remaining tile, lane = cell: the tile-to-tile rows (ttvis / ttany), then each cell's
+//          first head runs and its hint (the run or partial-tile mask that last hit), then the other heads;
+//       C. hard cells, a wave per cell: the tile-visibility rows (tvis / ftvis) give a certain hit or miss,
+//          the partial-tile masks decide the rest exactly; without the masks (memory, grids above 1024 a
+//          side) the cell's runs are scanned, with the tvis rows (and their summaries) as a miss certificate;
+//   * top-down again when Beamer's test prefers it (small frontier); the bookkeeping publishes the
+//     expandable part of X as the next F and rebuilds F's summaries.
+// DESIGN.md section 2 has the measurements behind each choice, including the variants measured and dropped
+// (phase-C prefix loaded with the row word, heads 4..7 loaded with the hint's operand, prefetching the next
+// queue entry or hard-cell chunk, more masks in flight).
 #include "common.hpp"
 
 namespace dmx {
 
 constexpr int KH = 8;        // head runs per cell (first KH entries of its scan order)
-// HV_FIRST: heads and tile-common runs ordered row / column runs first (1000^2: VGA 7.50 -> 6.11 s, phase A's
+// heads and tile-common runs are ordered row / column runs first (1000^2: VGA 7.50 -> 6.11 s, phase A's
 // clocks / 5.7: a diagonal run's test walks its tiles, 8 LDS reads a round trip)
-// PPRE_EARLY: phase C loads a row word's partial-tile prefix with the word itself
-// HEADS8_EARLY: phase B loads heads 4..7 with the hint's operand instead of after the first 4 head tests
 constexpr int CRK = 4;       // tile-common runs per tile
 constexpr int BEXT_DEFAULT = 0;   // scan-order runs past the KH heads phase B tests (final build: 0 -1.4 % vs 4, profiles/r3b_vga_env)
 constexpr int VGA_HMAX = 64;  // levels kept per source by the tile kernel (deeper: vga_do)
