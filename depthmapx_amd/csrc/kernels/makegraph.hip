@@ -15,7 +15,8 @@
 //     order, so runs are closed incrementally per row; a per-(bin,row) count array gives every run
 //     its final slot in reference (PixelRefH/V) order without sorting (counting placement);
 //   * runs are staged per wave in scratch, then copied once into a global pool reserved with one
-//     atomic per source, bins in reference order 0..31.
+//     atomic per source, bins in reference order 0..31; a whole-graph build also does the VGA
+//     symmetry certificate's scatter there (sym_run_scatter, common.hpp), run by run.
 //   All geometry is IEEE double in the reference's operation order (-ffp-contract=off).
 #include "common.hpp"
 
@@ -27,7 +28,6 @@ constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capa
 // side) in per-wave scratch memory: rows past 1024 are reached only by sight lines longer than 1024
 // cells, and a full-length LDS array would cost a 2000^2 grid a quarter of its waves
 constexpr int MK_OPEN_LDS = 1024;
-// BIN_BALLOT: the per-bin count and far distance updated once per ratio class of a candidate chunk
 
 struct MakeGraphParams {
     int cols, rows;
