@@ -61,6 +61,7 @@ SIGNATURES = {
     "dmx_ctx_last_stepdepth": (_i32, [_vp, _vp, _vp, _vp]),
     "dmx_ctx_last_stepdepth_detail": (_i32, [_vp, _vp]),
     "dmx_ctx_last_phase_cycles": (_i32, [_vp, _vp]),
+    "dmx_ctx_last_mk_reruns": (_i32, [_vp, _vp, ctypes.c_int64, _vp]),
     "dmx_chunk_write": (_i32, [_vp, _i64, _vp, _vp, _i64, _vp, _i32, _vp, _vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "dmx_pointmap_set_state": (_i32, [_vp, _vp]),
     "dmx_chunk_parse": (_i32, [_vp, _i64, _vp]),
@@ -124,6 +125,8 @@ def lib():
             raise DmxError(-2, "native library %s is missing: run depthmapx_amd.build.build()" % LIB_PATH)
         L = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("DMX_LIB") and not hasattr(L, name):
+                continue   # an older A/B build (timing probes) may lack entry points added since
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -12,7 +12,8 @@ ARCH = os.environ.get("DMX_OFFLOAD_ARCH", "gfx950")
 
 SOURCES = ["dmx_api.hip", "host/pointmap.cpp", "host/graphio.cpp", "host/graphfile.cpp"]
 FLAGS = ["--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
-         "-fno-fast-math", "-Wall", "-Wno-unused-variable", "-Wno-unused-function"]
+         "-fno-fast-math", "-Wall", "-Wno-unused-variable", "-Wno-unused-function",
+         "-Wno-bitwise-instead-of-logical"]
 
 
 def _deps():

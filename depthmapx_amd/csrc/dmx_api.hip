@@ -34,6 +34,7 @@
 #include "kernels/vga_local.hip"
 #include "kernels/fill.hip"
 #include "kernels/vstep.hip"
+#include "kernels/vga_ordered.hip"
 
 using namespace dmx;
 
@@ -193,6 +194,7 @@ struct dmx_ctx {
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
     long long last_stats[40] = {};
+    std::vector<int64_t> last_mk_reruns;   // sources the last makeGraph re-ran (MK_CAPACITY_TAG: capacity)
     // progress / cancel (dmx_ctx_set_progress, dmx_ctx_cancel): host-mapped block polled by the kernels
     DmxCtl* h_ctl = nullptr;
     DmxCtl* d_ctl = nullptr;
@@ -201,6 +203,8 @@ struct dmx_ctx {
     double progress_interval = 0.5;
     hipEvent_t ev_poll = nullptr;
     double last_fill_s[2] = {0, 0};   // GPU fill: blockLines, flood fill
+    double sqrt_err = 0.0;            // makeGraph moment square root: measured error bound (mk_sqrt_err)
+    long long sqrt_err_nmax = 0;      // ... over 1..sqrt_err_nmax
     long long last_fill_levels = 0;
 };
 
@@ -212,6 +216,7 @@ struct dmx_pointmap {
     int64_t nnodes = 0;
     std::vector<int32_t> node_cell;
     DevBuf<uint32_t> d_cellw;
+    DevBuf<uint32_t> d_cellw_t;   // the same words y-major (makeGraph's V octants)
     DevBuf<double> d_segs;
     DevBuf<int32_t> d_node_cell;
     DevBuf<int32_t> d_cell_node;
@@ -331,16 +336,13 @@ int prepare_merges(dmx_graph* g) {
     return DMX_OK;
 }
 
-const char* const k_order_msg = "merge links on context-filled cells: a search found both ends of such a link at one "
-                                "level, where the reference's result depends on which it pops first";
-
 int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     PointMapHost& h = *pm->host;
     if (!h.lines_blocked()) h.block_lines();
     if (pm->uploaded_version == pm->version && pm->uploaded_for == ctx->device) return DMX_OK;
     if (pm->uploaded_for >= 0 && pm->uploaded_for != ctx->device) {
         // another device's copies: release them (DevBuf::alloc would otherwise reuse the pointers)
-        pm->d_cellw.reset(); pm->d_segs.reset(); pm->d_node_cell.reset(); pm->d_cell_node.reset();
+        pm->d_cellw.reset(); pm->d_cellw_t.reset(); pm->d_segs.reset(); pm->d_node_cell.reset(); pm->d_cell_node.reset();
         pm->d_node_flags.reset(); pm->d_seed_tiles.reset(); pm->d_nonexp_tiles.reset();
         pm->uploaded_for = -1;
     }
@@ -376,6 +378,7 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
         }
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(pm->d_cellw.alloc(C));
+    HIPCHK(pm->d_cellw_t.alloc(C));
     HIPCHK(pm->d_segs.alloc(std::max<size_t>(h.segs().size(), 4)));
     HIPCHK(pm->d_node_cell.alloc(std::max<int64_t>(pm->nnodes, 1)));
     HIPCHK(pm->d_cell_node.alloc(C));
@@ -384,6 +387,14 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     HIPCHK(pm->d_nonexp_tiles.alloc(nonexp.size()));
     HIPCHK(hipMemcpyAsync(pm->d_nonexp_tiles.p, nonexp.data(), nonexp.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(pm->d_cellw.p, cellw.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
+    {
+        std::vector<uint32_t> cellw_t((size_t)C);
+        const int cols = h.cols(), rows = h.rows();
+        for (int x = 0; x < cols; x++)
+            for (int y = 0; y < rows; y++) cellw_t[(size_t)y * cols + x] = cellw[(size_t)x * rows + y];
+        HIPCHK(hipMemcpyAsync(pm->d_cellw_t.p, cellw_t.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));   // (cellw_t is freed on return)
+    }
     if (!h.segs().empty())
         HIPCHK(hipMemcpyAsync(pm->d_segs.p, h.segs().data(), h.segs().size() * 8, hipMemcpyHostToDevice, ctx->stream));
     if (pm->nnodes) {
@@ -449,6 +460,7 @@ size_t makegraph_lds(int gcap, int bcap, int D) {
     b += 16 * (size_t)gcap * 2 + 16 * (size_t)bcap; // gaps, gaps2, blocks
     b += 4 * 32 * 3 + 4 * 32;                        // binc, bfar, bnr, misc
     b += 16 * (size_t)bcap;                          // bsorted
+    b += 8 * (size_t)MK_EB;                          // staged emission records
     b += 4 * (size_t)gcap + 8 * (size_t)gcap + 4 * (size_t)bcap + 4 * ((size_t)gcap + 4);
     b += 4 * (size_t)std::min(D + 4, MK_OPEN_LDS);   // open-run state of the near rows (makegraph.hip)
     return (b + 15) & ~(size_t)15;
@@ -904,6 +916,29 @@ static mk_kernel_t mk_kernel(bool fixed, bool count, bool maxd, bool far) {
 }
 #undef MKK
 
+// The largest relative error of makeGraph's moment square root (MK_SQRT) over the integers 1..nmax, measured
+// exhaustively on the device (once per context and range): the certificate of the moment sums rests on it.
+static int mk_sqrt_err(dmx_ctx* ctx, long long nmax, double* err) {
+    if (ctx->sqrt_err_nmax < nmax) {
+        DevBuf<unsigned long long> e;
+        HIPCHK(e.alloc(1));
+        HIPCHK(hipMemsetAsync(e.p, 0, 8, ctx->stream));
+        hipLaunchKernelGGL(sqrt_err_kernel, dim3((unsigned)std::min<long long>((nmax + 255) / 256, 4096)), dim3(256), 0,
+                           ctx->stream, nmax, e.p);
+        HIPCHK(hipGetLastError());
+        unsigned long long bits = 0;
+        HIPCHK(copy_sync(ctx->stream, &bits, e.p, 8, hipMemcpyDeviceToHost));
+        double v;
+        std::memcpy(&v, &bits, 8);
+        if (!(v >= 0.0 && v < 0x1p-30)) return fail(DMX_ERR_STATE, "internal: the device square root is not accurate enough");
+        ctx->sqrt_err = v;
+        ctx->sqrt_err_nmax = nmax;
+        VLOG("makegraph: square-root error bound %.3g over 1..%lld\n", v, nmax);
+    }
+    *err = ctx->sqrt_err;
+    return DMX_OK;
+}
+
 // makeGraph over [node_begin, node_end), or only over the listed nodes of that range (`only`: the cost
 // sample of dmx_makegraph_balance; the graph's other nodes stay unset).  d_work (optional, [n][2]) receives
 // each published source's sieve depth steps and candidate chunks.
@@ -971,6 +1006,8 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         HIPCHK(hipGetLastError());
     }
     ctx->last_mk_s = 0;
+    double sqrt_err = 0.0;
+    if (int rc2 = mk_sqrt_err(ctx, 2ll * D * D, &sqrt_err)) return rc2;
     DevBuf<int64_t> fail_list, node_list;
     DevBuf<MakeGraphParams> dP;   // kernel parameters in device memory (see makegraph_kernel)
     HIPCHK(fail_list.alloc(std::max<int64_t>(n, 1)));
@@ -987,6 +1024,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
                     ((n >= 16 * kSample && big_pool) || (n >= kSample && getenv("DMX_MK_SAMPLE")));   // test hook
     double mk_total_s = 0.0;
     int64_t reruns = 0;   // sources re-run after a first-pass capacity or certification failure
+    std::vector<int64_t> mk_reruns;
     for (int restart = 0; restart < 4; restart++) {
         // one full pass, then re-runs of only the sources that overflowed an LDS / staging capacity
         double kernel_s = 0.0;
@@ -1062,7 +1100,8 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
             P.cols = h.cols(); P.rows = h.rows();
             P.spacing = h.spacing(); P.blx = h.bottom_left().x; P.bly = h.bottom_left().y;
             P.maxdist = maxdist;
-            P.cellw = pm->d_cellw.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
+            P.cellw = pm->d_cellw.p; P.cellw_t = pm->d_cellw_t.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
+            P.sqrt_err = sqrt_err;
             P.node_begin = node_begin; P.node_end = node_end;
             P.work_counter = ctx->counters.p + 0;
             P.ctl = ctx->d_ctl;
@@ -1117,7 +1156,12 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
                 break;
             }
             if (nfail == 0) break;
-            if (!sampling) reruns += nfail;
+            if (!sampling) {
+                reruns += nfail;
+                std::vector<int64_t> fl((size_t)nfail);
+                HIPCHK(copy_sync(ctx->stream, fl.data(), fail_list.p, (size_t)nfail * 8, hipMemcpyDeviceToHost));
+                mk_reruns.insert(mk_reruns.end(), fl.begin(), fl.end());
+            }
             if (err & KERR_GAP_CAPACITY) gcap *= 2;
             if (err & KERR_BLOCK_CAPACITY) spill_cap *= 4;
             if (err & KERR_STAGE_CAPACITY) capB *= 2;
@@ -1137,7 +1181,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
                  pool_cap * 8.0 / 1e9);
             continue;
         }
-        if (pool_over) { mk_total_s += kernel_s; continue; }
+        if (pool_over) { mk_total_s += kernel_s; mk_reruns.clear(); reruns = 0; continue; }
         HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
         if (n > 0 && !only) {   // (a sample leaves the other nodes' run starts unset)
             hipLaunchKernelGGL(gridconn_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, h.rows(),
@@ -1173,6 +1217,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         ctx->last_stats[32] = (long long)st[2];   // sieve depth steps
         ctx->last_stats[33] = (long long)st[3];   // 64-candidate chunks
         ctx->last_stats[34] = (long long)reruns;
+        ctx->last_mk_reruns = std::move(mk_reruns);
         ctx->last_mk_s = mk_total_s + kernel_s;   // every pass counted (sample, overflow re-runs)
         g->nruns = (int64_t)used;
         if (fuse_sym) { g->sym_fused = true; g->sym_prefix.reset(); }   // the prefix sums are no longer needed
@@ -1846,6 +1891,91 @@ static int prepare_tiles(dmx_graph* g) {
     return DMX_OK;
 }
 
+// threads of the tile BFS workgroup on grids above 4096 tiles (one workgroup per CU either way: F takes the
+// LDS); A/B builds: -DVGA_NT_BIG=512
+#ifndef VGA_NT_BIG
+#define VGA_NT_BIG 1024
+#endif
+// The reference's own level order (vga_ordered.hip) for the searches the level-synchronous kernels cannot
+// answer (merge links with a context-filled odd end found together with the other end at one level).
+// VGA global: one search per listed source node, its level histogram into the measures kernel (rows of `outp`,
+// levels into d_levels).  Visual step depth (seed_cells non-empty, PixelRef order): one search, the level of
+// every cell it reaches into d_cell_level [C].
+static int ordered_search(dmx_ctx* ctx, dmx_graph* g, double radius, const std::vector<int32_t>& src,
+                          const std::vector<int32_t>& seed_cells, float* outp, int64_t* d_levels, int32_t* d_cell_level) {
+    const PointMapHost& h = *g->pm->host;
+    const int64_t C = h.cells(), N = g->nnodes;
+    const bool vsd = !seed_cells.empty();
+    const int64_t nsearch = vsd ? 1 : (int64_t)src.size();
+    if (nsearch == 0) return DMX_OK;
+    size_t free_b = 0, total_b = 0;
+    HIPCHK(hipMemGetInfo(&free_b, &total_b));
+    const size_t per = (size_t)C * 5 + (size_t)N * 8;   // misc, extents, two level vectors
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>({nsearch, (int64_t)ctx->num_cu,
+                                                                    (int64_t)((free_b + cached_bytes()) / 4 / per)}));
+    DevBuf<uint8_t> misc;
+    DevBuf<int16_t> ext;
+    DevBuf<int32_t> vec, d_src, d_seeds, hist, nlev;
+    DevBuf<unsigned long long> junk;
+    HIPCHK(misc.alloc((size_t)blocks * C));
+    HIPCHK(ext.alloc((size_t)blocks * 2 * C));
+    HIPCHK(vec.alloc((size_t)blocks * 2 * std::max<int64_t>(N, 1)));
+    OrderedParams P;
+    P.rows = h.rows(); P.C = C; P.N = N;
+    P.node_run_start = g->node_run_start.p; P.node_nruns = g->node_nruns.p; P.pool = g->pool.p;
+    P.cell_node = g->pm->d_cell_node.p; P.node_cell = g->pm->d_node_cell.p; P.node_flags = g->pm->d_node_flags.p;
+    P.merge_cell = g->merges.empty() ? nullptr : g->d_merge_cell.p;
+    P.src = nullptr; P.nsrc = 0; P.radius = (int)radius; P.hist_all = nullptr; P.nlev_all = nullptr;
+    P.seeds = nullptr; P.nseeds = 0; P.cell_level = d_cell_level;
+    P.misc = misc.p; P.ext = ext.p; P.vec = vec.p;
+    P.error = ctx->counters.p + 1;
+    HIPCHK(hipMemsetAsync(ctx->counters.p + 1, 0, sizeof(int), ctx->stream));
+    if (vsd) {
+        HIPCHK(d_seeds.alloc(seed_cells.size()));
+        HIPCHK(hipMemcpyAsync(d_seeds.p, seed_cells.data(), seed_cells.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        P.seeds = d_seeds.p; P.nseeds = (int)seed_cells.size();
+    } else {
+        HIPCHK(d_src.alloc(src.size()));
+        HIPCHK(hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));
+        HIPCHK(nlev.alloc(std::max<int64_t>(N, 1)));
+        HIPCHK(hipMemcpyAsync(d_src.p, src.data(), src.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+        P.src = d_src.p; P.nsrc = (int)src.size(); P.hist_all = hist.p; P.nlev_all = nlev.p;
+    }
+    DevBuf<OrderedParams> dP;
+    HIPCHK(dP.alloc(1));
+    HIPCHK(hipMemcpyAsync(dP.p, &P, sizeof(P), hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(vga_ordered_kernel, dim3((unsigned)blocks), dim3(ORD_NT), 0, ctx->stream, (const OrderedParams*)dP.p);
+    HIPCHK(hipGetLastError());
+    int err = 0;
+    HIPCHK(copy_sync(ctx->stream, &err, ctx->counters.p + 1, sizeof(int), hipMemcpyDeviceToHost));
+    if (err) return fail(DMX_ERR_CAPACITY, "VGA BFS (reference order) exceeded its level capacity");
+    if (!vsd) {
+        HIPCHK(junk.alloc(32));
+        hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsearch + 255) / 256)), dim3(256), 0, ctx->stream,
+                           (int64_t)0, nsearch, hist.p, nlev.p, outp, d_levels, junk.p, (const int32_t*)d_src.p);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    VLOG("reference-order searches: %lld on %lld workgroups\n", (long long)nsearch, (long long)blocks);
+    return DMX_OK;
+}
+
+// The sources a level-synchronous kernel marked in d_oflag, run again in the reference's order.
+static int vga_order_rerun(dmx_ctx* ctx, dmx_graph* g, double radius, const uint8_t* d_oflag, float* outp,
+                           int64_t* d_levels) {
+    const int64_t N = g->nnodes;
+    std::vector<uint8_t> fl((size_t)N);
+    HIPCHK(copy_sync(ctx->stream, fl.data(), d_oflag, (size_t)N, hipMemcpyDeviceToHost));
+    std::vector<int32_t> src;
+    for (int64_t k = 0; k < N; k++)
+        if (fl[k]) src.push_back((int32_t)k);
+    const double t0 = now_s();
+    int rc = ordered_search(ctx, g, radius, src, {}, outp, d_levels, nullptr);
+    ctx->last_vga_s += now_s() - t0;
+    ctx->last_stats[38] = (int64_t)src.size();
+    return rc;
+}
+
 extern "C++" template <int NT, bool SPECIAL, bool RBM, bool FG>
 static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_t lds, int64_t* blocks_out,
                        DevBuf<unsigned long long>& xg, DevBuf<int4>& queue, DevBuf<int32_t>& list) {
@@ -1942,6 +2072,13 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.nmamb = Q.nmp && radius != -1.0 ? g->nmamb : 0;
     Q.mamb = Q.nmamb ? g->d_mamb.p : nullptr;
     Q.mseen = nullptr;
+    DevBuf<uint8_t> oflag;   // sources whose result depends on the reference's pop order (merge_order_check)
+    Q.oflag = nullptr;
+    if (Q.nmamb) {
+        HIPCHK(oflag.alloc(std::max<int64_t>(N, 1)));
+        HIPCHK(hipMemsetAsync(oflag.p, 0, (size_t)std::max<int64_t>(N, 1), ctx->stream));
+        Q.oflag = oflag.p;
+    }
     Q.src_list = d_src_list;   // [sb, se) index this list of source nodes (out must be on the device)
     // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
     Q.alpha = 60;   // top-down costs a frontier cell its whole run list (~R/N runs): keep it rare
@@ -1991,11 +2128,11 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
                            : launch_tile<256, false, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
             ntpb = 256;
         } else {
-            rc = sp ? (rbm ? launch_tile<1024, true, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
-                           : launch_tile<1024, true, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
-                    : (rbm ? launch_tile<1024, false, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
-                           : launch_tile<1024, false, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
-            ntpb = 1024;
+            rc = sp ? (rbm ? launch_tile<VGA_NT_BIG, true, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<VGA_NT_BIG, true, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list))
+                    : (rbm ? launch_tile<VGA_NT_BIG, false, true, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list)
+                           : launch_tile<VGA_NT_BIG, false, false, false>(ctx, Q, nsrc, L, &blocks, xg, queue, list));
+            ntpb = VGA_NT_BIG;
         }
         if (rc) return rc;
         CANCEL_POINT(ctx);
@@ -2015,8 +2152,10 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_vga_s = ms * 1e-3;
     int hc[2];
     HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
-    if (hc[1] & KERR_ORDER) return fail(DMX_ERR_UNSUPPORTED, k_order_msg);
-    if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level capacity");
+    if (hc[1] & ~KERR_ORDER) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level capacity");
+    ctx->last_stats[38] = 0;
+    if ((hc[1] & KERR_ORDER) && nseeds == 0)
+        if (int rc2 = vga_order_rerun(ctx, g, radius, oflag.p, outp, levels ? d_lv.p : nullptr)) return rc2;
     unsigned long long st[32];
     HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
     for (int i = 0; i < 5; i++) ctx->phase_cycles[i] = (long long)st[8 + i];
@@ -2149,10 +2288,14 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     Q.nmamb = Q.nmp && radius != -1.0 ? g->nmamb : 0;
     Q.mamb = Q.nmamb ? g->d_mamb.p : nullptr;
     DevBuf<int32_t> mseen;
+    DevBuf<uint8_t> oflag;
     if (Q.nmamb) {
         HIPCHK(mseen.alloc((size_t)blocks * Q.nmamb));
         HIPCHK(hipMemsetAsync(mseen.p, 0, (size_t)blocks * Q.nmamb * 4, ctx->stream));
         Q.mseen = mseen.p;
+        HIPCHK(oflag.alloc(N));
+        HIPCHK(hipMemsetAsync(oflag.p, 0, (size_t)N, ctx->stream));
+        Q.oflag = oflag.p;
     }
     HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
     if (nsrc > 0) {
@@ -2170,8 +2313,10 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     ctx->last_vga_s = ms * 1e-3;
     int hc[2];
     HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
-    if (hc[1] & KERR_ORDER) return fail(DMX_ERR_UNSUPPORTED, k_order_msg);
-    if (hc[1]) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level/frontier capacity");
+    if (hc[1] & ~KERR_ORDER) return fail(DMX_ERR_CAPACITY, "VGA BFS exceeded its level/frontier capacity");
+    ctx->last_stats[38] = 0;
+    if (hc[1] & KERR_ORDER)
+        if (int rc2 = vga_order_rerun(ctx, g, radius, oflag.p, outp, P.levels_out)) return rc2;
     unsigned long long st[8];
     HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
     ctx->last_stats[8] = (long long)st[5];   // bottom-up cells that scanned all their runs without a hit
@@ -2736,6 +2881,13 @@ int dmx_graph_special_nodes(dmx_graph* g, int32_t* nodes, int64_t* n) {
     return DMX_OK;
 }
 
+int dmx_ctx_last_mk_reruns(dmx_ctx* ctx, int64_t* nodes, int64_t cap, int64_t* n) {
+    if (!ctx || !n || cap < 0 || (cap > 0 && !nodes)) return fail(DMX_ERR_ARG, "bad arguments");
+    *n = (int64_t)ctx->last_mk_reruns.size();
+    for (int64_t i = 0; i < *n && i < cap; i++) nodes[i] = ctx->last_mk_reruns[(size_t)i];
+    return DMX_OK;
+}
+
 int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {
     if (!ctx || !out5) return fail(DMX_ERR_ARG, "bad arguments");
     for (int i = 0; i < 5; i++) out5[i] = ctx->phase_cycles[i];
@@ -2751,7 +2903,7 @@ int dmx_ctx_last_phase_cycles(dmx_ctx* ctx, int64_t* out5) {
 // Visual step depth for grids above 1024^2 or asymmetric graphs: the level-synchronous top-down
 // search of kernels/vstep.hip over the whole GPU.
 static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vector<int32_t>& seeds, int tw, int th,
-                                    float* out) {
+                                    float* out, const std::vector<int32_t>& sel_cells) {
     PointMapHost& h = *g->pm->host;
     const int rows = h.rows();
     const int64_t C = h.cells(), N = g->nnodes, nt = (int64_t)tw * th;
@@ -2812,8 +2964,17 @@ static int visual_stepdepth_topdown(dmx_ctx* ctx, dmx_graph* g, const std::vecto
     }
     int herr = 0;
     HIPCHK(copy_sync(s, &herr, err.p, sizeof(int), hipMemcpyDeviceToHost));
-    if (herr & KERR_ORDER) return fail(DMX_ERR_UNSUPPORTED, k_order_msg);
     HIPCHK(hipEventRecord(ctx->ev1, s));
+    if (herr & KERR_ORDER) {
+        // an unexpanded link end whose extraction depends on the pop order reached an unseen cell: the whole
+        // search in the reference's order (vga_ordered.hip), from the selection in PixelRef order
+        HIPCHK(hipMemsetAsync(level.p, 0xFF, C * 4, s));
+        if (int rc = ordered_search(ctx, g, -1.0, {}, sel_cells, nullptr, nullptr, level.p)) return rc;
+        HIPCHK(hipEventRecord(ctx->ev1, s));
+        ctx->last_stats[38] = 1;
+    } else {
+        ctx->last_stats[38] = 0;
+    }
     HIPCHK(copy_sync(s, lv.data(), level.p, C * 4, hipMemcpyDeviceToHost));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
@@ -2838,10 +2999,11 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
     const int cols = h.cols(), rows = h.rows();
     const int64_t C = (int64_t)cols * rows, N = g->nnodes;
     for (int64_t k = 0; k < N; k++) out[k] = -1.0f;
+    ctx->last_stats[38] = 0;
     const auto& st = h.state();
     std::vector<int32_t> seeds;   // nodes, selection order = std::set<int> PixelRef order, unique
+    std::vector<int32_t> sel;     // the selected filled cells in that order
     {
-        std::vector<int32_t> sel;
         for (int64_t i = 0; i < nsel; i++) {
             const int32_t c = sel_cells[i];
             if (c < 0 || c >= C) return fail(DMX_ERR_ARG, "selected cell outside the grid");
@@ -2883,7 +3045,7 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
         if (rc) return rc;
         tile = g->symmetric == 1;
     }
-    if (!tile) return visual_stepdepth_topdown(ctx, g, seeds, tw, th, out);
+    if (!tile) return visual_stepdepth_topdown(ctx, g, seeds, tw, th, out, sel);
     DevBuf<int32_t> d_seeds, d_level;
     HIPCHK(d_seeds.alloc(seeds.size()));
     HIPCHK(d_level.alloc((size_t)nt * 64));

@@ -9,6 +9,18 @@ namespace dmx {
 
 constexpr int WAVE = 64;
 
+// Kernel parameters read through a pointer to device memory (the persistent kernels: a large struct, its cold
+// fields reloaded with scalar loads instead of held in SGPRs).  Read through the constant address space, so
+// the compiler knows the pointers inside it are global: their loads, stores and atomics are global_* ops.
+// Through a generic pointer they would be flat_* ops, which count against both the memory and the LDS
+// counters and return out of order, so every use of a loaded value waits for all LDS and memory operations
+// in flight (vmcnt(0) lgkmcnt(0)).
+#define DMX_CONST_AS __attribute__((address_space(4)))
+template <typename T>
+__device__ __forceinline__ const DMX_CONST_AS T& const_params(const T* p) {
+    return *(const DMX_CONST_AS T*)p;
+}
+
 // Error flags raised by kernels (bitwise OR into a device word; the host maps them to status codes).
 enum KernelError : int {
     KERR_GAP_CAPACITY = 1,     // sieve gap list exceeded LDS capacity
@@ -109,7 +121,8 @@ __device__ __forceinline__ void merge_level_pass(const int2* mpairs, int nmp, in
 // other end b expandable.  When a source discovers both at the same level L (< radius), the reference's
 // outcome depends on which it pops first (vgavisualglobal.cpp:99-122): b first extracts a (a is not
 // counted, its runs feed L + 1); a first counts a and leaves it unexpanded.  The level-synchronous BFS
-// cannot tell, so such a source raises KERR_ORDER.  In every other case the merge pass above is exact: a
+// cannot tell, so such a source raises KERR_ORDER and is marked in oflag[src]: the host re-runs it in the
+// reference's own order (vga_ordered.hip).  In every other case the merge pass above is exact: a
 // new at L is not in F (not expanded) and so extracts nothing, and b extracts an unvisited a into F.
 // Called after the merge pass of level L (F: the expandable cells new at L; V includes every cell new at
 // L).  mamb[k] = (a, b); mseen[k] (per workgroup, thread k's own slot across levels) holds the stamp of the
@@ -119,7 +132,7 @@ __device__ __forceinline__ void merge_level_pass(const int2* mpairs, int nmp, in
 __device__ __forceinline__ void merge_order_check(const int2* mamb, int nmamb, int rows, int tw, int ntpb,
                                                   const unsigned long long* F, const unsigned long long* V,
                                                   bool v_lds, const unsigned long long* seed_tiles, int32_t* mseen,
-                                                  int32_t stamp, int* error) {
+                                                  int32_t stamp, int* error, uint8_t* oflag, int64_t src) {
     for (int k = threadIdx.x; k < nmamb; k += ntpb) {
         if (mseen[k] == stamp) continue;
         const int2 pr = mamb[k];
@@ -131,7 +144,10 @@ __device__ __forceinline__ void merge_order_check(const int2* mamb, int nmamb, i
             v_lds ? V[at] : __hip_atomic_load(&V[at], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (!(vw & ab)) continue;
         mseen[k] = stamp;
-        if ((F[bt] & bb) && !(F[at] & ab)) atomicOr(error, (int)KERR_ORDER);
+        if ((F[bt] & bb) && !(F[at] & ab)) {
+            atomicOr(error, (int)KERR_ORDER);
+            oflag[src] = 1;
+        }
     }
 }
 

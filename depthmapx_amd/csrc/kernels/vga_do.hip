@@ -58,6 +58,7 @@ struct VgaDoParams {
     const int2* mamb;           // [nmamb] links with a context-filled odd end (merge_order_check)
     int nmamb = 0;
     int32_t* mseen = nullptr;   // per workgroup [nmamb]
+    uint8_t* oflag = nullptr;   // [N] sources whose result depends on the reference's pop order
 };
 
 constexpr int DO_THREADS = 256;
@@ -407,7 +408,7 @@ __global__ void __launch_bounds__(DO_THREADS) vga_do_kernel(VgaDoParams P) {
                 if (P.nmamb) {
                     __syncthreads();
                     merge_order_check(P.mamb, P.nmamb, rows, tw, DO_THREADS, F, V, !GBM, P.seed_tiles,
-                                      P.mseen + (size_t)blockIdx.x * P.nmamb, (int32_t)src + 1, P.error);
+                                      P.mseen + (size_t)blockIdx.x * P.nmamb, (int32_t)src + 1, P.error, P.oflag, src);
                 }
             }
             __syncthreads();

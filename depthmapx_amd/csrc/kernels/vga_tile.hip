@@ -96,6 +96,7 @@ struct VgaTileParams {
     const int2* mamb;         // [nmamb] links with a context-filled odd end (that end first; merge_order_check)
     int nmamb;
     int32_t* mseen;           // per workgroup [nmamb] (merge_order_check)
+    uint8_t* oflag;           // [N] sources whose result depends on the reference's pop order (merge_order_check)
     int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
     int32_t* nlev_out;        // [N] levels (0: source skipped)
     int* error;
@@ -564,7 +565,7 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
 // so a row or column run still costs its summary words plus at most 2 frontier words.
 template <int NT, bool SPECIAL, bool RBM, bool FG>
 __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __restrict__ PP) {
-    const VgaTileParams& P = *PP;
+    const DMX_CONST_AS VgaTileParams& P = const_params(PP);
     extern __shared__ __attribute__((aligned(16))) unsigned long long tile_smem[];
     __shared__ TileShared S;
     constexpr int NW = NT / 64;
@@ -1156,7 +1157,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 if (P.nmamb && !seeded) {
                     __syncthreads();
                     merge_order_check(P.mamb, P.nmamb, rows, tw, NT, F, Vg, false, P.seed_tiles,
-                                      P.mseen + (size_t)blockIdx.x * P.nmamb, (int32_t)node + 1, P.error);
+                                      P.mseen + (size_t)blockIdx.x * P.nmamb, (int32_t)node + 1, P.error, P.oflag, node);
                 }
             }
             if (RBM) {

@@ -85,6 +85,18 @@ class Context:
                     mode=["serial", "batched", "batched-overflow-serial"][int(d[0])], batches=int(d[1]),
                     improved=int(d[2]), ambiguous=int(d[3]))
 
+    def last_mk_reruns(self):
+        """The sources the last makeGraph swept again: (certificate re-runs, capacity re-runs), node indices
+        (dmx_ctx_last_mk_reruns)."""
+        n = ctypes.c_int64()
+        N.check(N.lib().dmx_ctx_last_mk_reruns(self.h, None, 0, ctypes.byref(n)))
+        out = np.zeros(max(n.value, 1), dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_mk_reruns(self.h, N.ptr(out), n.value, ctypes.byref(n)))
+        out = out[:n.value]
+        cap = (out >> 62) & 1
+        nodes = out & ((1 << 62) - 1)
+        return np.unique(nodes[cap == 0]), np.unique(nodes[cap == 1])
+
     def last_phase_cycles(self):
         out = np.zeros(5, dtype=np.int64)
         N.check(N.lib().dmx_ctx_last_phase_cycles(self.h, N.ptr(out)))
@@ -97,7 +109,8 @@ class Context:
                 "vga_cells_reached", "vga_sources", "vga_fail_cells", "vga_fail_runs", "vga_hbm_bitmaps",
                 "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",
                 "vga_hard_cells", "vga_hard_certain", "vga_topdown_cycles", "vga_b_tiles", "vga_b_cells", "vga_tt_tiles", "vga_c_busy", "vga_c_scan", "vga_c_spec", "vga_n_spec", "vga_tt_pruned", "vga_b_row_cycles", "vga_b_cell_tiles",
-                "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks", "mk_reruns", "vga_pmask_loads", "vga_pmask_cells", "vga_pmask_bytes"]
+                "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks", "mk_reruns", "vga_pmask_loads", "vga_pmask_cells", "vga_pmask_bytes",
+                "vga_order_reruns"]
         # vga_c_scan, vga_c_spec, vga_b_row_cycles and vga_b_cell_cycles stay 0: the kernel no longer reads
         # the clock per hard cell or per tile (2.6 % of the 1000^2 VGA); the per-phase clocks remain
         d = {k: int(v) for k, v in zip(keys, out)}

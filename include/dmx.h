@@ -81,8 +81,15 @@ int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
  * over sources), [7] sources run, [8] bottom-up cells that found no hit, [9] their runs,
  * [10] bitmaps in HBM (direction-optimising), [11] tiles resolved by common runs, [12] launch
  * shape, [13] hard cells rejected by their tile-visibility row, [14] bytes of those rows read,
- * [15] runs scanned by hard cells, [16] hard cells that hit, [17] hard cells. */
+ * [15] runs scanned by hard cells, [16] hard cells that hit, [17] hard cells, ... [38] searches the last VGA
+ * global / visual step depth call ran again in the reference's level order (vga_ordered.hip). */
 int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
+
+/* The sources the last makeGraph swept a second time (graph node indices, in the order the passes listed
+ * them; a source can appear once per pass): bit 62 set for a capacity overflow (gap list, block spill,
+ * staging), clear for a moment-sum certificate that did not decide the float.  Writes
+ * min(cap, *n) entries; *n receives the count. */
+int dmx_ctx_last_mk_reruns(dmx_ctx* ctx, int64_t* nodes, int64_t cap, int64_t* n);
 
 /* Diagnostics of the last tile-resolved VGA launch: core-clock cycles spent (workgroup leader,
  * summed over workgroups) in level 1, phase A (tile-common runs), B (head runs), C (hard cells)
@@ -296,10 +303,11 @@ int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const in
  * 113-122), visual step depth (vgavisualglobaldepth.cpp:55-63), metric / angular all sources
  * (vgametric.cpp:97-105, vgaangular.cpp:95-104) and metric / angular step depth (vgametricdepth.cpp:68-83,
  * vgaangulardepth.cpp:57-67).  Both ends must be filled cells of the graph (DMX_ERR_ARG at the analysis).
- * A link with one end CONTEXTFILLED at an odd PixelRef is followed exactly, except where the reference's
- * result depends on its pop order inside a level: VGA global with a radius where a source finds both ends
- * at one level, and visual step depth where extracting the unexpanded end would reach a new cell -- those
- * calls return DMX_ERR_UNSUPPORTED.  VGA visual local has no merge logic.  The links are set on the
+ * A link with one end CONTEXTFILLED at an odd PixelRef is followed exactly too: where the reference's result
+ * depends on its pop order inside a level (VGA global with a radius where a source finds both ends at one
+ * level; visual step depth where extracting the unexpanded end would reach a new cell) that source or search
+ * is run again in the reference's own level order (kernels/vga_ordered.hip).  VGA visual local has no merge
+ * logic.  The links are set on the
  * graph's point map as well (they belong to the points: a chunk written from it saves them).  A chunk
  * (dmx_chunk_merges, dmx_chunk_load) must store every link on both of its points (DMX_ERR_ARG otherwise). */
 int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n);

@@ -55,6 +55,41 @@ def _check_makegraph_blocks(pm, g, om, blocks, threads=16):
         assert got["bins"][:, :, 3].sum() > 0
 
 
+def _ranges(nodes):
+    """Sorted unique node indices as maximal contiguous [b, e) ranges."""
+    nodes = np.unique(np.asarray(nodes, dtype=np.int64))
+    if len(nodes) == 0:
+        return []
+    cut = np.nonzero(np.diff(nodes) != 1)[0] + 1
+    return [(int(p[0]), int(p[-1]) + 1) for p in np.split(nodes, cut)]
+
+
+def _check_makegraph_sample(g, om, nodes, threads=16):
+    """Bins, runs and the 3 float attributes of every listed node bit-exact against the oracle's sparkPixel2
+    of the same nodes (OracleMap.make_graph_sample: the node list only, 16 threads)."""
+    nodes = np.unique(np.asarray(nodes, dtype=np.int64))
+    om.make_graph_sample(nodes, threads=threads)
+    ref = om.graph()
+    off = np.concatenate([[0], np.cumsum(ref["bins"][:, :, 3].sum(axis=1))])
+    for (b, e) in _ranges(nodes):
+        got = g.copy_range(b, e)
+        np.testing.assert_array_equal(got["bins"], ref["bins"][b:e], err_msg="bins of nodes [%d,%d)" % (b, e))
+        np.testing.assert_array_equal(got["runs"], ref["runs"][off[b]:off[e]], err_msg="runs of nodes [%d,%d)" % (b, e))
+        np.testing.assert_array_equal(got["attrs"].view(np.uint32), ref["attrs"][b:e].view(np.uint32),
+                                      err_msg="attributes of nodes [%d,%d)" % (b, e))
+    return len(nodes)
+
+
+def _mk_wide_sample(N, nblocks, seed, reruns):
+    """nblocks blocks of 64 sources spread over the map (seeded) plus every source the whole-map build
+    re-ran (moment certificate or capacity): the paths whose bit-exactness rests on a certificate."""
+    rng = np.random.default_rng(seed)
+    starts = np.unique(np.concatenate([np.linspace(0, N - BLOCK, nblocks // 2).astype(np.int64),
+                                       rng.integers(0, N - BLOCK, size=nblocks - nblocks // 2)]))
+    blocks = np.concatenate([np.arange(b, b + BLOCK) for b in starts])
+    return np.unique(np.concatenate([blocks] + [np.asarray(r, dtype=np.int64) for r in reruns])), len(starts)
+
+
 def _release(ctx, *objs):
     for o in objs:
         o.close()
@@ -71,6 +106,7 @@ def big1000(ctx):
     pm = dmx.PointMap(region, lines, 1.0)
     assert pm.make_points(0.5, 0.5)
     g = pm.make_graph(ctx)
+    g.reruns = ctx.last_mk_reruns()
     om = OracleMap(region, 1.0, lines)
     assert om.fill(0.5, 0.5)
     yield pm, g, om
@@ -84,6 +120,20 @@ def test_1000_makegraph_blocks_match_oracle(big1000):
     assert info["nnodes"] == pm.info()["filled"] == 998001
     np.testing.assert_array_equal(pm.state(), om.state())
     _check_makegraph_blocks(pm, g, om, _blocks(pm, info["nnodes"], seed=1000))
+
+
+def test_1000_makegraph_wide_sample_matches_oracle(big1000):
+    """configs[2] makeGraph on >= 8,192 sources (128 spread blocks of 64) plus every source the whole-map build
+    swept again -- the ~0.4 % whose certified moment sums straddled a float rounding and any capacity
+    re-runs -- bit-exact against the oracle (~0.8 ms a source on 16 threads)."""
+    pm, g, om = big1000
+    N = g.info()["nnodes"]
+    cert, cap = g.reruns
+    assert len(cert) > 0, "the whole-map build took no certificate re-run"
+    nodes, nb = _mk_wide_sample(N, 128, 1001, [cert, cap])
+    assert nb * BLOCK >= 8192
+    n = _check_makegraph_sample(g, om, nodes)
+    print("1000^2 makeGraph sample: %d sources (%d certificate re-runs, %d capacity re-runs)" % (n, len(cert), len(cap)))
 
 
 def _neighbour_nodes(pm, cells, N):
@@ -230,6 +280,7 @@ def big2000(ctx):
     pm = dmx.PointMap(region, lines, 1.0)
     assert pm.make_points(0.5, 0.5)
     g = pm.make_graph(ctx)
+    g.reruns = ctx.last_mk_reruns()
     om = OracleMap(region, 1.0, lines)
     assert om.fill(0.5, 0.5)
     yield pm, g, om
@@ -272,6 +323,19 @@ def test_2000_makegraph_blocks_match_oracle(big2000):
     _check_makegraph_blocks(pm, g, om, blocks)
 
 
+def test_2000_makegraph_wide_sample_matches_oracle(big2000):
+    """configs[4] makeGraph on >= 4,096 sources (64 spread blocks of 64) plus every source the whole-map build
+    swept again (moment certificate, capacity), bit-exact against the oracle."""
+    pm, g, om = big2000
+    N = g.info()["nnodes"]
+    cert, cap = g.reruns
+    assert len(cert) > 0, "the whole-map build took no certificate re-run"
+    nodes, nb = _mk_wide_sample(N, 64, 2002, [cert, cap])
+    assert nb * BLOCK >= 4096
+    n = _check_makegraph_sample(g, om, nodes)
+    print("2000^2 makeGraph sample: %d sources (%d certificate re-runs, %d capacity re-runs)" % (n, len(cert), len(cap)))
+
+
 def test_2000_metric_stepdepth_batched_equals_serial(big2000, ctx, monkeypatch):
     """configs[4] step depth from the cell nearest the centre: batched == serial on every column, and
     the result's invariants (every reached cell's length >= its straight-line distance; the selected
@@ -301,11 +365,11 @@ def test_2000_vga_sources_match_oracle(big2000, ctx):
     """configs[4] grid (2000^2, above the 1024^2 that an LDS frontier holds): the tile BFS with its frontier in
     HBM and its line summaries in LDS, on seeded sources -- a block in the middle of the map, one next to the
     densest occluders and random ones -- against the oracle's BFS over the same graph (node count exact,
-    floats within 1e-6).  16 sources (one oracle BFS is ~1 minute of CPU here); DMX_TEST_WIDE=1 checks 64."""
+    floats within 1e-6).  64 sources (one oracle BFS is ~1 minute of CPU here, 16 threads)."""
     import torch
     pm, g, om = big2000
     N = g.info()["nnodes"]
-    n = 64 if os.environ.get("DMX_TEST_WIDE") else 16
+    n = 64
     rng = np.random.default_rng(2000)
     (db, _), _ = _densest_block(pm, N)
     src = sorted(set([N // 2, N // 2 + 1, db, db + 1] + [int(v) for v in rng.integers(0, N, size=n)]))[:n]

@@ -14,7 +14,8 @@ CPU: the C restatement (oracle/) against the columns the real reference wrote fo
 built from source) -- this pins the oracle's merge semantics.  GPU: the HIP kernels against the pinned
 oracle on seeded synthetic maps with random merge links (every kernel family: tile-resolved BFS,
 direction-optimising BFS, top-down visual step depth, the serial metric / angular searches), and the
-exact handling of links with a context-filled end, refused only where the reference's pop order decides."""
+exact handling of links with a context-filled end, in the reference's own level order where its pop order
+decides (kernels/vga_ordered.hip)."""
 import json
 import lzma
 import os
@@ -257,12 +258,12 @@ def _contextfilled_links(seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [3, 4, 6])
 @pytest.mark.parametrize("kernel", ["tile", "do"])
-def test_gpu_contextfilled_links_exact_or_refused_where_order_matters(ctx, monkeypatch, seed, kernel):
+def test_gpu_contextfilled_links_exact_where_order_matters(ctx, monkeypatch, seed, kernel):
     """Merge links with a context-filled odd end under a radius: the GPU answers exactly what the reference
-    computes, unless some source finds both ends at one level -- then the reference's count depends on its
-    pop order inside the level (the oracle's two orders differ) and the call is refused (DMX_ERR_UNSUPPORTED).
-    Radius n expands every cell and always runs."""
-    import depthmapx_amd as dmx
+    computes.  Where some source finds both ends at one level the reference's count depends on its pop order
+    inside the level (the oracle's two orders differ): the level-synchronous kernel flags those sources and
+    they run again in the reference's order (vga_order_reruns > 0); elsewhere nothing is re-run.  Radius n
+    expands every cell."""
     import pyoracle
     if kernel == "do":
         monkeypatch.setenv("DMX_VGA_KERNEL", "do")
@@ -284,25 +285,22 @@ def test_gpu_contextfilled_links_exact_or_refused_where_order_matters(ctx, monke
         finally:
             pyoracle.set_pop_forward(False)
         order_free = np.array_equal(ref.view(np.uint32), fwd.view(np.uint32))
-        try:
-            got = g.vga_visual_global(radius=radius)
-        except dmx.DmxError as e:
-            assert e.status == -5
-            assert not order_free, radius
-            outcomes.append("refused")
-            continue
+        got = g.vga_visual_global(radius=radius)
+        reruns = ctx.last_stats()["vga_order_reruns"]
         np.testing.assert_array_equal(got[:, 5], ref[:, 5])
         assert np.allclose(got, ref, rtol=1e-6, atol=1e-6)
-        outcomes.append("exact")
+        if not order_free:
+            assert reruns > 0, radius
+        outcomes.append("reference order" if reruns else "level-synchronous")
     assert len(outcomes) == 3
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", [3, 4, 6])
 def test_gpu_visual_step_depth_with_contextfilled_links(ctx, seed):
-    """Visual step depth with context-filled odd link ends: exact (bit for bit with the oracle), or refused
-    only where extracting an unexpanded end would reach a new cell -- where the two pop orders differ."""
-    import depthmapx_amd as dmx
+    """Visual step depth with context-filled odd link ends: exact (bit for bit with the oracle).  Where
+    extracting an unexpanded end would reach a new cell (the two pop orders can differ) the search runs in the
+    reference's order (vga_order_reruns == 1)."""
     import pyoracle
     pm, om, om2, pairs = _contextfilled_links(seed)
     pm.set_merges(pairs)
@@ -323,12 +321,9 @@ def test_gpu_visual_step_depth_with_contextfilled_links(ctx, seed):
             fwd = om2.visual_stepdepth([c])
         finally:
             pyoracle.set_pop_forward(False)
-        try:
-            got = g.visual_step_depth(cells=[c])
-        except dmx.DmxError as e:
-            assert e.status == -5
-            assert not np.array_equal(ref.view(np.uint32), fwd.view(np.uint32))
-            continue
+        got = g.visual_step_depth(cells=[c])
+        if not np.array_equal(ref.view(np.uint32), fwd.view(np.uint32)):
+            assert ctx.last_stats()["vga_order_reruns"] == 1
         np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
         ran += 1
     assert ran > 0

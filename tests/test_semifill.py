@@ -12,7 +12,8 @@ seed), mixed_gallery (plus a block of FULL cells drawn with the pencil tool, Poi
 (the reference's makeGraph of it) and mixed_link (plus merge links from LINK mode: a context-filled odd cell to
 a full cell, a context-filled even cell to an odd one).  The .graph regression cases on them (semi_*, mixed_*,
 link_*) run through dmxcli in test_graphfile.py; here: the fill itself, the oracle pinned on every case, the
-three BFS kernels on the reference's graph, and the order dependence behind the two refused cases.
+three BFS kernels on the reference's graph, and the order dependence of link_vis_global_3, which the engine
+answers in the reference's own level order (kernels/vga_ordered.hip).
 """
 import ctypes
 import json
@@ -254,14 +255,15 @@ def _both_orders(om, pmd, args):
     return fwd, back, fwd_nolink, back_nolink
 
 
-def test_refused_case_depends_on_the_pop_order(tmp_path):
+def test_order_dependent_case_depends_on_the_pop_order(tmp_path):
     """What link_vis_global_3 computes changes with the order the reference pops a level in: the oracle with
     the reference's order (back to front) reproduces the reference's columns, front to back it does not (a
     source finds a context-filled odd cell and its linked full cell at one level: popped first, the full
     cell extracts its partner, which is then never counted).  On the same map without the links the order
-    changes nothing.  The engine refuses the case (test_graphfile: DMX_ERR_UNSUPPORTED)."""
+    changes nothing.  The engine runs such sources in the reference's order (test_graphfile runs the case and
+    compares it with the reference's output; test_merge_links covers seeded maps)."""
     case = "link_vis_global_3"
-    assert CASES[case].get("refused")
+    assert not CASES[case].get("refused")
     om, pmd = _oracle_map(tmp_path, case)
     fwd, back, fwd_nolink, back_nolink = _both_orders(om, pmd, CASES[case]["args"])
     _compare(back, _ref_cols(case), CASES[case]["columns"])
