@@ -460,7 +460,6 @@ size_t makegraph_lds(int gcap, int bcap, int D) {
     b += 16 * (size_t)gcap * 2 + 16 * (size_t)bcap; // gaps, gaps2, blocks
     b += 4 * 32 * 3 + 4 * 32;                        // binc, bfar, bnr, misc
     b += 16 * (size_t)bcap;                          // bsorted
-    b += 8 * (size_t)MK_EB;                          // staged emission records
     b += 4 * (size_t)gcap + 8 * (size_t)gcap + 4 * (size_t)bcap + 4 * ((size_t)gcap + 4);
     b += 4 * (size_t)std::min(D + 4, MK_OPEN_LDS);   // open-run state of the near rows (makegraph.hip)
     return (b + 15) & ~(size_t)15;
@@ -1810,7 +1809,8 @@ static int prepare_tiles(dmx_graph* g) {
     }
     const int dmax = std::max(cols, rows);
     const size_t lds = (size_t)8 * (dmax + 2) * 4;
-    if (lds > 150 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the tile-common-run pass");
+    // a capacity of the tile path: the callers fall back to the direction-optimising / top-down searches
+    if (lds > 150 * 1024) return fail(DMX_ERR_CAPACITY, "grid too long for the tile-common-run pass");
     hipLaunchKernelGGL(tile_cr_kernel, dim3((unsigned)std::min<int64_t>(nt, (int64_t)ctx->num_cu * 8)), dim3(CR_THREADS),
                        lds, s, cols, rows, tw, th, g->regular_tiles.p, g->pm->d_cell_node.p, g->node_run_start.p,
                        g->node_nruns.p, g->scan_start.p, g->scan_pool.p, g->pool.p, dmax, g->cr.p);
@@ -1854,7 +1854,7 @@ static int prepare_tiles(dmx_graph* g) {
         }
         const int ncw = (nt + 3) / 4;
         const size_t tv_lds = ((size_t)(ncw + 1) / 2 + (size_t)(tvw + (ncw + 1) / 2)) * 8;   // one node per workgroup
-        if (tv_lds > 150 * 1024) return fail(DMX_ERR_UNSUPPORTED, "grid too large for the tile-visibility pass");
+        if (tv_lds > 150 * 1024) return fail(DMX_ERR_CAPACITY, "grid too large for the tile-visibility pass");
         int64_t pb, pe;
         prep_range(g, pb, pe);
         if (pe > pb) {
@@ -1878,7 +1878,8 @@ static int prepare_tiles(dmx_graph* g) {
         const char* pm_env = getenv("DMX_VGA_PMASK");
         if (ftv && !(pm_env && atoi(pm_env) == 0))
             if (int rc = prepare_pmask(g, rows, tw, th, tvw, Ct)) return rc;
-        if (wide) {
+        // the row summaries keep word k in lane k (vga_tile.hip reads them with readlane): at most 64 words
+        if (wide && (tvw + 63) / 64 <= 64) {
             HIPCHK(g->tvsum.alloc((size_t)Ct * ((tvw + 63) / 64)));
             hipLaunchKernelGGL(tile_vsum_kernel, dim3((unsigned)((Ct + 3) / 4)), dim3(256), 0, s, Ct, tvw, g->tvis.p,
                                g->tvsum.p);
@@ -2519,14 +2520,27 @@ static int vga_search_all(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_o
     return DMX_OK;
 }
 
+// The symmetry scatter a whole-graph makeGraph did as it published (sym_diff 4*C*8 B, sym_ho N*8 B: ~160 MB at
+// 2000^2) serves only the VGA BFS's preparation.  The analyses that do not use it release it; a VGA call after
+// them runs the separate scatter pass instead (prepare_symmetry).
+static void release_sym_scatter(dmx_graph* g) {
+    if (g && g->sym_fused && !g->scan_ready) {
+        g->sym_diff.reset();
+        g->sym_ho.reset();
+        g->sym_fused = false;
+    }
+}
+
 int dmx_vga_metric(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
     SAME_DEVICE(ctx, g);
+    release_sym_scatter(g);
     if (int rc = prepare_merges(g)) return rc;
     return vga_search_all<false>(ctx, g, radius, gates_only, sb, se, out);
 }
 
 int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out) {
     SAME_DEVICE(ctx, g);
+    release_sym_scatter(g);
     if (int rc = prepare_merges(g)) return rc;
     return vga_search_all<true>(ctx, g, radius, gates_only, sb, se, out);
 }
@@ -2534,6 +2548,7 @@ int dmx_vga_angular(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
 // ---------------------------------------------------------------- VGA visual local
 int dmx_vga_local(dmx_ctx* ctx, dmx_graph* g, int gates_only, int64_t sb, int64_t se, float* out) {
     SAME_DEVICE(ctx, g);
+    release_sym_scatter(g);
     if (!ctx || !g || !out) return fail(DMX_ERR_ARG, "bad arguments");
     if (g->node_begin != 0 || g->node_end != g->nnodes)
         return fail(DMX_ERR_STATE, "VGA needs the whole graph (assemble the shards first)");
@@ -2854,12 +2869,14 @@ static int stepdepth_impl(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, 
 
 int dmx_metric_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     SAME_DEVICE(ctx, g);
+    release_sym_scatter(g);
     if (int rc = prepare_merges(g)) return rc;
     return stepdepth_impl<false>(ctx, g, sel_cells, nsel, out);
 }
 
 int dmx_angular_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, int64_t nsel, float* out) {
     SAME_DEVICE(ctx, g);
+    release_sym_scatter(g);
     if (int rc = prepare_merges(g)) return rc;
     return stepdepth_impl<true>(ctx, g, sel_cells, nsel, out);
 }
@@ -3053,6 +3070,7 @@ int dmx_visual_stepdepth(dmx_ctx* ctx, dmx_graph* g, const int32_t* sel_cells, i
     HIPCHK(hipMemsetAsync(d_level.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
     std::vector<float> dummy(7);
     rc = vga_tile_impl(ctx, g, -1.0, 0, 0, 1, dummy.data(), false, nullptr, tw, th, d_seeds.p, (int)seeds.size(), d_level.p);
+    if (rc == DMX_ERR_CAPACITY) return visual_stepdepth_topdown(ctx, g, seeds, tw, th, out, sel);
     if (rc) return rc;
     std::vector<int32_t> lv((size_t)nt * 64);
     HIPCHK(copy_sync(ctx->stream, lv.data(), d_level.p, lv.size() * 4, hipMemcpyDeviceToHost));
@@ -3280,6 +3298,12 @@ int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n) {
     g->pm->host->set_merge(std::move(per_cell));
     g->merges = std::move(uniq);
     g->merges_ready = false;
+    if (g->merges.empty()) {   // prepare_merges returns early on no links: drop the previous links' device state
+        g->nmamb = 0;
+        g->d_mamb.reset();
+        g->d_mpairs.reset();
+        g->d_merge_cell.reset();
+    }
     return DMX_OK;
 }
 

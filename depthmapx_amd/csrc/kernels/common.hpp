@@ -15,7 +15,12 @@ constexpr int WAVE = 64;
 // Through a generic pointer they would be flat_* ops, which count against both the memory and the LDS
 // counters and return out of order, so every use of a loaded value waits for all LDS and memory operations
 // in flight (vmcnt(0) lgkmcnt(0)).
+// (The host pass only type-checks the kernels; there the qualifier is left out.)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define DMX_CONST_AS __attribute__((address_space(4)))
+#else
+#define DMX_CONST_AS
+#endif
 template <typename T>
 __device__ __forceinline__ const DMX_CONST_AS T& const_params(const T* p) {
     return *(const DMX_CONST_AS T*)p;

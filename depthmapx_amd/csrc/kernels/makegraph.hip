@@ -23,25 +23,33 @@
 
 namespace dmx {
 
+// A/B flags of this round (scripts/build_ab.sh -DMKF_...=0/1)
+#ifndef MKF_OBIN
+#define MKF_OBIN 1   // the octant's 5 class bins packed in one word (bit-field extract, no per-class registers)
+#endif
+#ifndef MKF_CLASS
+#define MKF_CLASS 1  // ratio class without short-circuit branches; the FP64 whichbin only behind a wave vote
+#endif
+#ifndef MKF_MOM
+#define MKF_MOM 1    // moments and far distances from dx^2 + dy^2 (sqrt_nr, exact integer second moment)
+#endif
+#ifndef MKF_YMAJ
+#define MKF_YMAJ 0   // V octants read the y-major copy of the cell words (a chunk's lanes load consecutive words)
+#endif
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
 // open-run state of rows 0 .. MK_OPEN_LDS-1 lives in LDS, of farther rows (grids above ~1020 cells a
 // side) in per-wave scratch memory: rows past 1024 are reached only by sight lines longer than 1024
 // cells, and a full-length LDS array would cost a 2000^2 grid a quarter of its waves
 constexpr int MK_OPEN_LDS = 1024;
-// emission records staged in LDS per wave (flushed to the wave's HBM staging area when full): the hot loop then
-// issues no global stores, whose completion every later load wait would include (vmcnt counts loads and
-// stores together, in order)
-constexpr int MK_EB = 128;
-// failure-list entries: node | MK_CAPACITY_TAG for a capacity overflow (else a moment certificate failure)
 constexpr int64_t MK_CAPACITY_TAG = 1ll << 62, MK_NODE_MASK = MK_CAPACITY_TAG - 1;
 
 struct MakeGraphParams {
     int cols, rows;
     double spacing, blx, bly;
     double maxdist;
-    const uint32_t* cellw;     // [C] packed cell word (common.hpp), x-major
-    const uint32_t* cellw_t;   // [C] the same words y-major (the V octants' lines)
-    double sqrt_err;           // bound on |MK_SQRT(n) - sqrt(n)| / sqrt(n) over the integers n <= 2 dmax^2
+    const uint32_t* cellw;     // [C] packed cell word (common.hpp)
+    const uint32_t* cellw_t;
+    double sqrt_err;
     const double* segs;        // [S][4] cropped segment start/end
     const int32_t* node_cell;  // [N] node -> x-major cell index
     int64_t node_begin, node_end;
@@ -228,68 +236,71 @@ __device__ __forceinline__ uint32_t pack_open(int slot, int s, int l) {
 
 // ---- certified moment sums
 // The reference accumulates sum(d) and sum(d*d) as two serial FP64 chains in addlist order
-// (pointdata.cpp:1490-1495) and stores them as floats.  The fast path sums each lane's share, reduces the
-// wave, and bounds the distance between that and the serial chain (the chain's rounding, gamma_(n-1) * sum
-// for non-negative summands, plus ours): when every double within that bound rounds to the same float,
-// that float IS the reference's value.  Otherwise the source is re-run with the serial chains
-// (exact_moments), which happens for ~0.4 % of sources at 1000^2.
+// (pointdata.cpp:1490-1495) and stores them as floats.  The fast path sums each lane's share in
+// double-double (error-free TwoSum), reduces the wave, and bounds the serial chain's rounding error
+// by gamma_(n-1) * sum (non-negative summands): when every double within that bound rounds to the
+// same float, that float IS the reference's value.  Otherwise the source is re-run with the serial
+// chains (exact_moments), which happens for ~0.2 % of sources at 1000^2.
+__device__ __forceinline__ void dd_add(double& h, double& l, double v) {
+    const double s = h + v;
+    const double bb = s - h;
+    l += (h - (s - bb)) + (v - bb);
+    h = s;
+}
+__device__ __forceinline__ void dd_merge(double& h, double& l, double bh, double bl) {
+    const double s = h + bh;
+    const double bb = s - h;
+    const double e = (h - (s - bb)) + (bh - bb);
+    const double t = (l + bl) + e;
+    h = s + t;
+    l = t - (h - s);
+}
+// Plain per-lane double sums reduced by a 6-level butterfly: |S~ - S| <= gamma_(m+6) S with m the
+// largest per-lane count; the reference's serial chain is within gamma_(n-1) S of S.
+__device__ __forceinline__ bool certified_float_sum(double S, long long n, long long m, float* out) {
+    const double u = 0x1p-53;
+    const double g1 = (double)n * u / (1.0 - (double)n * u);
+    const double g2 = (double)(m + 7) * u / (1.0 - (double)(m + 7) * u);
+    const double E = 2.0 * (g1 + g2) * S + S * 0x1p-50;
+    const float a = (float)(S - E), b = (float)(S + E);
+    *out = a;
+    return a == b;
+}
+__device__ __forceinline__ bool certified_float(double h, double l, long long n, float* out) {
+    const double u = 0x1p-53;
+    const double g = (double)n * u / (1.0 - (double)n * u);
+    const double E = 2.0 * g * h + 2.0 * fabs(l) + h * 0x1p-50;
+    const float a = (float)(h - E), b = (float)(h + E);
+    *out = a;
+    return a == b;
+}
+
 // The float of S when every double within E of S rounds to it (then it is the float of any sum within E).
-__device__ __forceinline__ bool certified_float(double S, double E, float* out) {
+__device__ __forceinline__ bool certified_float_e(double S, double E, float* out) {
     const float a = (float)(S - E), b = (float)(S + E);
     *out = a;
     return a == b;
 }
 
-// Square roots of the moment sums: v_rsq_f64 (~2^-23 relative) and one Newton step (5 FP64 instructions; the
-// error, ~2^-44, is measured exhaustively over the integers the kernel feeds it by sqrt_err_kernel and bounds
-// the certificate) instead of the correctly rounded expansion (~17 instructions; v_sqrt_f64 alone is only
-// good to ~2^-23).  -DDMX_MK_IEEESQRT: the IEEE square root (A/B builds).
+// Square roots of the moment sums (MKF_MOM): v_rsq_f64 (~2^-23 relative) and one Newton step (5 FP64
+// instructions; the error, ~2^-44, is measured exhaustively over the integers the kernel feeds it by
+// sqrt_err_kernel and bounds the certificate) instead of the correctly rounded expansion (~17 instructions).
 __device__ __forceinline__ double sqrt_nr(double x) {   // x >= 1
     const double r = __builtin_amdgcn_rsq(x);
     const double g = x * r, h = 0.5 * r;
     return fma(fma(-g, g, x), h, g);
 }
-#ifdef DMX_MK_IEEESQRT
-#define MK_SQRT(x) sqrt(x)
-#else
-#define MK_SQRT(x) sqrt_nr(x)
-#endif
 
-// max over n in [1, nmax] of |MK_SQRT(n) - sqrt(n)| / sqrt(n), as the bits of a non-negative double
+// max over n in [1, nmax] of |sqrt_nr(n) - sqrt(n)| / sqrt(n), as the bits of a non-negative double
 __global__ void sqrt_err_kernel(long long nmax, unsigned long long* err_bits) {
     double e = 0.0;
     for (long long n = 1 + (long long)blockIdx.x * blockDim.x + threadIdx.x; n <= nmax;
          n += (long long)gridDim.x * blockDim.x) {
-        const double x = (double)n, r = sqrt(x), h = MK_SQRT(x);
+        const double x = (double)n, r = sqrt(x), h = sqrt_nr(x);
         e = fmax(e, fabs(h - r) / r);
     }
     for (int off = 32; off >= 1; off >>= 1) e = fmax(e, __shfl_xor(e, off));
     if ((threadIdx.x & 63) == 0) atomicMax(err_bits, (unsigned long long)__double_as_longlong(e));
-}
-
-// DPP scans (no LDS round trip).  Row scans cover lanes 0..15 of each row of 16; the wave scan all 64 lanes.
-template <int CTRL, int ROWM = 0xf>
-__device__ __forceinline__ int dpp_(int old, int v) { return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWM, 0xf, false); }
-__device__ __forceinline__ int row_incl_sum(int v) {
-    v += dpp_<0x111>(0, v);
-    v += dpp_<0x112>(0, v);
-    v += dpp_<0x114>(0, v);
-    v += dpp_<0x118>(0, v);
-    return v;
-}
-// exclusive prefix max within the row, identity 0 (v >= 0)
-__device__ __forceinline__ int row_excl_max0(int v) {
-    v = max(v, dpp_<0x111>(0, v));
-    v = max(v, dpp_<0x112>(0, v));
-    v = max(v, dpp_<0x114>(0, v));
-    v = max(v, dpp_<0x118>(0, v));
-    return dpp_<0x111>(0, v);
-}
-__device__ __forceinline__ int wave_incl_sum_dpp(int v) {
-    v = row_incl_sum(v);
-    v += dpp_<0x142, 0xa>(0, v);   // row_bcast:15 into rows 1 and 3
-    v += dpp_<0x143, 0xc>(0, v);   // row_bcast:31 into rows 2 and 3
-    return v;
 }
 
 struct Lds {
@@ -305,7 +316,6 @@ struct Lds {
     int* bnr;         // [32] runs per bin
     int* misc;        // [32] scalars: 0 ng, 1 nb, 16..23 segment start, 24..31 segment length
     double2* bsorted; // [bcap] sort output
-    unsigned long long* emit;   // [MK_EB] staged emission records
     int* bflag;       // [bcap] first-occurrence flags
 };
 
@@ -342,7 +352,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         L.bnr = (int*)p; p += 4 * 32;
         L.misc = (int*)p; p += 4 * 32;
         L.bsorted = (double2*)p; p += sizeof(double2) * bcap;
-        L.emit = (unsigned long long*)p; p += 8 * MK_EB;
         L.gc = (int2*)p; p += 8 * gcap;   // (8-aligned: follows the 16-byte arrays)
         L.ga = (int*)p; p += 4 * gcap;
         L.bflag = (int*)p; p += 4 * bcap;
@@ -372,7 +381,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     auto pref = P.prefix + (size_t)wave_global * (3 * (D + 1) + 4);
     auto rcnt = P.runcnt + (size_t)wave_global * (3 * (D + 1) + 4);   // zeroed by the host
     const double sp = P.spacing;
-    const int capA = P.capA;
 
     // LDS state that persists across sources is reset here once
     const int AX = 3 * (D + 1); // rcnt[AX] counts the runs of the axis row (ind 0)
@@ -395,7 +403,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     for (;;) {
         int s_idx = 0;
         if (lane == 0) s_idx = ctl_poll(P.ctl, atomicAdd(P.work_counter, 1));
-        s_idx = __builtin_amdgcn_readfirstlane(__shfl(s_idx, 0));
+        s_idx = __shfl(s_idx, 0);
         int64_t node;
         if (P.node_list) {
             if (s_idx >= P.list_n) break;
@@ -405,22 +413,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             if (node >= P.node_end) break;
         }
         const int cell = P.node_cell[node];
-        const int cx = __builtin_amdgcn_readfirstlane(cell / P.rows), cy = __builtin_amdgcn_readfirstlane(cell % P.rows);
+        const int cx = cell / P.rows, cy = cell % P.rows;
         const double c0x = P.blx + sp * 1.0 * (double)cx, c0y = P.bly + sp * 1.0 * (double)cy;
         if (lane < 32) { L.binc[lane] = 0; L.bfar[lane] = 0; L.bnr[lane] = 0; }
         __syncthreads();
 
         double tsum = 0.0, tsum2 = 0.0; // wave-uniform, reference order (exact_moments)
-        double s1 = 0.0;             // per-lane sum of sqrt(dx^2 + dy^2) (fast path, certified at the end)
-        unsigned long long s2n = 0;  // per-lane sum of dx^2 + dy^2 (exact)
+        double s1 = 0.0, s2 = 0.0;   // per-lane sums (fast path, certified at the end)
+        unsigned long long s2n = 0;  // MKF_MOM: per-lane sum of dx^2 + dy^2 (exact)
         int mcnt = 0;                // this lane's summand count
-        bool binerr = false;         // a visible cell's bin outside its octant (never expected)
-        bool certfail = false;       // the moment certificate failed (re-run with the serial chains)
         int nsize = 0;
         unsigned long long examined = 0;
         uint32_t nsteps = 0, nchunks = 0;   // sieve depth steps / 64-candidate chunks (the source's work)
         int bpos = 0;        // next free run slot in stageB
         bool failed = false;
+        bool certfail = false;
 
         const uint32_t own = P.cellw[cell];
         const int own_n = cell_nseg(own), own_off = cell_seg_off(own);
@@ -459,153 +466,48 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             int dq = 0;                 // deepest depth visited in this octant
             int diag_n = 0, diag_min = 0, diag_max = 0;
             int nA = 0;                 // emissions staged in this octant
-            int nAf = 0;                // ... of which in stA (the rest in L.emit)
-            // L.emit -> stA[nAf..nA)
-            auto flush_emit = [&]() {
-                wave_sync();
-                for (int i = lane; i < nA - nAf; i += 64)
-                    if (nAf + i < capA) stA[nAf + i] = L.emit[i];
-                nAf = nA;
-                wave_sync();
-            };
             const int q_sector = c_sector_base[q], q_axis = c_axis_bin[q], q_diag = c_diag_bin[q];
-            // whichbin of this octant's directions by ratio class (axis, < tan15, < tan30, < 1, diagonal), 6 bits
-            // a class in one word
-            unsigned obin = 0;
+            // whichbin of this octant's directions by ratio class: axis, < tan15, < tan30, < 1, diagonal
+#if MKF_OBIN
+            unsigned obinp = 0;   // 6 bits a class
             {
                 const double rr[5] = {0.0, 0.1, 0.4, 0.8, 1.0};
 #pragma unroll
                 for (int k = 0; k < 5; k++) {
                     const double mj = 10.0, mn = 10.0 * rr[k];
                     const double ax = (q >= 4 ? mn : mj), ay = (q >= 4 ? mj : mn);
-                    obin |= (unsigned)whichbin((q & 1) ? ax : -ax, (q <= 1 || q >= 6) ? ay : -ay) << (6 * k);
+                    obinp |= (unsigned)whichbin((q & 1) ? ax : -ax, (q <= 1 || q >= 6) ? ay : -ay) << (6 * k);
                 }
-                obin = __builtin_amdgcn_readfirstlane(obin);
+                obinp = __builtin_amdgcn_readfirstlane(obinp);
             }
-            // Octant geometry as one line per depth (octant_cell): H octants (q < 4) step the depth along x and
-            // the row index along y, V octants the other way round.  Candidate (depth, ind) is word
-            // rowbase(depth) + isgn * ind of the cell-word copy whose lines run along ind (x-major for H,
-            // y-major for V), so the 64 lanes of a chunk load consecutive words; it lies in the grid iff the
-            // depth line does and ind <= imax_oct.
-            const bool hq = q < 4;
-            const int sxs = (q & 1) ? 1 : -1, sys = (q <= 1 || q >= 6) ? 1 : -1;
-            const uint32_t* cw = hq ? P.cellw : P.cellw_t;
-            const int lstride = hq ? P.rows : P.cols;
-            const int dpos0 = hq ? cx : cy, ipos0 = hq ? cy : cx;
-            const int dsgn = hq ? sxs : sys, isgn = hq ? sys : sxs;
-            const int dlim = hq ? P.cols : P.rows, ilim = hq ? P.rows : P.cols;
-            const int imax_oct = isgn > 0 ? ilim - 1 - ipos0 : ipos0;
-            const bool axis_ok = (q == 0 || q == 1 || q == 5 || q == 6);   // ind 0 is this octant's (sieve2 :1545)
+#define OBIN(k) ((int)__builtin_amdgcn_ubfe(obinp, (unsigned)(6 * (k)), 6u))
+#else
+            int obin[5];
+            {
+                const double rr[5] = {0.0, 0.1, 0.4, 0.8, 1.0};
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    const double mj = 10.0, mn = 10.0 * rr[k];
+                    const double ax = (q >= 4 ? mn : mj), ay = (q >= 4 ? mj : mn);
+                    obin[k] = whichbin((q & 1) ? ax : -ax, (q <= 1 || q >= 6) ? ay : -ay);
+                }
+            }
+#define OBIN(k) obin[k]
+#endif
             int depth = 0;
-            // Cell words of the current depth's first two chunks (t = lane, lane + 64).  They are loaded at the top
-            // of the previous depth under its gap list, which stays the current one when that depth adds no block
-            // (wc_ok), so the loads are in flight while the previous depth runs.
-            uint32_t wc0 = 0, wc1 = 0;
-            bool wc_ok = false;
-            // Visit ranges of up to 16 gaps in registers: lane g holds gap g's exclusive candidate prefix,
-            // ind - t offset and centregap bounds; more gaps take the LDS arrays ga / gpre / gc.
-            int r_pre = 0, r_base = 0, r_clo = 0, r_chi = 0;
-            // sieve2's per-gap loops (pointdata.cpp:1518-1526) for depth d: the visited inds of gap g are
-            // [max(lo, F), min(hi, d)] with F the last ind visited in an earlier gap (firstind, inclusive).
-            // Register form (ng <= 16); cg: the centregap bounds too.
-            auto ranges_reg = [&](int d, int& pre, int& base, int& clo, int& chi, bool cg) -> int {
-                const bool gv = lane < ng;
-                double zx = 0.0, zy = 0.0;
-                if (gv) { const double2 z = L.gaps[lane]; zx = z.x; zy = z.y; }
-                const double dd = (double)d;
-                const int lo = (int)ceil(zx * (dd - 0.5) - 0.5);
-                const int hi = (int)floor(zy * (dd + 0.5) + 0.5);
-                const int b = min(hi, d);
-                int ci;
-                if (ng == 1) {   // one gap: F = 0
-                    const int a = max(lo, 0);
-                    ci = (b >= a) ? b - a + 1 : 0;
-                    pre = 0;
-                    base = a;
-                } else {
-                    const int F = row_excl_max0((gv && b >= lo) ? b : 0);
-                    const int a = max(lo, F);
-                    const int c = (gv && b >= a) ? b - a + 1 : 0;
-                    ci = row_incl_sum(c);
-                    pre = ci - c;
-                    base = a - pre;
-                }
-                if (cg) {
-                    // centregap (:1530): (double)ind >= start*depth && (double)ind <= end*depth
-                    clo = (int)ceil(zx * dd);
-                    chi = (int)floor(zy * dd);
-                }
-                return __builtin_amdgcn_readlane(ci, ng - 1);
-            };
-            // LDS form (ng > 16): 64 gaps a round, prefix scans over the wave
-            auto ranges_lds = [&](int d) -> int {
-                int carryF = 0, carryT = 0;
-                for (int base = 0; base < ng; base += 64) {
-                    const int g = base + lane;
-                    int lo = 0, b = -1;
-                    bool vis = false;
-                    if (g < ng) {
-                        const double2 z = L.gaps[g];
-                        lo = (int)ceil(z.x * (d - 0.5) - 0.5);
-                        const int hi = (int)floor(z.y * (d + 0.5) + 0.5);
-                        b = min(hi, d);
-                        vis = (b >= lo);
-                        L.gc[g] = make_int2((int)ceil(z.x * d), (int)floor(z.y * d));
-                    }
-                    const int incl = wave_incl_max(vis ? b : INT_MIN);
-                    int excl = __shfl_up(incl, 1);
-                    if (lane == 0) excl = INT_MIN;
-                    const int F = max(carryF, max(excl, 0));
-                    const int a = max(lo, F);
-                    const int c = (g < ng && b >= a) ? (b - a + 1) : 0;
-                    const int ci = wave_incl_sum(c);
-                    if (g < ng) { L.ga[g] = a; L.gpre[g] = carryT + ci - c; }
-                    carryT += __shfl(ci, 63);
-                    carryF = max(carryF, __shfl(incl, 63));
-                }
-                if (lane == 0) L.gpre[ng] = carryT;
-                wave_sync();
-                return carryT;
-            };
-            // the gap of candidate t (register form): the last gap whose prefix is <= t
-            auto gap_of = [&](int t, int pre, int base, int& off) {
-                off = __builtin_amdgcn_readlane(base, 0);
-                for (int g = 1; g < ng; g++)
-                    off = (t >= __builtin_amdgcn_readlane(pre, g)) ? __builtin_amdgcn_readlane(base, g) : off;
-            };
+            // cell word of candidate t = lane of the next depth, loaded while this depth finishes: the
+            // next depth's candidates are known before its collectgarbage, and they stay the same
+            // when that adds no block (nb == 0: the gap list is unchanged)
+            uint32_t pf_w = 0;
+            bool pf_ok = false;
+            int pf_T = 0;   // candidates of the prefetched depth (its ranges are in L.ga / gpre / gc)
             for (;;) {
                 // ---------------- collectgarbage (sparksieve2.cpp:89-132) for the previous depth
-                int nb = __builtin_amdgcn_readfirstlane(L.misc[1]);
-                if (nb > 0) wc_ok = false;   // the gap list changes: the speculative loads are stale
+                int nb = L.misc[1];
+                if (nb > 0) pf_ok = false;
                 if (nb > bcap + P.spill_cap) { failed = true; if (lane == 0) atomicOr(P.error, KERR_BLOCK_CAPACITY); }
                 if (failed) break;
-                if (nb == 1 && ng <= 64) {
-                    // One block (the common case: a wall crossing the sweep front): the merge loop of
-                    // sparksieve2.cpp:100-131 touches each gap on its own -- a gap is left alone when the block
-                    // ends before it, trimmed at either end, erased when the trim leaves <= 1e-10 of it, or split
-                    // when the block lies strictly inside -- so the lanes do all gaps at once.
-                    const double2 bk = L.blocks[0];
-                    const bool gv = lane < ng;
-                    double gx = 0.0, gy = 0.0;
-                    if (gv) { const double2 v = L.gaps[lane]; gx = v.x; gy = v.y; }
-                    const bool untouched = bk.y < gx;
-                    const double ns = (bk.x <= gx && bk.y > gx) ? bk.y : gx;
-                    const double ne = (bk.y >= gy && bk.x < gy) ? bk.x : gy;
-                    const bool create = !(bk.x <= gx) && !(bk.y >= gy);
-                    const bool erased = !untouched && ne <= ns + 1e-10;
-                    const bool split = !untouched && !erased && !(bk.y > ne) && create;
-                    const int cnt = !gv ? 0 : (erased ? 0 : (split ? 2 : 1));
-                    const int ci = wave_incl_sum_dpp(cnt);
-                    const int no = __builtin_amdgcn_readlane(ci, 63);
-                    if (no > gcap) { if (lane == 0) atomicOr(P.error, KERR_GAP_CAPACITY); failed = true; break; }
-                    const int pos = ci - cnt;
-                    if (cnt == 1) L.gaps2[pos] = make_double2(ns, ne);
-                    if (cnt == 2) { L.gaps2[pos] = make_double2(gx, bk.x); L.gaps2[pos + 1] = make_double2(bk.y, gy); }
-                    double2* tmp = L.gaps; L.gaps = L.gaps2; L.gaps2 = tmp;
-                    ng = no;
-                    if (lane == 0) L.misc[1] = 0;
-                    wave_sync();
-                } else if (nb > 0 && nb <= 64 && nb <= bcap && ng <= 64) {
+                if (nb > 0 && nb <= 64 && nb <= bcap && ng <= 64) {
                     // Register path (the common case): lane i holds block i and lane g gap g; the
                     // dedup, the ranks and the serial merge read other lanes through v_readlane
                     // (wave-uniform indices) instead of chains of dependent LDS reads.
@@ -738,7 +640,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         L.misc[0] = no;
                     }
                     __syncthreads();
-                    ng = __builtin_amdgcn_readfirstlane(L.misc[0]);
+                    ng = L.misc[0];
                     if (ng < 0) { failed = true; break; }
                     for (int i = lane; i < ng; i += 64) L.gaps[i] = L.gaps2[i];
                     if (lane == 0) L.misc[1] = 0;
@@ -750,90 +652,95 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 depth++;
                 if (COUNT) nsteps++;
                 // ---------------- sieve2 for this depth (pointdata.cpp:1512-1565)
-                const bool regs = ng <= 16;
-                const int T = regs ? ranges_reg(depth, r_pre, r_base, r_clo, r_chi, true) : ranges_lds(depth);
-                examined += (unsigned long long)T;
-                // speculative: the next depth's first two chunks under this gap list (used if this depth adds no
-                // block); the loads stay in flight while this depth runs
-                // (issued on every path, so the wait for them at the next depth can leave the newer loads
-                // outstanding)
-                int a0 = 0, a1 = 0;
-                if (regs) {
-                    int npre, nbase, u0, u1;
-                    const int Tn = ranges_reg(depth + 1, npre, nbase, u0, u1, false);
-                    const int dp1 = dpos0 + dsgn * (depth + 1);
-                    const int im1 = (dp1 >= 0 && dp1 < dlim) ? imax_oct : -1;
-                    const int rb1 = dp1 * lstride + ipos0;
-                    int o0, o1;
-                    gap_of(lane, npre, nbase, o0);
-                    gap_of(lane + 64, npre, nbase, o1);
-                    const int i0 = o0 + lane, i1 = o1 + lane + 64;
-                    a0 = (lane < Tn && i0 <= im1) ? rb1 + isgn * i0 : 0;
-                    a1 = (lane + 64 < Tn && i1 <= im1) ? rb1 + isgn * i1 : 0;
+                // per-gap visit ranges with the monotone firstind rule
+                int carryF = 0, carryT = 0;
+                if (ng <= 8 && pf_ok) {
+                    // the previous depth's prefetch already laid out this depth's ranges (same gap list)
+                    carryT = pf_T;
+                } else if (ng <= 8) {
+                    // few gaps (the common case): a wave-uniform loop over the gaps in order -- no
+                    // cross-lane scans.  F = the largest b of the earlier visited gaps (at least 0).
+                    int F = 0, T = 0;
+                    for (int g = 0; g < ng; g++) {
+                        const double2 z = L.gaps[g];
+                        const int lo = (int)ceil(z.x * (depth - 0.5) - 0.5);
+                        const int hi = (int)floor(z.y * (depth + 0.5) + 0.5);
+                        const int b = min(hi, depth);
+                        const int a = max(lo, F);
+                        const int c = (b >= a) ? (b - a + 1) : 0;
+                        if (lane == 0) {
+                            L.ga[g] = a;
+                            L.gpre[g] = T;
+                            L.gc[g] = make_int2((int)ceil(z.x * depth), (int)floor(z.y * depth));
+                        }
+                        T += c;
+                        if (b >= lo) F = max(F, b);
+                    }
+                    carryT = T;
                 }
-                const uint32_t wn0 = cw[a0], wn1 = cw[a1];
-                // this depth's words (loaded one depth ago) are complete once at most these two are outstanding:
-                // an explicit vmcnt(2) (the compiler's own wait at the first use drains every load in flight)
-                __builtin_amdgcn_s_waitcnt(0x0F72);   // vmcnt(2) expcnt(7) lgkmcnt(15)
-                const uint32_t w0 = wc0, w1 = wc1;
+                for (int base = 0; base < ng && ng > 8; base += 64) {
+                    int g = base + lane;
+                    int lo = 0, b = -1;
+                    bool vis = false;
+                    if (g < ng) {
+                        double2 z = L.gaps[g];
+                        lo = (int)ceil(z.x * (depth - 0.5) - 0.5);
+                        int hi = (int)floor(z.y * (depth + 0.5) + 0.5);
+                        b = min(hi, depth);
+                        vis = (b >= lo);
+                        L.gc[g] = make_int2((int)ceil(z.x * depth), (int)floor(z.y * depth));
+                    }
+                    int bp = vis ? b : INT_MIN;
+                    int incl = wave_incl_max(bp);
+                    int excl = __shfl_up(incl, 1);
+                    if (lane == 0) excl = INT_MIN;
+                    int F = max(carryF, max(excl, 0));
+                    int a = max(lo, F);
+                    int c = (g < ng && b >= a) ? (b - a + 1) : 0;
+                    int ci = wave_incl_sum(c);
+                    if (g < ng) { L.ga[g] = a; L.gpre[g] = carryT + ci - c; }
+                    carryT += __shfl(ci, 63);
+                    carryF = max(carryF, __shfl(incl, 63));
+                }
+                if (lane == 0) L.gpre[ng] = carryT;
+                wave_sync();
+                const int T = carryT;
+                examined += (unsigned long long)T;
                 MK_T(1);
-                const int dp = dpos0 + dsgn * depth;
-                const int imax = (dp >= 0 && dp < dlim) ? imax_oct : -1;
-                const int rowbase = dp * lstride + ipos0;
-                const unsigned d2 = (unsigned)depth * (unsigned)depth;
-                const float fd = (float)depth, mg = 1e-6f * fd, c15 = 0.267949192f * fd, c30 = 0.577350269f * fd;
-                // the first gap's values (uniform); further gaps through gap_of
-                const int b0 = regs ? __builtin_amdgcn_readlane(r_base, 0) : 0;
-                const int clo0 = regs ? __builtin_amdgcn_readlane(r_clo, 0) : 0;
-                const int chi0 = regs ? __builtin_amdgcn_readlane(r_chi, 0) : 0;
                 bool hasgaps = false;
-                int gcur = 0; // per-lane gap pointer of the LDS ranges (t increases monotonically)
+                int gcur = 0; // per-lane gap pointer (t increases monotonically)
                 for (int t0 = 0; t0 < T; t0 += 64) {
                     if (COUNT) nchunks++;
-                    const int t = t0 + lane;
-                    const bool valid = t < T;
-                    int ind, clo, chi;
-                    if (regs) {
-                        ind = b0 + t; clo = clo0; chi = chi0;
-                        for (int g = 1; g < ng; g++) {
-                            const bool s = t >= __builtin_amdgcn_readlane(r_pre, g);
-                            ind = s ? __builtin_amdgcn_readlane(r_base, g) + t : ind;
-                            clo = s ? __builtin_amdgcn_readlane(r_clo, g) : clo;
-                            chi = s ? __builtin_amdgcn_readlane(r_chi, g) : chi;
-                        }
-                    } else {
-                        ind = 0; clo = 0; chi = -1;
-                        if (valid) {
-                            while (L.gpre[gcur + 1] <= t) gcur++;
-                            ind = L.ga[gcur] + (t - L.gpre[gcur]);
-                            const int2 gcr = L.gc[gcur];
-                            clo = gcr.x; chi = gcr.y;
-                        }
+                    int t = t0 + lane;
+                    bool valid = t < T;
+                    int ind = 0, hx = 0, hy = 0;
+                    int2 gcr = make_int2(0, -1);
+                    bool ingrid = false, add = false;
+                    uint32_t w = 0;
+                    if (valid) {
+                        while (L.gpre[gcur + 1] <= t) gcur++;
+                        ind = L.ga[gcur] + (t - L.gpre[gcur]);
+                        gcr = L.gc[gcur];
+                        octant_cell(q, cx, cy, depth, ind, hx, hy);
+                        ingrid = (hx >= 0 && hx < P.cols && hy >= 0 && hy < P.rows);
                     }
-                    const bool ingrid = valid && ind <= imax;
-                    uint32_t w;
-                    if (wc_ok && t0 < 128) {
-                        w = (t0 == 0) ? w0 : w1;
-                    } else {
-                        w = cw[ingrid ? rowbase + isgn * ind : 0];
-                        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) here, so the prefetched path needs none
-                    }
-                    w = ingrid ? w : 0u;
-                    const int nl = cell_nseg(w);
-                    // candidate for the addlist (:1530-1547): centregap, FILLED, and the octant owns the axis /
-                    // diagonal cell
-                    const bool cand = ingrid & (ind >= clo) & (ind <= chi) & cell_filled(w) & ((ind != 0) | axis_ok) &
-                                      ((ind != depth) | hq);
-                    bool blocked = false;
-                    const bool slow = ingrid & ((nl > 0) | (hasmax & cand));
-                    if (ballot(slow) != 0ull) {
-                        if (slow) {
-                            int hx, hy;
-                            octant_cell(q, cx, cy, depth, ind, hx, hy);
-                            const int off = cell_seg_off(w);
-                            if (cand) {
-                                // sparkSieve2::testblock (sparksieve2.cpp:45-63)
-                                const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
+                    if (ingrid) {
+                        const int hc = hx * P.rows + hy;
+#if MKF_YMAJ
+                        w = (pf_ok && t0 == 0) ? pf_w : (q < 4 ? P.cellw[hc] : P.cellw_t[hy * P.cols + hx]);
+#else
+                        w = (pf_ok && t0 == 0) ? pf_w : P.cellw[hc];
+#endif
+                        const int nl = cell_nseg(w), off = cell_seg_off(w);
+                        // (double)ind >= start*depth && (double)ind <= end*depth, on the integer
+                        // bounds of the two FP64 products (computed once per gap and depth)
+                        const bool centregap = ind >= gcr.x && ind <= gcr.y;
+                        if (centregap && cell_filled(w) &&
+                            (ind != 0 || q == 0 || q == 1 || q == 5 || q == 6) && (ind != depth || q < 4)) {
+                            // sparkSieve2::testblock (sparksieve2.cpp:45-63)
+                            const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
+                            bool blocked = false;
+                            if (hasmax || nl > 0) {
                                 Seg ray = make_seg(Vec2{c0x, c0y}, Vec2{px, py});
                                 if (hasmax && ray.length() > P.maxdist) blocked = true;
                                 const double tol = sp * 1e-10;
@@ -843,122 +750,191 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                                     if (rects_touch(ray.r, s.r, tol) && segs_cross(ray, s, tol)) blocked = true;
                                 }
                             }
-                            // sparkSieve2::block for every in-grid candidate (sparksieve2.cpp:67-87)
-                            for (int k = 0; k < nl; k++) {
-                                const double* sg = P.segs + 4 * (size_t)(off + k);
-                                double ta = tanify(c0x, c0y, sg[0], sg[1], q), tb = tanify(c0x, c0y, sg[2], sg[3], q);
-                                const int slot = atomicAdd(&L.misc[1], 1);
-                                put_block(slot, (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10));
-                            }
+                            add = !blocked;
+                        }
+                        // sparkSieve2::block for every in-grid candidate (sparksieve2.cpp:67-87)
+                        for (int k = 0; k < nl; k++) {
+                            const double* sg = P.segs + 4 * (size_t)(off + k);
+                            double ta = tanify(c0x, c0y, sg[0], sg[1], q), tb = tanify(c0x, c0y, sg[2], sg[3], q);
+                            const int slot = atomicAdd(&L.misc[1], 1);
+                            put_block(slot, (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10));
                         }
                     }
-                    const bool add = cand & !blocked;
                     hasgaps |= (ballot(ingrid) != 0ull);
                     MK_T(2);
                     // ---- visible cells: bins, moments (reference order), run tracking
-                    const unsigned long long am = ballot(add);
+                    unsigned long long am = ballot(add);
                     if (am) {
+                        int bin = -1;
+                        double this_dist = 0.0;
                         // whichbin(depixelate(c) - centre) (pointdata.h:432-520) decided on the exact ratio
                         // ind/depth: 0 and 1 are the axis / diagonal; tan15 and tan30 are irrational, so a float
                         // test with a 1e-6 margin decides every cell the reference's FP64 ratio (error ~1e-15)
                         // decides; cells inside the margin take the FP64 path
-                        const float fi = (float)ind;
-                        const float e15 = fi - c15, e30 = fi - c30;
-                        int k = 1 + (e15 >= 0.0f) + (e30 >= 0.0f);
-                        k = (ind == depth) ? 4 : k;
-                        k = (ind == 0) ? 0 : k;
-                        int bin = (int)__builtin_amdgcn_ubfe(obin, (unsigned)(6 * k), 6u);
-                        const bool amb = add & (ind != 0) & (ind != depth) & ((fabsf(e15) < mg) | (fabsf(e30) < mg));
-                        if (ballot(amb) != 0ull) {
-                            if (amb) {
-                                int hx, hy;
-                                octant_cell(q, cx, cy, depth, ind, hx, hy);
+#if MKF_CLASS
+                        {
+                            const float fd = (float)depth, fi = (float)ind, mg = 1e-6f * fd;
+                            const float e15 = fi - 0.267949192f * fd, e30 = fi - 0.577350269f * fd;
+                            int k = 1 + (e15 >= 0.0f) + (e30 >= 0.0f);
+                            k = (ind == depth) ? 4 : k;
+                            k = (ind == 0) ? 0 : k;
+                            bin = OBIN(k);
+                            const bool amb = add & (ind != 0) & (ind != depth) & ((fabsf(e15) < mg) | (fabsf(e30) < mg));
+                            if (ballot(amb) != 0ull) {
+                                if (amb) {
+                                    const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
+                                    bin = whichbin(px - c0x, py - c0y);
+                                }
+                            }
+                        }
+#else
+                        if (add) {
+                            int k;
+                            if (ind == 0) k = 0;
+                            else if (ind == depth) k = 4;
+                            else {
+                                const float fd = (float)depth, fi = (float)ind, mg = 1e-6f * fd;
+                                const float e15 = fi - 0.267949192f * fd, e30 = fi - 0.577350269f * fd;
+                                k = (fabsf(e15) < mg || fabsf(e30) < mg) ? -1 : 1 + (e15 >= 0.0f) + (e30 >= 0.0f);
+                            }
+                            if (k >= 0) {
+                                bin = OBIN(k);
+                            } else {
                                 const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
                                 bin = whichbin(px - c0x, py - c0y);
                             }
                         }
-                        const unsigned n = d2 + __umul24((unsigned)ind, (unsigned)ind);   // dx^2 + dy^2 (exact)
-                        // per bin: the count, and the far distance (:1489) as the float of the largest
-                        // dx^2 + dy^2 (the dists grow with it, and (float) rounding keeps the order).  A chunk's
-                        // lanes are in ind order, so a bin's last lane holds its largest dx^2 + dy^2.
-#pragma unroll
-                        for (int kk = 0; kk < 5; kk++) {
-                            const unsigned long long mk = ballot(add & (bin == (int)((obin >> (6 * kk)) & 63u)));
-                            if (mk) {   // one lane per bin: no same-address LDS atomics across the lanes
-                                const unsigned nf = (unsigned)__builtin_amdgcn_readlane((int)n, 63 - __clzll((long long)mk));
-                                if (lane == 0) {
-                                    const int b = (int)((obin >> (6 * kk)) & 63u);
-                                    atomicAdd(&L.binc[b], (unsigned)__popcll(mk));
-                                    atomicMax(&L.bfar[b], nf);
-                                }
-                            }
+#endif
+#if MKF_MOM
+                        // dx^2 + dy^2 (exact): the far distance (:1489) is the float of the bin's largest one (the
+                        // dists grow with it, and (float) rounding keeps the order)
+                        const unsigned n2 = (unsigned)(depth * depth) + __umul24((unsigned)ind, (unsigned)ind);
+                        if (add) {
+                            atomicAdd(&L.binc[bin], 1u);
+                            atomicMax(&L.bfar[bin], n2);
                         }
+#else
+                        if (add) {
+                            const double dx = (double)(hx - cx), dy = (double)(hy - cy);
+                            this_dist = sqrt(dx * dx + dy * dy) * sp;
+                            atomicAdd(&L.binc[bin], 1u);
+                            atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
+                        }
+#endif
                         MK_T(3);
                         if (exact) {
-                            // serial sums in lane order = reference addlist order (pointdata.cpp:1490-1495)
+                            // serial sums in lane order = reference addlist order
                             // (the lane index is wave-uniform: v_readlane into SGPRs keeps the serial
                             // chain on two dependent FP64 adds per cell instead of an LDS round trip)
+#if MKF_MOM
+                            if (add) this_dist = sqrt((double)n2) * sp;   // sqrt(dx*dx + dy*dy) * spacing
+#endif
+                            const int d_lo = __double2loint(this_dist), d_hi = __double2hiint(this_dist);
                             unsigned long long mm = am;
                             while (mm) {
                                 const int l = __ffsll((long long)mm) - 1;
-                                const double v = sqrt((double)__builtin_amdgcn_readlane((int)n, l)) * sp;
+                                const double v = __hiloint2double(__builtin_amdgcn_readlane(d_hi, l),
+                                                                  __builtin_amdgcn_readlane(d_lo, l));
                                 tsum += v;
                                 tsum2 += v * v;
                                 mm &= mm - 1;
                             }
-                        } else {
-                            const double r = MK_SQRT((double)max(n, 1u));
-                            s1 += add ? r : 0.0;
-                            s2n += add ? n : 0u;
-                            mcnt += add ? 1 : 0;
+                        } else if (add) {
+#if MKF_MOM
+                            s1 += sqrt_nr((double)n2);
+                            s2n += n2;
+#else
+                            s1 += this_dist;
+                            s2 += this_dist * this_dist;
+#endif
+                            mcnt++;
                         }
                         MK_T(4);
                         nsize += __popcll(am);
-                        // run tracking (the diagonal cell of an H octant is a single span, ngraph.cpp:243-258)
-                        const bool dg = (ind == depth) & hq;
-                        const int slot = (ind == 0) ? 3 : bin - q_sector;
-                        binerr |= add & (dg ? (bin != q_diag) : ((ind == 0) ? (bin != q_axis) : ((slot < 0) | (slot > 2))));
+                        // run tracking
                         bool emit = false;
                         unsigned long long rec = 0;
-                        if (add & !dg) {
-                            const int sl = slot & 3;
-                            uint32_t o = ld_open(ind);
-                            int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
-                            const bool ext = (o & 1u) && oslot == sl && ol == depth - 1;
-                            emit = (o & 1u) && !ext;   // the rank within (slot, row) is set after the octant
-                            rec = pack_emit(oslot, ind, os, ol, 0);
-                            st_open(ind, pack_open(sl, ext ? os : depth, depth));
+                        if (add) {
+                            if (ind == depth && q < 4) { // diagonal bin: single span (ngraph.cpp:243-258)
+                                if (bin != q_diag) atomicOr(P.error, KERR_BIN_MISMATCH);
+                            } else {
+                                int slot;
+                                if (ind == 0) { slot = 3; if (bin != q_axis) atomicOr(P.error, KERR_BIN_MISMATCH); }
+                                else { slot = bin - q_sector; if (slot < 0 || slot > 2) { atomicOr(P.error, KERR_BIN_MISMATCH); slot = 0; } }
+                                uint32_t o = ld_open(ind);
+                                int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
+                                if ((o & 1u) && oslot == slot && ol == depth - 1) {
+                                    st_open(ind, pack_open(slot, os, depth));
+                                } else {
+                                    if (o & 1u) {   // the rank within (slot, row) is set after the octant
+                                        emit = true;
+                                        rec = pack_emit(oslot, ind, os, ol, 0);
+                                    }
+                                    st_open(ind, pack_open(slot, depth, depth));
+                                }
+                            }
                         }
                         // the diagonal cell (at most one per depth) -- wave-uniform bookkeeping
-                        unsigned long long dm = ballot(add & dg);
+                        unsigned long long dm = ballot(add && ind == depth && q < 4);
                         if (dm) {
                             if (diag_n == 0) diag_min = depth;
                             diag_max = depth;
                             diag_n++;
                         }
-                        const unsigned long long em = ballot(emit);
+                        unsigned long long em = ballot(emit);
                         if (em) {
-                            const int ne = __popcll(em);
-                            if (nA - nAf + ne > MK_EB) flush_emit();
-                            if (emit) L.emit[nA - nAf + prefix_popc(em)] = rec;
-                            nA += ne;
+                            int pos = nA + prefix_popc(em);
+                            if (emit) {
+                                if (pos < P.capA) stA[pos] = rec;
+                            }
+                            nA += __popcll(em);
                         }
                     }
                     MK_T(5);
                 }
-                if (nA > capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
+                if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
                 if (!hasgaps) break;      // sieve2 returned false (pointdata.cpp:1458)
                 dq = depth;
-                wc0 = wn0;
-                wc1 = wn1;
-                wc_ok = regs;   // cleared at the loop top if this depth added a block
+                // prefetch: candidate t = lane of depth + 1 under the current gap list (few-gap case)
+                pf_ok = false;
+                if (ng <= 8 && !failed) {
+                    const int d1 = depth + 1;
+                    int F1 = 0, T1 = 0, pind = -1;
+                    for (int g = 0; g < ng; g++) {
+                        const double2 z = L.gaps[g];
+                        const int lo = (int)ceil(z.x * (d1 - 0.5) - 0.5);
+                        const int hi = (int)floor(z.y * (d1 + 0.5) + 0.5);
+                        const int b = min(hi, d1);
+                        const int a = max(lo, F1);
+                        const int c = (b >= a) ? (b - a + 1) : 0;
+                        if (lane >= T1 && lane < T1 + c) pind = a + (lane - T1);
+                        if (lane == 0) {   // depth d1's visit ranges, reused if no block changes the gaps
+                            L.ga[g] = a;
+                            L.gpre[g] = T1;
+                            L.gc[g] = make_int2((int)ceil(z.x * d1), (int)floor(z.y * d1));
+                        }
+                        T1 += c;
+                        if (b >= lo) F1 = max(F1, b);
+                    }
+                    pf_T = T1;
+                    if (pind >= 0) {
+                        int px, py;
+                        octant_cell(q, cx, cy, d1, pind, px, py);
+#if MKF_YMAJ
+                        if (px >= 0 && px < P.cols && py >= 0 && py < P.rows)
+                            pf_w = q < 4 ? P.cellw[px * P.rows + py] : P.cellw_t[py * P.cols + px];
+#else
+                        if (px >= 0 && px < P.cols && py >= 0 && py < P.rows) pf_w = P.cellw[px * P.rows + py];
+#endif
+                    }
+                    pf_ok = true;
+                }
                 // rows past MK_OPEN_LDS live in scratch memory: order this depth's stores before the next
                 // depth's loads of the same rows (other lanes); only sight lines past 1024 cells get here
                 if (depth >= MK_OPEN_LDS) __syncthreads();
                 wave_sync();
             }
             if (failed) break;
-            flush_emit();
             // ---------------- flush open rows, then place this octant's runs canonically
             __syncthreads();
             for (int base = 0; base <= dq; base += 64) {
@@ -977,11 +953,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 unsigned long long em = ballot(emit);
                 if (em) {
                     int pos = nA + prefix_popc(em);
-                    if (emit && pos < capA) stA[pos] = rec;
+                    if (emit && pos < P.capA) stA[pos] = rec;
                     nA += __popcll(em);
                 }
             }
-            if (nA > capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); break; }
+            if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); break; }
             __syncthreads();
             // ranks within (slot, row): the runs of one row and slot are staged in depth order, so a
             // record's rank is the number of earlier records with its key (earlier chunks: the running
@@ -1095,7 +1071,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             MK_T(6);
         }
         float m1f = 0.0f, m2f = 0.0f;
-        if (ballot(binerr) != 0ull) { if (lane == 0) atomicOr(P.error, KERR_BIN_MISMATCH); }
         if (!failed) {
             if (exact) {
                 m1f = (float)tsum;
@@ -1104,32 +1079,32 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 int mmax = mcnt;
                 for (int off = 32; off >= 1; off >>= 1) {
                     s1 += __shfl_xor(s1, off);
+                    s2 += __shfl_xor(s2, off);
                     s2n += __shfl_xor(s2n, off);
                     mmax = max(mmax, __shfl_xor(mmax, off));
                 }
                 // lanes reduce in different orders: take lane 0's sums
-                s1 = __shfl(s1, 0);
-                const double S1 = s1 * sp;
-                const double S2 = (double)s2n * (sp * sp);
-                // The reference's serial chains (pointdata.cpp:1490-1495) are within gamma_(n-1) of the exact
-                // sums of their terms, and those terms within 2u (dist) and 5u (dist^2) of sp*sqrt(n_i) and
-                // sp^2*n_i.  Ours: the lanes' sums of approximate square roots (each within sqrt_err) reduced by
-                // a 6-level butterfly (gamma_(m+6)) times sp; the exact integer sum times sp^2 (3u).  E bounds
-                // |ours - reference| with a factor 2 to spare; when every double within E of ours rounds to one
-                // float, that float is the reference's.
+                s1 = __shfl(s1, 0); s2 = __shfl(s2, 0);
+#if MKF_MOM
+                // The reference's serial chains (pointdata.cpp:1490-1495) are within gamma_(n-1) of the exact sums
+                // of their terms, and those within 2u (dist) and 5u (dist^2) of sp*sqrt(n_i) and sp^2*n_i.  Ours:
+                // the lanes' sums of approximate roots (each within sqrt_err) reduced by a 6-level butterfly
+                // (gamma_(m+6)) times sp; the exact integer sum times sp^2 (3u).  E bounds |ours - reference| with
+                // a factor 2 to spare.
+                const double S1 = s1 * sp, S2 = (double)s2n * (sp * sp);
                 const double u = 0x1p-53;
                 const double g1 = (double)nsize * u / (1.0 - (double)nsize * u);
                 const double g2 = (double)(mmax + 7) * u / (1.0 - (double)(mmax + 7) * u);
-                const double E1 = 2.0 * (g1 + g2 + P.sqrt_err) * S1 + S1 * 0x1p-49;
-                const double E2 = 2.0 * g1 * S2 + S2 * 0x1p-48;
-                const bool ok1 = certified_float(S1, E1, &m1f);
-                const bool ok2 = certified_float(S2, E2, &m2f);
-                if (!(ok1 && ok2)) { failed = true; certfail = true; }   // re-run with the serial chains
+                const bool ok1 = certified_float_e(S1, 2.0 * (g1 + g2 + P.sqrt_err) * S1 + S1 * 0x1p-49, &m1f);
+                const bool ok2 = certified_float_e(S2, 2.0 * g1 * S2 + S2 * 0x1p-48, &m2f);
+#else
+                const bool ok1 = certified_float_sum(s1, nsize, mmax, &m1f);
+                const bool ok2 = certified_float_sum(s2, nsize, mmax, &m2f);
+#endif
+                if (!(ok1 && ok2)) { failed = true; certfail = true; }
             }
         }
         if (failed) {
-            // the failure list tags capacity failures (MK_CAPACITY_TAG); the host strips nothing: node_list
-            // entries are masked on read
             if (lane == 0) P.fail_list[atomicAdd(P.fail_count, 1)] = node | (certfail ? 0 : MK_CAPACITY_TAG);
             // leave the wave in a clean LDS state and drop this source
             for (int i = lane; i < D + 4; i += 64) st_open(i, 0u);
@@ -1171,8 +1146,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         if (lane < 32) {
             P.bin_nruns[k * 32 + lane] = L.bnr[lane];
             P.bin_count[k * 32 + lane] = (uint16_t)L.binc[lane];
+#if MKF_MOM
             const unsigned nf = L.bfar[lane];
             P.bin_dist[k * 32 + lane] = nf ? (float)(sqrt((double)nf) * sp) : 0.0f;
+#else
+            P.bin_dist[k * 32 + lane] = __uint_as_float(L.bfar[lane]);
+#endif
         }
         if (lane == 0) {
             atomicAdd(&P.stats[0], examined);

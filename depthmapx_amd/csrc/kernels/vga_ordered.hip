@@ -130,7 +130,7 @@ __device__ __forceinline__ void ord_extract(const OrderedParams& P, int64_t k, i
 }
 
 __global__ void __launch_bounds__(ORD_NT) vga_ordered_kernel(const OrderedParams* __restrict__ PP) {
-    OrderedParams P = *PP;   // this workgroup's scratch: misc [C], ext [C][2], vec [2][N] per workgroup
+    OrderedParams P = const_params(PP);   // this workgroup's scratch: misc [C], ext [C][2], vec [2][N] per workgroup
     P.misc += (size_t)blockIdx.x * P.C;
     P.ext += (size_t)blockIdx.x * 2 * P.C;
     P.vec += (size_t)blockIdx.x * 2 * P.N;

@@ -156,3 +156,44 @@ def test_vga_source_list_above_1024_matches_full_run(ctx):
     a = got[100:164].astype(np.float64)
     np.testing.assert_array_equal(a[:, 5], ref[:, 5])
     assert (np.abs(a - ref) <= 1e-6 * np.maximum(1.0, np.abs(ref))).all()
+
+
+def test_long_grid_falls_back_and_matches_oracle(ctx):
+    """A strip 6001 x 13 cells: its long side is past the tile BFS's tile-common-run pass (the LDS holds
+    32 B per cell of the longest side, ~4,800 cells), a capacity of the tile path -- VGA global, its
+    source-list entry and visual step depth fall back to the direction-optimising / top-down searches
+    instead of failing, and match the restatement over the same graph."""
+    import torch
+    from pyoracle import OracleMap
+    W, H = 6000.0, 12.0
+    rng = np.random.default_rng(11)
+    walls = [[0, 0, W, 0], [W, 0, W, H], [W, H, 0, H], [0, H, 0, 0]]
+    xs = rng.uniform(50.0, W - 50.0, size=12)
+    walls += [[x, 0.0, x, 7.5] if i % 2 else [x + 3.0, 4.5, x + 3.0, H] for i, x in enumerate(xs)]
+    lines = np.array(walls, dtype=np.float64)
+    region = [0.0, 0.0, W, H]
+    pm = dmx.PointMap(region, lines, 1.0)
+    assert pm.make_points(0.5, 0.5)
+    g = pm.make_graph(ctx)
+    N = g.info()["nnodes"]
+    assert max(pm.cols, pm.rows) > 4800
+    om = OracleMap(region, 1.0, lines)
+    assert om.fill(0.5, 0.5)
+    full = g.copy(runs=True)
+    om.set_graph_view(full["bins"], full["runs"])
+    b, e = N // 2, N // 2 + 256
+    got = g.vga_visual_global(src_begin=b, src_end=e)[b:e].astype(np.float64)
+    assert ctx.last_stats()["vga_kernel"] != "tile-resolved"
+    src = np.arange(b, e, 16, dtype=np.int64)
+    ref, _ = om.vga_global_sample(src, threads=16)
+    want = ref[src].astype(np.float64)
+    mine = got[src - b]
+    np.testing.assert_array_equal(mine[:, 5], want[:, 5])
+    assert (np.abs(mine - want) <= 1e-6 * np.maximum(1.0, np.abs(want))).all()
+    out = torch.full((N, 7), -1.0, dtype=torch.float32, device="cuda")
+    g.vga_visual_global_device_list(out.data_ptr(), src)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy()[src].view(np.uint32), got[src - b].astype(np.float32).view(np.uint32))
+    cell = int(np.nonzero(pm.state() & 2)[0][N // 3])
+    v = g.visual_step_depth(cells=[cell])
+    np.testing.assert_array_equal(v.view(np.uint32), om.visual_stepdepth([cell]).view(np.uint32))
