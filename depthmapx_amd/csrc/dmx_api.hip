@@ -216,7 +216,6 @@ struct dmx_pointmap {
     int64_t nnodes = 0;
     std::vector<int32_t> node_cell;
     DevBuf<uint32_t> d_cellw;
-    DevBuf<uint32_t> d_cellw_t;   // the same words y-major (makeGraph's V octants)
     DevBuf<double> d_segs;
     DevBuf<int32_t> d_node_cell;
     DevBuf<int32_t> d_cell_node;
@@ -342,7 +341,7 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     if (pm->uploaded_version == pm->version && pm->uploaded_for == ctx->device) return DMX_OK;
     if (pm->uploaded_for >= 0 && pm->uploaded_for != ctx->device) {
         // another device's copies: release them (DevBuf::alloc would otherwise reuse the pointers)
-        pm->d_cellw.reset(); pm->d_cellw_t.reset(); pm->d_segs.reset(); pm->d_node_cell.reset(); pm->d_cell_node.reset();
+        pm->d_cellw.reset(); pm->d_segs.reset(); pm->d_node_cell.reset(); pm->d_cell_node.reset();
         pm->d_node_flags.reset(); pm->d_seed_tiles.reset(); pm->d_nonexp_tiles.reset();
         pm->uploaded_for = -1;
     }
@@ -378,7 +377,6 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
         }
     HIPCHK(hipSetDevice(ctx->device));
     HIPCHK(pm->d_cellw.alloc(C));
-    HIPCHK(pm->d_cellw_t.alloc(C));
     HIPCHK(pm->d_segs.alloc(std::max<size_t>(h.segs().size(), 4)));
     HIPCHK(pm->d_node_cell.alloc(std::max<int64_t>(pm->nnodes, 1)));
     HIPCHK(pm->d_cell_node.alloc(C));
@@ -387,14 +385,6 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     HIPCHK(pm->d_nonexp_tiles.alloc(nonexp.size()));
     HIPCHK(hipMemcpyAsync(pm->d_nonexp_tiles.p, nonexp.data(), nonexp.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(pm->d_cellw.p, cellw.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
-    {
-        std::vector<uint32_t> cellw_t((size_t)C);
-        const int cols = h.cols(), rows = h.rows();
-        for (int x = 0; x < cols; x++)
-            for (int y = 0; y < rows; y++) cellw_t[(size_t)y * cols + x] = cellw[(size_t)x * rows + y];
-        HIPCHK(hipMemcpyAsync(pm->d_cellw_t.p, cellw_t.data(), C * 4, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));   // (cellw_t is freed on return)
-    }
     if (!h.segs().empty())
         HIPCHK(hipMemcpyAsync(pm->d_segs.p, h.segs().data(), h.segs().size() * 8, hipMemcpyHostToDevice, ctx->stream));
     if (pm->nnodes) {
@@ -1099,7 +1089,7 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
             P.cols = h.cols(); P.rows = h.rows();
             P.spacing = h.spacing(); P.blx = h.bottom_left().x; P.bly = h.bottom_left().y;
             P.maxdist = maxdist;
-            P.cellw = pm->d_cellw.p; P.cellw_t = pm->d_cellw_t.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
+            P.cellw = pm->d_cellw.p; P.segs = pm->d_segs.p; P.node_cell = pm->d_node_cell.p;
             P.sqrt_err = sqrt_err;
             P.node_begin = node_begin; P.node_end = node_end;
             P.work_counter = ctx->counters.p + 0;
@@ -1200,15 +1190,18 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
         unsigned long long used = 0;
         std::memcpy(&used, &hc[2], 8);
-        unsigned long long st[16];
+        unsigned long long st[22];
         HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
         if (verbose()) {
             double tot = 0;
-            for (int i = 8; i < 16; i++) tot += (double)st[i];
+            for (int i = 8; i < 18; i++) tot += (double)st[i];
             VLOG("makegraph phases (wave clocks): garbage %.1f%%, ranges %.1f%%, candidates %.1f%%, bins %.1f%%, "
-                 "moments %.1f%%, run tracking %.1f%%, placement %.1f%%, publish %.1f%% (%.3g total)\n", 100 * st[8] / tot,
+                 "moments %.1f%%, run tracking %.1f%%, placement %.1f%%, publish %.1f%%, depth tail %.1f%%, "
+                 "octant setup %.1f%% (%.3g total; %llu depth steps, %llu chunks, %llu candidates)\n", 100 * st[8] / tot,
                  100 * st[9] / tot, 100 * st[10] / tot, 100 * st[11] / tot, 100 * st[12] / tot, 100 * st[13] / tot,
-                 100 * st[14] / tot, 100 * st[15] / tot, tot);
+                 100 * st[14] / tot, 100 * st[15] / tot, 100 * st[16] / tot, 100 * st[17] / tot, tot, st[2], st[3], st[0]);
+            VLOG("makegraph merges: %llu (%llu with one block), %.2f blocks and %.2f gaps a merge\n", st[18], st[19],
+                 st[18] ? (double)st[20] / st[18] : 0.0, st[18] ? (double)st[21] / st[18] : 0.0);
         }
         ctx->last_stats[0] = (long long)st[0];
         ctx->last_stats[1] = (long long)st[1];

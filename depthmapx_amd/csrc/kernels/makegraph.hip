@@ -23,19 +23,6 @@
 
 namespace dmx {
 
-// A/B flags of this round (scripts/build_ab.sh -DMKF_...=0/1)
-#ifndef MKF_OBIN
-#define MKF_OBIN 1   // the octant's 5 class bins packed in one word (bit-field extract, no per-class registers)
-#endif
-#ifndef MKF_CLASS
-#define MKF_CLASS 1  // ratio class without short-circuit branches; the FP64 whichbin only behind a wave vote
-#endif
-#ifndef MKF_MOM
-#define MKF_MOM 1    // moments and far distances from dx^2 + dy^2 (sqrt_nr, exact integer second moment)
-#endif
-#ifndef MKF_YMAJ
-#define MKF_YMAJ 0   // V octants read the y-major copy of the cell words (a chunk's lanes load consecutive words)
-#endif
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
 // open-run state of rows 0 .. MK_OPEN_LDS-1 lives in LDS, of farther rows (grids above ~1020 cells a
 // side) in per-wave scratch memory: rows past 1024 are reached only by sight lines longer than 1024
@@ -48,7 +35,6 @@ struct MakeGraphParams {
     double spacing, blx, bly;
     double maxdist;
     const uint32_t* cellw;     // [C] packed cell word (common.hpp)
-    const uint32_t* cellw_t;
     double sqrt_err;
     const double* segs;        // [S][4] cropped segment start/end
     const int32_t* node_cell;  // [N] node -> x-major cell index
@@ -282,7 +268,7 @@ __device__ __forceinline__ bool certified_float_e(double S, double E, float* out
     return a == b;
 }
 
-// Square roots of the moment sums (MKF_MOM): v_rsq_f64 (~2^-23 relative) and one Newton step (5 FP64
+// Square roots of the moment sums: v_rsq_f64 (~2^-23 relative) and one Newton step (5 FP64
 // instructions; the error, ~2^-44, is measured exhaustively over the integers the kernel feeds it by
 // sqrt_err_kernel and bounds the certificate) instead of the correctly rounded expansion (~17 instructions).
 __device__ __forceinline__ double sqrt_nr(double x) {   // x >= 1
@@ -395,9 +381,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     };
     for (int i = lane; i < min(D + 4, MK_OPEN_LDS); i += 64) L.openr[i] = 0;
     __syncthreads();
-    // 0 depth-0 + collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible: bins,
-    // 4 visible: serial moments, 5 visible: run tracking, 6 octant flush + placement, 7 publish
-    unsigned long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // 0 collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible: bins, 4 visible: serial
+    // moments, 5 visible: run tracking, 6 octant flush + placement, 7 publish, 8 depth tail (next depth's
+    // prefetch), 9 octant setup + depth 0
+    unsigned long long cyc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long mst[4] = {0, 0, 0, 0};   // PROF: merges, one-block merges, blocks, gaps at merges
     unsigned long long tmark = PROF ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
@@ -420,7 +408,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
 
         double tsum = 0.0, tsum2 = 0.0; // wave-uniform, reference order (exact_moments)
         double s1 = 0.0, s2 = 0.0;   // per-lane sums (fast path, certified at the end)
-        unsigned long long s2n = 0;  // MKF_MOM: per-lane sum of dx^2 + dy^2 (exact)
+        unsigned long long s2n = 0;  // per-lane sum of dx^2 + dy^2 (exact)
         int mcnt = 0;                // this lane's summand count
         int nsize = 0;
         unsigned long long examined = 0;
@@ -468,7 +456,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             int nA = 0;                 // emissions staged in this octant
             const int q_sector = c_sector_base[q], q_axis = c_axis_bin[q], q_diag = c_diag_bin[q];
             // whichbin of this octant's directions by ratio class: axis, < tan15, < tan30, < 1, diagonal
-#if MKF_OBIN
             unsigned obinp = 0;   // 6 bits a class
             {
                 const double rr[5] = {0.0, 0.1, 0.4, 0.8, 1.0};
@@ -481,20 +468,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 obinp = __builtin_amdgcn_readfirstlane(obinp);
             }
 #define OBIN(k) ((int)__builtin_amdgcn_ubfe(obinp, (unsigned)(6 * (k)), 6u))
-#else
-            int obin[5];
-            {
-                const double rr[5] = {0.0, 0.1, 0.4, 0.8, 1.0};
-#pragma unroll
-                for (int k = 0; k < 5; k++) {
-                    const double mj = 10.0, mn = 10.0 * rr[k];
-                    const double ax = (q >= 4 ? mn : mj), ay = (q >= 4 ? mj : mn);
-                    obin[k] = whichbin((q & 1) ? ax : -ax, (q <= 1 || q >= 6) ? ay : -ay);
-                }
-            }
-#define OBIN(k) obin[k]
-#endif
             int depth = 0;
+            MK_T(9);
             // cell word of candidate t = lane of the next depth, loaded while this depth finishes: the
             // next depth's candidates are known before its collectgarbage, and they stay the same
             // when that adds no block (nb == 0: the gap list is unchanged)
@@ -505,10 +480,44 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 // ---------------- collectgarbage (sparksieve2.cpp:89-132) for the previous depth
                 int nb = L.misc[1];
                 if (nb > 0) pf_ok = false;
+                if (PROF && nb > 0) { mst[0]++; mst[1] += (nb == 1); mst[2] += nb; mst[3] += ng; }
                 if (nb > bcap + P.spill_cap) { failed = true; if (lane == 0) atomicOr(P.error, KERR_BLOCK_CAPACITY); }
                 if (failed) break;
-                if (nb > 0 && nb <= 64 && nb <= bcap && ng <= 64) {
-                    // Register path (the common case): lane i holds block i and lane g gap g; the
+                if (nb == 1 && ng <= 64) {
+                    // One block K (the common case): the sequential walk below meets every gap before the one
+                    // where K is consumed with K itself, and leaves the gaps after it unchanged -- and for those
+                    // gaps the same rule, applied to (gap, K) alone, also gives "unchanged" (they start past
+                    // K's end).  So each gap's 0, 1 or 2 output gaps are a function of the gap and K, computed
+                    // in the gap's lane, and placed by a wave prefix count.
+                    const double2 kb = L.blocks[0];
+                    const double kx = kb.x, ky = kb.y;
+                    const bool have = lane < ng;
+                    double gx = 0.0, gy = 0.0;
+                    if (have) { const double2 v = L.gaps[lane]; gx = v.x; gy = v.y; }
+                    double ax = gx, ay = gy, bx2 = 0.0, by2 = 0.0;
+                    int nout = have ? 1 : 0;
+                    if (have && !(ky < gx)) {
+                        bool create = true;
+                        double cx_ = gx, cy_ = gy;
+                        if (kx <= cx_) { create = false; if (ky > cx_) cx_ = ky; }
+                        if (ky >= cy_) { create = false; if (kx < cy_) cy_ = kx; }
+                        ax = cx_;
+                        ay = cy_;
+                        if (cy_ <= cx_ + 1e-10) nout = 0;
+                        else if (!(ky > cy_) && create) { nout = 2; ay = kx; bx2 = ky; by2 = cy_; }
+                    }
+                    const unsigned long long m1 = ballot(nout >= 1), m2 = ballot(nout == 2);
+                    const int pos = prefix_popc(m1) + prefix_popc(m2);
+                    const int no = __popcll(m1) + __popcll(m2);
+                    if (no > gcap) { if (lane == 0) atomicOr(P.error, KERR_GAP_CAPACITY); failed = true; break; }
+                    wave_sync();
+                    if (nout >= 1) L.gaps[pos] = make_double2(ax, ay);
+                    if (nout == 2) L.gaps[pos + 1] = make_double2(bx2, by2);
+                    ng = no;
+                    if (lane == 0) L.misc[1] = 0;
+                    wave_sync();
+                } else if (nb > 0 && nb <= 64 && nb <= bcap && ng <= 64) {
+                    // Register path (a few blocks): lane i holds block i and lane g gap g; the
                     // dedup, the ranks and the serial merge read other lanes through v_readlane
                     // (wave-uniform indices) instead of chains of dependent LDS reads.
                     const bool valid = lane < nb;
@@ -650,7 +659,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 // loop condition: sieve.hasGaps() (pointdata.cpp:1454)
                 if (ng == 0) break;
                 depth++;
-                if (COUNT) nsteps++;
+                if (COUNT || PROF) nsteps++;
                 // ---------------- sieve2 for this depth (pointdata.cpp:1512-1565)
                 // per-gap visit ranges with the monotone firstind rule
                 int carryF = 0, carryT = 0;
@@ -710,7 +719,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 bool hasgaps = false;
                 int gcur = 0; // per-lane gap pointer (t increases monotonically)
                 for (int t0 = 0; t0 < T; t0 += 64) {
-                    if (COUNT) nchunks++;
+                    if (COUNT || PROF) nchunks++;
                     int t = t0 + lane;
                     bool valid = t < T;
                     int ind = 0, hx = 0, hy = 0;
@@ -724,13 +733,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         octant_cell(q, cx, cy, depth, ind, hx, hy);
                         ingrid = (hx >= 0 && hx < P.cols && hy >= 0 && hy < P.rows);
                     }
+                    int nlb = 0, offb = 0;
                     if (ingrid) {
                         const int hc = hx * P.rows + hy;
-#if MKF_YMAJ
-                        w = (pf_ok && t0 == 0) ? pf_w : (q < 4 ? P.cellw[hc] : P.cellw_t[hy * P.cols + hx]);
-#else
                         w = (pf_ok && t0 == 0) ? pf_w : P.cellw[hc];
-#endif
                         const int nl = cell_nseg(w), off = cell_seg_off(w);
                         // (double)ind >= start*depth && (double)ind <= end*depth, on the integer
                         // bounds of the two FP64 products (computed once per gap and depth)
@@ -771,7 +777,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         // ind/depth: 0 and 1 are the axis / diagonal; tan15 and tan30 are irrational, so a float
                         // test with a 1e-6 margin decides every cell the reference's FP64 ratio (error ~1e-15)
                         // decides; cells inside the margin take the FP64 path
-#if MKF_CLASS
                         {
                             const float fd = (float)depth, fi = (float)ind, mg = 1e-6f * fd;
                             const float e15 = fi - 0.267949192f * fd, e30 = fi - 0.577350269f * fd;
@@ -787,25 +792,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                                 }
                             }
                         }
-#else
-                        if (add) {
-                            int k;
-                            if (ind == 0) k = 0;
-                            else if (ind == depth) k = 4;
-                            else {
-                                const float fd = (float)depth, fi = (float)ind, mg = 1e-6f * fd;
-                                const float e15 = fi - 0.267949192f * fd, e30 = fi - 0.577350269f * fd;
-                                k = (fabsf(e15) < mg || fabsf(e30) < mg) ? -1 : 1 + (e15 >= 0.0f) + (e30 >= 0.0f);
-                            }
-                            if (k >= 0) {
-                                bin = OBIN(k);
-                            } else {
-                                const double px = P.blx + sp * 1.0 * (double)hx, py = P.bly + sp * 1.0 * (double)hy;
-                                bin = whichbin(px - c0x, py - c0y);
-                            }
-                        }
-#endif
-#if MKF_MOM
                         // dx^2 + dy^2 (exact): the far distance (:1489) is the float of the bin's largest one (the
                         // dists grow with it, and (float) rounding keeps the order)
                         const unsigned n2 = (unsigned)(depth * depth) + __umul24((unsigned)ind, (unsigned)ind);
@@ -813,22 +799,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             atomicAdd(&L.binc[bin], 1u);
                             atomicMax(&L.bfar[bin], n2);
                         }
-#else
-                        if (add) {
-                            const double dx = (double)(hx - cx), dy = (double)(hy - cy);
-                            this_dist = sqrt(dx * dx + dy * dy) * sp;
-                            atomicAdd(&L.binc[bin], 1u);
-                            atomicMax(&L.bfar[bin], __float_as_uint((float)this_dist));
-                        }
-#endif
                         MK_T(3);
                         if (exact) {
                             // serial sums in lane order = reference addlist order
                             // (the lane index is wave-uniform: v_readlane into SGPRs keeps the serial
                             // chain on two dependent FP64 adds per cell instead of an LDS round trip)
-#if MKF_MOM
                             if (add) this_dist = sqrt((double)n2) * sp;   // sqrt(dx*dx + dy*dy) * spacing
-#endif
                             const int d_lo = __double2loint(this_dist), d_hi = __double2hiint(this_dist);
                             unsigned long long mm = am;
                             while (mm) {
@@ -840,13 +816,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                                 mm &= mm - 1;
                             }
                         } else if (add) {
-#if MKF_MOM
                             s1 += sqrt_nr((double)n2);
                             s2n += n2;
-#else
-                            s1 += this_dist;
-                            s2 += this_dist * this_dist;
-#endif
                             mcnt++;
                         }
                         MK_T(4);
@@ -920,15 +891,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     if (pind >= 0) {
                         int px, py;
                         octant_cell(q, cx, cy, d1, pind, px, py);
-#if MKF_YMAJ
-                        if (px >= 0 && px < P.cols && py >= 0 && py < P.rows)
-                            pf_w = q < 4 ? P.cellw[px * P.rows + py] : P.cellw_t[py * P.cols + px];
-#else
                         if (px >= 0 && px < P.cols && py >= 0 && py < P.rows) pf_w = P.cellw[px * P.rows + py];
-#endif
                     }
                     pf_ok = true;
                 }
+                MK_T(8);
                 // rows past MK_OPEN_LDS live in scratch memory: order this depth's stores before the next
                 // depth's loads of the same rows (other lanes); only sight lines past 1024 cells get here
                 if (depth >= MK_OPEN_LDS) __syncthreads();
@@ -1085,7 +1052,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 }
                 // lanes reduce in different orders: take lane 0's sums
                 s1 = __shfl(s1, 0); s2 = __shfl(s2, 0);
-#if MKF_MOM
                 // The reference's serial chains (pointdata.cpp:1490-1495) are within gamma_(n-1) of the exact sums
                 // of their terms, and those within 2u (dist) and 5u (dist^2) of sp*sqrt(n_i) and sp^2*n_i.  Ours:
                 // the lanes' sums of approximate roots (each within sqrt_err) reduced by a 6-level butterfly
@@ -1097,10 +1063,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 const double g2 = (double)(mmax + 7) * u / (1.0 - (double)(mmax + 7) * u);
                 const bool ok1 = certified_float_e(S1, 2.0 * (g1 + g2 + P.sqrt_err) * S1 + S1 * 0x1p-49, &m1f);
                 const bool ok2 = certified_float_e(S2, 2.0 * g1 * S2 + S2 * 0x1p-48, &m2f);
-#else
-                const bool ok1 = certified_float_sum(s1, nsize, mmax, &m1f);
-                const bool ok2 = certified_float_sum(s2, nsize, mmax, &m2f);
-#endif
                 if (!(ok1 && ok2)) { failed = true; certfail = true; }
             }
         }
@@ -1146,12 +1108,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         if (lane < 32) {
             P.bin_nruns[k * 32 + lane] = L.bnr[lane];
             P.bin_count[k * 32 + lane] = (uint16_t)L.binc[lane];
-#if MKF_MOM
             const unsigned nf = L.bfar[lane];
             P.bin_dist[k * 32 + lane] = nf ? (float)(sqrt((double)nf) * sp) : 0.0f;
-#else
-            P.bin_dist[k * 32 + lane] = __uint_as_float(L.bfar[lane]);
-#endif
         }
         if (lane == 0) {
             atomicAdd(&P.stats[0], examined);
@@ -1161,15 +1119,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 atomicAdd(&P.stats[3], (unsigned long long)nchunks);
                 P.src_work[2 * k] = nsteps;
                 P.src_work[2 * k + 1] = nchunks;
+            } else if (PROF) {
+                atomicAdd(&P.stats[2], (unsigned long long)nsteps);
+                atomicAdd(&P.stats[3], (unsigned long long)nchunks);
+                for (int i = 0; i < 4; i++) atomicAdd(&P.stats[18 + i], mst[i]);
             }
             if (PROF)
-                for (int i = 0; i < 8; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
+                for (int i = 0; i < 10; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
             P.attrs[k * 3 + 0] = (float)nsize;
             P.attrs[k * 3 + 1] = m1f;
             P.attrs[k * 3 + 2] = m2f;
         }
         __syncthreads();
-        for (int i = 0; i < 8; i++) cyc[i] = 0;
+        for (int i = 0; i < 10; i++) cyc[i] = 0;
+        for (int i = 0; i < 4; i++) mst[i] = 0;
         MK_T(7);
     }
 }
