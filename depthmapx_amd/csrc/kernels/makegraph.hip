@@ -29,6 +29,11 @@ constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capa
 // cells, and a full-length LDS array would cost a 2000^2 grid a quarter of its waves
 constexpr int MK_OPEN_LDS = 1024;
 constexpr int64_t MK_CAPACITY_TAG = 1ll << 62, MK_NODE_MASK = MK_CAPACITY_TAG - 1;
+// symmetry adjacency bits: open-run state, emission record (shallow / deep end adjacent), staged run (bit 14
+// of x0 / x1: the start / end range add cancels; grids below 16384 cells a side)
+constexpr uint32_t MK_OPEN_ADJ = 0x80000000u;
+constexpr int MK_REC_SHALLOW = 58, MK_REC_DEEP = 59;
+constexpr int16_t MK_RUN_FLAG = 0x4000;
 
 struct MakeGraphParams {
     int cols, rows;
@@ -185,6 +190,27 @@ __device__ __forceinline__ unsigned long long pack_emit(int slot, int ind, int d
            ((unsigned long long)de << 30) | ((unsigned long long)k << 44);
 }
 
+// Symmetry range adds of one published run (common.hpp sym_run_scatter) with two changes the in-hash does not
+// see: a single cell takes its octant's direction (x for H octants, y for V: its prefix sum is the cell
+// whatever the direction), so a run and its neighbour in the row share one difference array; and the ends
+// flagged by the sweep (a run ending where the row's next run starts) skip the +s / -s pair that cancels.
+__device__ __forceinline__ unsigned long long sym_run_scatter_q(Run ru, int q, bool skip0, bool skip1, unsigned long long su,
+                                                                int cols, int rows, const unsigned long long* prefix,
+                                                                unsigned long long* diff) {
+    const int64_t C = (int64_t)cols * rows;
+    const int dir = (ru.x0 == ru.x1 && ru.y0 == ru.y1) ? (q < 4 ? 0 : 1) : run_dir(ru);
+    int dx, dy;
+    dir_step(dir, dx, dy);
+    const int px = ru.x0 - dx, py = ru.y0 - dy, ex = ru.x1 + dx, ey = ru.y1 + dy;
+    const unsigned long long* Pf = prefix + (int64_t)dir * C;
+    unsigned long long acc = Pf[(int64_t)ru.x1 * rows + ru.y1];
+    if (px >= 0 && px < cols && py >= 0 && py < rows) acc -= Pf[(int64_t)px * rows + py];
+    unsigned long long* Df = diff + (int64_t)dir * C;
+    if (!skip0) atomicAdd(&Df[(int64_t)ru.x0 * rows + ru.y0], su);
+    if (!skip1 && ex >= 0 && ex < cols && ey >= 0 && ey < rows) atomicAdd(&Df[(int64_t)ex * rows + ey], (unsigned long long)(0ull - su));
+    return acc;
+}
+
 // Run for (ind, depth range) in octant q; H octants (q<4) run along x, V octants along y.
 __device__ __forceinline__ Run make_run(int q, int cx, int cy, int ind, int ds, int de) {
     int ax, ay, bx, by;
@@ -215,7 +241,8 @@ __device__ __forceinline__ void wave_sync() {
 __device__ __forceinline__ uint32_t ld_l2(const uint32_t* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ __forceinline__ void st_l2(uint32_t* p, uint32_t v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 
-// open-run state per row: valid(1) | slot(2) | start(14) | last(14)
+// open-run state per row: valid(1) | slot(2) | start(14) | last(14) | adjacent(1): the run started where the
+// row's previous run ended (MK_OPEN_ADJ)
 __device__ __forceinline__ uint32_t pack_open(int slot, int s, int l) {
     return 1u | ((uint32_t)slot << 1) | ((uint32_t)s << 3) | ((uint32_t)l << 17);
 }
@@ -367,6 +394,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     auto pref = P.prefix + (size_t)wave_global * (3 * (D + 1) + 4);
     auto rcnt = P.runcnt + (size_t)wave_global * (3 * (D + 1) + 4);   // zeroed by the host
     const double sp = P.spacing;
+    // the fused symmetry scatter's adjacency flags ride in bit 14 of the staged runs' x coordinates
+    const bool symflags = P.sym_diff != nullptr && P.cols < 16384 && P.rows < 16384;
 
     // LDS state that persists across sources is reset here once
     const int AX = 3 * (D + 1); // rcnt[AX] counts the runs of the axis row (ind 0)
@@ -835,13 +864,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                                 uint32_t o = ld_open(ind);
                                 int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
                                 if ((o & 1u) && oslot == slot && ol == depth - 1) {
-                                    st_open(ind, pack_open(slot, os, depth));
+                                    st_open(ind, pack_open(slot, os, depth) | (o & MK_OPEN_ADJ));
                                 } else {
+                                    // a run that ends where the row's next run starts (a bin boundary, not a
+                                    // gap): the two runs' facing ends need no symmetry range adds
+                                    const bool adj = (o & 1u) && ol == depth - 1;
                                     if (o & 1u) {   // the rank within (slot, row) is set after the octant
                                         emit = true;
-                                        rec = pack_emit(oslot, ind, os, ol, 0);
+                                        rec = pack_emit(oslot, ind, os, ol, 0) | ((unsigned long long)(o >> 31) << MK_REC_SHALLOW) |
+                                              ((unsigned long long)adj << MK_REC_DEEP);
                                     }
-                                    st_open(ind, pack_open(slot, depth, depth));
+                                    st_open(ind, pack_open(slot, depth, depth) | (adj ? MK_OPEN_ADJ : 0u));
                                 }
                             }
                         }
@@ -868,7 +901,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 dq = depth;
                 // prefetch: candidate t = lane of depth + 1 under the current gap list (few-gap case)
                 pf_ok = false;
-                if (ng <= 8 && !failed) {
+                // (a depth that added blocks changes the gap list: its next depth recomputes the ranges and
+                // reloads its cells, so nothing is prefetched for it)
+                if (ng <= 8 && !failed && L.misc[1] == 0) {
                     const int d1 = depth + 1;
                     int F1 = 0, T1 = 0, pind = -1;
                     for (int g = 0; g < ng; g++) {
@@ -913,7 +948,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     if (o & 1u) {
                         int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
                         emit = true;
-                        rec = pack_emit(oslot, ind, os, ol, 0);
+                        rec = pack_emit(oslot, ind, os, ol, 0) | ((unsigned long long)(o >> 31) << MK_REC_SHALLOW);
                     }
                     st_open(ind, 0u);
                 }
@@ -1014,7 +1049,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     int key = slot * R1 + r;
                     pos = low_n + (dasc ? (int)pref[key] + k : (int)pref[key + 1] - 1 - k);
                 }
-                seg[pos] = make_run(q, cx, cy, ind, ds, de);
+                Run ru = make_run(q, cx, cy, ind, ds, de);
+                if (symflags) {   // the adjacency bits, from depth order (shallow / deep end) to start / end
+                    const bool sh = (rec >> MK_REC_SHALLOW) & 1ull, dp = (rec >> MK_REC_DEEP) & 1ull;
+                    const bool inc = (q < 4) ? (q & 1) != 0 : (q >= 6);   // coordinate grows with depth
+                    if (inc ? sh : dp) ru.x0 |= MK_RUN_FLAG;
+                    if (inc ? dp : sh) ru.x1 |= MK_RUN_FLAG;
+                }
+                seg[pos] = ru;
             }
             if (diag_runs && lane == 0) {
                 // Bin::make diagonal: first pushed pixel, replaced by the last one if it lies left/right
@@ -1092,9 +1134,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 const Run* src = stB + L.misc[16 + q];
                 const int len = L.misc[24 + q];
                 for (int i = lane; i < len; i += 64) {
-                    const Run r = src[i];
+                    Run r = src[i];
+                    bool skip0 = false, skip1 = false;
+                    if (symflags) {
+                        skip0 = (r.x0 & MK_RUN_FLAG) != 0;
+                        skip1 = (r.x1 & MK_RUN_FLAG) != 0;
+                        r.x0 &= ~MK_RUN_FLAG;
+                        r.x1 &= ~MK_RUN_FLAG;
+                    }
                     P.pool[dst + i] = r;
-                    if (sym) ho += sym_run_scatter(r, su, P.cols, P.rows, P.sym_prefix, P.sym_diff);
+                    if (sym) ho += sym_run_scatter_q(r, q, skip0, skip1, su, P.cols, P.rows, P.sym_prefix, P.sym_diff);
                 }
                 dst += len;
             }
