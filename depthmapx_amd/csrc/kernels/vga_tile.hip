@@ -183,9 +183,24 @@ struct FView {
     const unsigned long long* CB;   // [tw*8][wc]: bit ty of column x: tile (x>>3, ty) has one in column x
     int tw, wr, wc;
 };
-#ifndef VGA_KH0
-#define VGA_KH0 2   // phase B: heads loaded with the cell's first loads (A/B builds: -DVGA_KH0=n)
-#endif
+// A run as one 64-bit word: the runs a loop picks with a non-constant index are kept as separate words and
+// chosen by selects (an indexed private array would live in scratch memory: a store and a load a lane per
+// element and use, ~1 TB a launch at 1000^2 with the spills)
+__device__ __forceinline__ Run run_of(unsigned long long w) {
+    Run r;
+    __builtin_memcpy(&r, &w, sizeof(Run));
+    return r;
+}
+__device__ __forceinline__ unsigned long long run_word(const Run* p) { return *(const unsigned long long*)p; }
+
+// Workgroup-shared scalars read from LDS after a barrier are the same in every lane: reading them through
+// readfirstlane keeps them (and the level loop's counters built from them) in scalar registers instead of
+// 64-bit VGPR pairs that the 128-VGPR budget spills around every level
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ long long uni64(unsigned long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v), hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (long long)(((unsigned long long)hi << 32) | lo);
+}
 // Tiles [t0, t1] of one summary line (bit per tile, one word per 64 tiles):
 // OR of F[base + tx * stride] & (cell mask of tile tx), 8 frontier tiles per round.
 template <bool VERT>
@@ -296,6 +311,7 @@ struct TileShared {
     int mpart;            // merge partner cell of the source (-1: none)
     unsigned long long cnt, mass;
     unsigned long long mcorr, mdisc;   // merge pass: pairs discovered together, partners of U_f joined
+    long long m_f, m_u, disc, target;  // the level loop's state (in LDS: no VGPRs live across the levels)
 };
 
 // Next work item: one grid counter (progress and cancel ride on it).  Contiguous per-XCD ranges, so that an
@@ -612,7 +628,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             __syncthreads();
             if (tid == 0) S.src = grab_work(P.ctl, P.work_counter);
             __syncthreads();
-            src = P.src_begin + (int64_t)S.src * P.chunk;
+            src = P.src_begin + (int64_t)uni(S.src) * P.chunk;
             chunk_end = min(src + (int64_t)P.chunk, P.src_end);
         } else {
             src++;
@@ -648,7 +664,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 or_wg(&Vg[t], b);
             }
             __syncthreads();
-            n_in_uf += (long long)S.cnt;
+            n_in_uf += uni64(S.cnt);
             __syncthreads();
             if (tid == 0) S.cnt = 0;
         }
@@ -663,7 +679,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 else if (pr.y == scell) S.mpart = pr.x;
             }
             __syncthreads();
-            const int pc = S.mpart;
+            const int pc = uni(S.mpart);
             if (pc >= 0) {
                 spart = P.cell_node[pc];
                 const int px = pc / rows, py = pc % rows;
@@ -675,17 +691,21 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             __syncthreads();
             if (tid == 0) S.mpart = -1;
         }
-        const long long target = P.uf_count - n_in_uf;
-        long long m_f = seeded ? P.nseeds : (spart >= 0 ? 2 : 1), m_u = target, discovered = 0;
         int level = 0, nlev = 1;
         bool overflow = false;
-        if (tid == 0) { S.tn[0] = 0; S.tn[1] = 0; }
+        if (tid == 0) {
+            S.tn[0] = 0; S.tn[1] = 0;
+            S.target = P.uf_count - n_in_uf;
+            S.m_f = seeded ? P.nseeds : (spart >= 0 ? 2 : 1);
+            S.m_u = S.target;
+            S.disc = 0;
+        }
         __syncthreads();
         if (tid == 0) hist[0] = seeded ? P.nseeds : 1;
         for (;;) {
             if (P.radius != -1 && level >= P.radius) break;
-            if (discovered >= target) break;
-            const bool bottom_up = level > 0 && (m_f * (long long)P.alpha > m_u);
+            if (uni64(S.disc) >= uni64(S.target)) break;
+            const bool bottom_up = level > 0 && (uni64(S.m_f) * (long long)P.alpha > uni64(S.m_u));
             tmark = __builtin_amdgcn_s_memtime();
             if (level == 0) {
                 // ---- level 1: rasterise the source's runs (top-down from {s}, or from every seed)
@@ -703,15 +723,15 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 // ---- A: tile-common runs
                 // only the tiles the previous level's bookkeeping listed can hold an unvisited cell
                 const int32_t* TLc = TL + (level & 1) * nt;
-                const int ntl = S.tn[level & 1];
+                const int ntl = uni(S.tn[level & 1]);
                 for (int t0 = 0; t0 < ntl; t0 += NT) {
                     const int t = t0 + tid < ntl ? TLc[t0 + tid] : nt;
                     unsigned long long U = 0ull, rg = ~0ull;
                     if (t < nt) {
                         // V, the regular mask and the CRK common runs in one round trip
-                        Run c[CRK];
-#pragma unroll
-                        for (int j = 0; j < CRK; j++) c[j] = P.cr[CRK * t + j];
+                        static_assert(CRK == 4, "phase A keeps the common runs in four words");
+                        const unsigned long long c0 = run_word(P.cr + CRK * t), c1 = run_word(P.cr + CRK * t + 1),
+                                                 c2 = run_word(P.cr + CRK * t + 2), c3 = run_word(P.cr + CRK * t + 3);
                         U = ~Vg[t];
                         rg = P.regular_tiles[t];
                         const unsigned long long R = U & rg;
@@ -724,11 +744,13 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
 // C_FUSED: phase C's row test and mask test in one pass per cell (1000^2: VGA 5.57 -> 5.11 s)
                             bool hit = false;
 #pragma unroll 1
-                            for (int j = 0; j < CRK; j++)
-                                if (!hit && j < P.crk && c[j].x0 >= 0) {
+                            for (int j = 0; j < CRK; j++) {
+                                const Run cj = run_of(j == 0 ? c0 : j == 1 ? c1 : j == 2 ? c2 : c3);
+                                if (!hit && j < P.crk && cj.x0 >= 0) {
                                     rt++;
-                                    hit = run_hits_fs(FV, c[j]);
+                                    hit = run_hits_fs(FV, cj);
                                 }
+                            }
                             if (hit) { Xg[t] = R; U &= ~R; ST(7, 1); }
                         }
                     }
@@ -747,7 +769,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 }
                 sync_global();
                 if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(9, n - tmark); tmark = n; }
-                const int qn = S.qn;
+                const int qn = uni(S.qn);
                 // ---- B: a wave per queued tile, lane = cell of the tile.  The tile-to-tile rows
                 // (ttvis: a frontier tile every regular cell of t sees completely resolves them all;
                 // ttany: no frontier tile in view of any regular cell of t, none is at this level)
@@ -761,7 +783,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     // the cell loads follow the entry without a round trip of their own
                     int it = 0;
                     if (lane == 0) it = atomicAdd(&S.bn, 1);
-                    it = __shfl(it, 0);
+                    it = __builtin_amdgcn_readlane(it, 0);
                     if (it >= qn) break;
                     const int4 e = Q[it];
                     const int t = e.x;
@@ -776,15 +798,15 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     int64_t pof = 0;
                     // heads loaded with the cell's first loads, the rest of the KH heads in the extension loop
                     // (round 4 at 1000^2: 4 -> 2 heads 4.67 -> 4.60 s, fewer live registers at the head tests)
-                    constexpr int KH0 = VGA_KH0;
-                    Run hd[KH0];
+                    constexpr int KH0 = 2;
+                    unsigned long long hd0 = 0ull, hd1 = 0ull;
                     if (cand) {
                         ss = P.tscan_start[id];
                         nr = P.tnruns[id];
                         hp = Hn[id];
                         if (P.pmask) pof = P.poff[id];
-#pragma unroll
-                        for (int r = 0; r < KH0; r++) hd[r] = P.heads[r * hstride + id];
+                        hd0 = run_word(P.heads + id);
+                        hd1 = run_word(P.heads + hstride + id);
                     }
                     unsigned long long acc = 0ull, acca = ~0ull;
                     if (P.ttvis) {
@@ -834,7 +856,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         for (int r = 0; r < KH0; r++)
                             if (!hit && r < nr) {
                                 rt++;
-                                hit = run_hits_fs(FV, hd[r]);
+                                hit = run_hits_fs(FV, run_of(r == 0 ? hd0 : hd1));
                             }
                         if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
                         else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
@@ -885,7 +907,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 }
                 sync_global();
                 if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(10, n - tmark); tmark = n; }
-                const int hn = S.hn;
+                const int hn = uni(S.hn);
                 // ---- C: hard cells.  A wave grabs CCH list entries at once (one coalesced load);
                 // C0 tests their tile-visibility rows two cells at a time (16 row words a lane in
                 // flight): a frontier tile the cell sees completely is a certain hit (regular cell:
@@ -899,7 +921,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 for (;;) {
                     int it0 = 0;
                     if (lane == 0) it0 = atomicAdd(&S.item, CCH);
-                    it0 = __shfl(it0, 0);
+                    it0 = __builtin_amdgcn_readlane(it0, 0);
                     if (it0 >= hn) break;
                     const int cn = min(CCH, hn - it0);
                     const int myv = lane < cn ? L[it0 + lane] : -1;
@@ -1072,11 +1094,11 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 sync_global();
                 for (int t = tid; t < nt; t += NT) F[t] = 0ull;
                 sync_global();
-                const int fn = S.hn;
+                const int fn = uni(S.hn);
                 for (;;) {
                     int it = 0;
                     if (lane == 0) it = atomicAdd(&S.item, 1);
-                    it = __shfl(it, 0);
+                    it = __builtin_amdgcn_readlane(it, 0);
                     if (it >= fn) break;
                     int x, y;
                     xy_of_tile_id(L[it], tw, x, y);
@@ -1111,7 +1133,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             unsigned long long c_loc = 0, m_loc = 0;
             const int32_t* TLc = TL + (level & 1) * nt;
             int32_t* TLn = TL + ((level + 1) & 1) * nt;
-            const int nwalk = have_list ? S.tn[level & 1] : nt;
+            const int nwalk = have_list ? uni(S.tn[level & 1]) : nt;
             for (int i0 = 0; i0 < nwalk; i0 += NT) {
                 const int t = i0 + tid < nwalk ? (have_list ? TLc[i0 + tid] : i0 + tid) : -1;
                 bool open = false;
@@ -1198,13 +1220,16 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 }
             }
             sync_global();
-            const long long cnt = (long long)S.cnt, mass = (long long)S.mass;
-            const long long mcorr = (long long)S.mcorr, mdisc = (long long)S.mdisc;
+            const long long cnt = uni64(S.cnt), mass = uni64(S.mass);
+            const long long mcorr = uni64(S.mcorr), mdisc = uni64(S.mdisc);
             if (tid == 0) { const unsigned long long n = __builtin_amdgcn_s_memtime(); ST(12, n - tmark); tmark = n; }
             __syncthreads();
             if (tid == 0) {
                 S.cnt = 0; S.mass = 0; S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.mcorr = 0; S.mdisc = 0;
                 S.tn[level & 1] = 0;   // this level's list is spent; it is the next level's append target
+                S.disc += cnt + mdisc;
+                S.m_u -= cnt + mdisc;
+                S.m_f = mass;
             }
             // the next level's first appends (phase A's queue, the top-down frontier list) must not race
             // the resets above: a wave that appended before them lost its entries
@@ -1212,9 +1237,6 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
             if (cnt == 0) break;
             if (level + 1 >= VGA_HMAX) { overflow = true; break; }
             if (tid == 0) hist[level + 1] = (int)(cnt - mcorr);
-            discovered += cnt + mdisc;
-            m_u -= cnt + mdisc;
-            m_f = mass;
             level++;
             nlev = level + 1;
             if (tid == 0) ST(bottom_up ? 3 : 4, 1);

@@ -3,7 +3,8 @@ scratch spill traffic, waits and memory ops inside each loop.  usage: python scr
 import re, sys
 L = open(sys.argv[1]).read().split("\n")
 maxd = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-s = next(i for i, l in enumerate(L) if re.match(r"^_Z\S*makegraph_kernel\S*:", l))
+kname = sys.argv[3] if len(sys.argv) > 3 else "makegraph_kernel"
+s = next(i for i, l in enumerate(L) if re.match(r"^_Z\S*%s\S*:" % kname, l))
 e = next(i for i in range(s, len(L)) if L[i].strip().startswith(".Lfunc_end"))
 body = L[s:e]
 ext = {}
