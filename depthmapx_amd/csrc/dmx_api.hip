@@ -1820,23 +1820,25 @@ static int prepare_tiles(dmx_graph* g) {
     const bool ftv_on = !(ftv_env && atoi(ftv_env) == 0);
     // Grids up to 1024 cells a side (tvw <= 256: the masks' row test reads 4 words a lane): tvis, ftvis, the
     // tile rows and the partial-tile masks when they take at most a quarter of the free memory.  Wider grids
-    // (2000^2: 8 KB a row, 32 GB) keep tvis alone, as the phase-C miss certificate in front of the run scan,
-    // when it takes at most a third of what is free next to the graph and its scan order.
+    // (2000^2: 8 KB a row, 32 GB) keep tvis, the phase-C miss certificate in front of the run scan, when it takes
+    // at most a third of what is free next to the graph and its scan order, and ftvis too (the certain-hit
+    // test) when both leave 24 GiB free for the search's own buffers.
     const bool wide = tvw > 256;
     const size_t free_all = free_b + cached_bytes();
-    const bool ftv = ftv_on && !wide;
+    bool ftv = ftv_on && (!wide || 2 * tv_bytes + (24ull << 30) <= free_all);
     bool tv_build = tv_on && N && tv_bytes <= (32ull << 30) &&
                     (wide ? tv_bytes <= free_all / 3 : tv_bytes * (ftv ? 2 : 1) <= free_b / 4);
     if (g->prep_fn) {
-        // every rank must take the same branch (the rows are all-reduced): build only if all can
+        // every rank must take the same branches (the rows are all-reduced): build only what all can
         DevBuf<int64_t> veto;
         HIPCHK(veto.alloc(1));
-        const int64_t v = tv_build ? 0 : 1;
+        const int64_t v = (tv_build ? 0 : 1) + (ftv ? 0 : (1ll << 20));
         HIPCHK(hipMemcpyAsync(veto.p, &v, 8, hipMemcpyHostToDevice, s));
         if (int rc = prep_allreduce(g, veto.p, 1, DMX_I64)) return rc;
         int64_t vs = 0;
         HIPCHK(copy_sync(g->ctx->stream, &vs, veto.p, 8, hipMemcpyDeviceToHost));
-        tv_build = vs == 0;
+        tv_build = (vs & ((1ll << 20) - 1)) == 0;
+        ftv = (vs >> 20) == 0;
     }
     if (tv_build) {
         HIPCHK(g->tvis.alloc(Ct * tvw));
@@ -1862,14 +1864,14 @@ static int prepare_tiles(dmx_graph* g) {
         if (ftv)
             if (int rc = prep_allreduce(g, g->ftvis.p, Ct * tvw, DMX_I64)) return rc;
         const char* tt_env = getenv("DMX_VGA_TTVIS");
-        if (ftv && !(tt_env && atoi(tt_env) == 0)) {
+        if (ftv && !wide && !(tt_env && atoi(tt_env) == 0)) {
             HIPCHK(g->ttvis.alloc((size_t)2 * nt * tvw));   // ttvis, then ttany
             hipLaunchKernelGGL(tile_tt_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, nt, tvw, g->regular_tiles.p,
                                g->ftvis.p, g->tvis.p, g->ttvis.p, g->ttvis.p + (size_t)nt * tvw);
             HIPCHK(hipGetLastError());
         }
         const char* pm_env = getenv("DMX_VGA_PMASK");
-        if (ftv && !(pm_env && atoi(pm_env) == 0))
+        if (ftv && !wide && !(pm_env && atoi(pm_env) == 0))
             if (int rc = prepare_pmask(g, rows, tw, th, tvw, Ct)) return rc;
         // the row summaries keep word k in lane k (vga_tile.hip reads them with readlane): at most 64 words
         if (wide && (tvw + 63) / 64 <= 64) {

@@ -954,8 +954,8 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                     }
                                 }
                             } else {
-                                // wider grids (tvis alone): the row summaries leave out the words that are
-                                // zero for the cell; summary word k (lane k) holds bit `lane` for row word w
+                                // wider grids: the row summaries leave out the words that are zero for the
+                                // cell (ftvis lies inside tvis); summary word k (lane k) holds bit `lane` for row word w
                                 const int tvsw = (P.tvw + 63) / 64;
                                 unsigned long long sm0 = 0ull, sm1 = 0ull;
                                 if (lane < tvsw) {
@@ -973,8 +973,14 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                     if (!((s0 | s1) >> lane & 1ull)) continue;
                                     const unsigned long long fs = Fsr[w];   // w < tvw: its summary bit is set
                                     if (fs) {
-                                        if ((s0 >> lane) & 1ull) ta0 |= tv0[w] & fs;
-                                        if ((s1 >> lane) & 1ull) ta1 |= tv1[w] & fs;
+                                        if ((s0 >> lane) & 1ull) {
+                                            ta0 |= tv0[w] & fs;
+                                            if (fv0) fa0 |= fv0[w] & fs;
+                                        }
+                                        if ((s1 >> lane) & 1ull) {
+                                            ta1 |= tv1[w] & fs;
+                                            if (fv1) fa1 |= fv1[w] & fs;
+                                        }
                                     }
                                 }
                             }

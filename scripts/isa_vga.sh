@@ -7,7 +7,7 @@ cat > /tmp/vt_only.hip <<HIP
 #include "$R/depthmapx_amd/csrc/kernels/vga.hip"
 #include "$R/depthmapx_amd/csrc/kernels/vga_do.hip"
 #include "$R/depthmapx_amd/csrc/kernels/vga_tile.hip"
-template __global__ void dmx::vga_tile_kernel<$NT, true, true, false>(const dmx::VgaTileParams*);
+template __global__ void dmx::vga_tile_kernel<$NT, ${VARIANT:-true, true, false}>(const dmx::VgaTileParams*);
 HIP
 cd /tmp
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-fast-math --cuda-device-only -S \
