@@ -2103,6 +2103,10 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     else if (rb_ok && lds_rbcb + lds_h <= lds_cap) { fg = true; rbm = true; L = lds_rbcb + lds_h; }
     else if (lds_sc + lds_h <= lds_cap) { fg = true; L = lds_sc + lds_h; }
     else return fail(DMX_ERR_CAPACITY, "grid too large for the tile BFS's LDS summaries");
+    // With the frontier in HBM a top-down level's run rasterisation takes global atomics: past level 1 the
+    // bottom-up levels win (2000^2 interior block: alpha 60 -> 200: 2.70 -> 2.28 s, identical output;
+    // 1000 and 100000 the same, profiles/r5_vga2000_alpha.jsonl)
+    if (fg && !getenv("DMX_VGA_ALPHA")) Q.alpha = 1000;
     DevBuf<unsigned long long> xg;
     DevBuf<int4> queue;
     DevBuf<int32_t> list;

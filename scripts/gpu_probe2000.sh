@@ -6,7 +6,7 @@ OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/${TAG:-v2000}
 mkdir -p $OUT
 ( while true; do sleep 45; date +%s >> $OUT/heartbeat; done ) > /dev/null 2>&1 &
 HB=$!
-timeout -k 10 ${PROBE_TIMEOUT:-700} python -u scripts/probe_vga2000.py --nsrc ${NSRC:-4096} --blocks ${BLOCKS:-4} --check-do 16 > $OUT/probe2000.jsonl 2> $OUT/progress.txt
+timeout -k 10 ${PROBE_TIMEOUT:-700} python -u scripts/probe_vga2000.py --nsrc ${NSRC:-4096} --blocks ${BLOCKS:-4} ${PROBE_ARGS:---check-do 16} > $OUT/probe2000.jsonl 2> $OUT/progress.txt
 rc=$?
 kill $HB
 grep -v amdgpu.ids $OUT/progress.txt | cut -c1-300

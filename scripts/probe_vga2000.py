@@ -22,7 +22,8 @@ def main():
     ap.add_argument("--nsrc", type=int, default=4096)
     ap.add_argument("--blocks", type=int, default=4)
     ap.add_argument("--check-do", type=int, default=0, help="sources of the first block re-run on vga_do and compared")
-    ap.add_argument("--alphas", default="", help="comma list: re-time the first block with DMX_VGA_ALPHA set to each")
+    ap.add_argument("--alphas", default="", help="comma list: re-time one block with DMX_VGA_ALPHA set to each")
+    ap.add_argument("--alpha-block", type=int, default=0, help="the block the alpha sweep re-times")
     a = ap.parse_args()
     W = 1999
     ctx = dmx.Context(0)
@@ -54,11 +55,12 @@ def main():
         print(json.dumps(rec["blocks"][-1]), file=sys.stderr, flush=True)
     for al in [x for x in a.alphas.split(",") if x]:
         os.environ["DMX_VGA_ALPHA"] = al
-        b = starts[0]
+        b = starts[a.alpha_block]
         out = g.vga_visual_global(src_begin=b, src_end=b + per)
         st = ctx.last_stats()
-        same = bool(np.array_equal(out[b:b + per].view(np.uint32), outs[0].view(np.uint32)))
-        rec.setdefault("alpha_sweep", []).append({"alpha": int(al), "kernel_s": ctx.last_timing()[1], "identical": same,
+        same = bool(np.array_equal(out[b:b + per].view(np.uint32), outs[a.alpha_block].view(np.uint32)))
+        rec.setdefault("alpha_sweep", []).append({"alpha": int(al), "block": a.alpha_block, "kernel_s": ctx.last_timing()[1],
+                                                  "identical": same,
                                                   "bottom_up_levels": st["vga_bottom_up_levels"],
                                                   "top_down_levels": st["vga_top_down_levels"],
                                                   "runs_tested": st["vga_runs_expanded"],
