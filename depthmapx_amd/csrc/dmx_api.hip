@@ -250,6 +250,7 @@ struct dmx_graph {
     DevBuf<unsigned long long> notuf_tiles;
     int64_t uf_count = -1;
     bool scan_ready = false;   // prepare_uf done (scan order; U_f from the symmetry pass or coverage counting)
+    bool scan_released = false;   // the scan order gave its memory to the wide-grid masks (runs read in pool order)
     // bottom-up scan order: runs of each node longest-first, indexed by cell
     DevBuf<Run> scan_pool;
     DevBuf<int64_t> cell_scan_start;
@@ -1519,6 +1520,7 @@ static int prep_allreduce(dmx_graph* g, void* p, int64_t count, int dtype) {
 // U_f (filled cells that appear in some run: the early-exit universe of every BFS) by range counts,
 // plus the longest-first scan pool.  O(runs) with a few line-prefix passes.
 static int prepare_symmetry(dmx_graph* g);
+static int build_scan_order(dmx_graph* g);
 static int prepare_uf(dmx_graph* g) {
     if (g->scan_ready) return DMX_OK;
     // the symmetry pass computes U_f from its in-set hashes; coverage counting only when it is skipped
@@ -1553,12 +1555,23 @@ static int prepare_uf(dmx_graph* g) {
                            g->pm->d_cell_node.p, cov.p, g->uf_tiles.p, g->notuf_tiles.p, cnt.p);
         HIPCHK(hipGetLastError());
     }
-    // scan pool (node order, runs longest-first inside each node)
-    std::vector<int32_t> nr((size_t)std::max<int64_t>(N, 1));
-    if (N) HIPCHK(hipMemcpyAsync(nr.data(), g->node_nruns.p, N * 4, hipMemcpyDeviceToHost, s));
     unsigned long long ufc = have_uf ? (unsigned long long)g->uf_count : 0ull;
-    if (!have_uf) HIPCHK(hipMemcpyAsync(&ufc, cnt.p, 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    if (!have_uf) HIPCHK(copy_sync(s, &ufc, cnt.p, 8, hipMemcpyDeviceToHost));
+    if (int rc = build_scan_order(g)) return rc;
+    g->uf_count = (int64_t)ufc;
+    g->scan_ready = true;
+    return DMX_OK;
+}
+
+// The scan order: every node's runs longest-first (scan_pool, node order), with per-node and per-cell starts.
+static int build_scan_order(dmx_graph* g) {
+    dmx_ctx* ctx = g->ctx;
+    hipStream_t s = ctx->stream;
+    PointMapHost& h = *g->pm->host;
+    const int rows = h.rows();
+    const int64_t C = (int64_t)h.cols() * rows, N = g->nnodes;
+    std::vector<int32_t> nr((size_t)std::max<int64_t>(N, 1));
+    if (N) HIPCHK(copy_sync(s, nr.data(), g->node_nruns.p, N * 4, hipMemcpyDeviceToHost));
     std::vector<int64_t> ss((size_t)std::max<int64_t>(N, 1));
     int64_t acc = 0;
     for (int64_t k = 0; k < N; k++) { ss[k] = acc; acc += nr[k]; }
@@ -1576,9 +1589,19 @@ static int prepare_uf(dmx_graph* g) {
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(s));
-    g->uf_count = (int64_t)ufc;
-    g->scan_ready = true;
+    g->scan_released = false;
     return DMX_OK;
+}
+
+// The wide-grid partial-tile masks take the scan order's place (prepare_tiles): the searches that read the
+// scan order itself (vga_do, a tile search without the masks) free the tile-visibility data and rebuild it.
+static int restore_scan_order(dmx_graph* g) {
+    if (!g->scan_released) return DMX_OK;
+    g->pmask.reset(); g->ppre.reset(); g->poff.reset();
+    g->tvis.reset(); g->ftvis.reset(); g->tvsum.reset(); g->ttvis.reset();
+    g->tvw = 0;
+    g->tiles_ready = false;
+    return build_scan_order(g);
 }
 
 // In-set corrections for bottom-up BFS (vga_do.hip, "symmetry / in-set corrections").
@@ -1731,7 +1754,7 @@ static int prepare_symmetry(dmx_graph* g) {
 // all-reducing its ~10 GB over the ranks would cost more, and whether a rank has them does not change
 // its results (phase C scans runs without them), so the ranks need not agree.  Skipped when they would
 // take more than a quarter of the free memory.
-static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_t Ct) {
+static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_t Ct, bool wide) {
     dmx_ctx* ctx = g->ctx;
     hipStream_t s = ctx->stream;
     DevBuf<int64_t> cnt, scratch;
@@ -1748,20 +1771,44 @@ static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_
     HIPCHK(copy_sync(s, &total, g->poff.p + Ct, 8, hipMemcpyDeviceToHost));
     size_t free_b = 0, total_b = 0;
     HIPCHK(hipMemGetInfo(&free_b, &total_b));
-    const bool build = total > 0 && (size_t)total * 8 <= free_b / 4;
+    const size_t mask_b = (size_t)total * 8;
+    bool build = total > 0 && mask_b <= free_b / 4;
+    const int pmcap = wide ? PM_CAP_WIDE : PM_CAP;
+    if (wide && total > 0 && tile_pmask_lds(tvw, pmcap) <= 150 * 1024) {
+        // Above 1024 cells a side the masks (~80 GB at 2000^2) fit only in the scan order's place: the runs
+        // are then scanned in pool order (the heads and tile-common runs stay, built from the scan order;
+        // only special nodes still scan, from the first run; every regular cell phase C sees takes the masks)
+        const size_t reserve = 16ull << 30;   // the search's per-workgroup buffers
+        const size_t free_all = free_b + cached_bytes();
+        const size_t scan_b = g->scan_pool.p ? g->scan_pool.n * sizeof(Run) + (size_t)g->nnodes * 8 +
+                                                   (size_t)g->cell_scan_start.n * 12 : 0;
+        if (mask_b + reserve <= free_all) {
+            build = true;
+        } else if (g->scan_pool.p && mask_b + reserve <= free_all + scan_b) {
+            g->scan_pool.reset(); g->scan_start.reset(); g->cell_scan_start.reset(); g->cell_nruns.reset();
+            g->scan_released = true;
+            hipLaunchKernelGGL(tile_pool_order_kernel, dim3((unsigned)((g->nnodes + 255) / 256)), dim3(256), 0, s, rows, tw,
+                               g->pm->d_node_cell.p, g->nnodes, g->node_run_start.p, g->tscan_start.p);
+            HIPCHK(hipGetLastError());
+            VLOG("vga prep: scan order released for %.1f GB of partial-tile masks\n", mask_b / 1e9);
+            build = true;
+        } else {
+            build = false;
+        }
+    }
     if (!build) {
         g->poff.reset();
         g->ppre.reset();
         return DMX_OK;
     }
     HIPCHK(g->pmask.alloc((size_t)total));
-    HIPCHK(hipMemsetAsync(g->pmask.p, 0, (size_t)total * 8, s));
+    HIPCHK(hipMemsetAsync(g->pmask.p, 0, mask_b, s));
     const int64_t N = g->nnodes;
     if (N > 0) {
         const int64_t nb = std::min<int64_t>(N, (int64_t)ctx->num_cu * 16);
-        hipLaunchKernelGGL(tile_pmask_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), 0, s, rows, tw, th,
-                           g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, g->tvis.p,
-                           g->ftvis.p, g->poff.p, g->pmask.p);
+        hipLaunchKernelGGL(tile_pmask_kernel, dim3((unsigned)nb), dim3(64 * TV_WAVES), tile_pmask_lds(tvw, pmcap), s, rows,
+                           tw, th, g->pm->d_node_cell.p, N, g->node_run_start.p, g->node_nruns.p, g->pool.p, g->tvis.p,
+                           g->ftvis.p, g->poff.p, g->pmask.p, pmcap);
         HIPCHK(hipGetLastError());
     }
     return DMX_OK;
@@ -1871,8 +1918,9 @@ static int prepare_tiles(dmx_graph* g) {
             HIPCHK(hipGetLastError());
         }
         const char* pm_env = getenv("DMX_VGA_PMASK");
-        if (ftv && !wide && !(pm_env && atoi(pm_env) == 0))
-            if (int rc = prepare_pmask(g, rows, tw, th, tvw, Ct)) return rc;
+        // (wide grids: the masks need the row summaries, at most 64 words of them, and a 16-bit row prefix)
+        if (ftv && !(pm_env && atoi(pm_env) == 0) && (!wide || ((tvw + 63) / 64 <= 64 && nt <= 65535)))
+            if (int rc = prepare_pmask(g, rows, tw, th, tvw, Ct, wide)) return rc;
         // the row summaries keep word k in lane k (vga_tile.hip reads them with readlane): at most 64 words
         if (wide && (tvw + 63) / 64 <= 64) {
             HIPCHK(g->tvsum.alloc((size_t)Ct * ((tvw + 63) / 64)));
@@ -2042,14 +2090,15 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.cols = h.cols(); Q.rows = h.rows(); Q.tw = tw; Q.th = th;
     Q.seed_tiles = g->notuf_tiles.p; Q.regular_tiles = g->regular_tiles.p; Q.nonexp_tiles = g->pm->d_nonexp_tiles.p;
     Q.cr = g->cr.p; Q.heads = g->heads.p; Q.tscan_start = g->tscan_start.p; Q.tnruns = g->tnruns.p;
-    Q.scan_pool = g->scan_pool.p;
+    Q.scan_pool = g->scan_released ? g->pool.p : g->scan_pool.p;   // (tscan_start then indexes the pool)
     Q.tvis = g->tvw ? g->tvis.p : nullptr; Q.tvw = g->tvw;
     Q.tvsum = (g->tvw && g->tvsum.p) ? g->tvsum.p : nullptr;
     Q.ftvis = (g->tvw && g->ftvis.p) ? g->ftvis.p : nullptr;
     Q.ttvis = (g->tvw && g->ttvis.p) ? g->ttvis.p : nullptr;
     Q.ttany = Q.ttvis ? g->ttvis.p + (size_t)tw * th * g->tvw : nullptr;
-    const char* pmk_env = getenv("DMX_VGA_PMASK");   // also a launch-time switch (the masks stay built)
-    Q.pmask = (Q.ftvis && g->pmask.p && !(pmk_env && atoi(pmk_env) == 0)) ? g->pmask.p : nullptr;
+    const char* pmk_env = getenv("DMX_VGA_PMASK");   // also a launch-time switch (the masks stay built), except
+    // where the masks replaced the scan order (phase C's scan of the regular cells reads the scan order)
+    Q.pmask = (Q.ftvis && g->pmask.p && (g->scan_released || !(pmk_env && atoi(pmk_env) == 0))) ? g->pmask.p : nullptr;
     Q.poff = Q.pmask ? g->poff.p : nullptr;
     Q.ppre = Q.pmask ? g->ppre.p : nullptr;
     Q.node_cell = g->pm->d_node_cell.p; Q.cell_node = g->pm->d_cell_node.p; Q.node_flags = g->pm->d_node_flags.p;
@@ -2224,6 +2273,7 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
             if (rc2 != DMX_ERR_CAPACITY) return rc2;   // capacity (level histogram): retry with vga_do
         }
     }
+    if (int rc3 = restore_scan_order(g)) return rc3;   // (vga_do reads the scan order)
     const size_t lds_do = (size_t)tw * th * 8 * 3 + (maxlev + 4) * 4 + 64;
     const char* force = getenv("DMX_VGA_KERNEL");
     const bool want_v1 = force && std::string(force) == "v1";

@@ -572,6 +572,66 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
     return false;
 }
 
+// The exact test on wide grids (tvw > 256 row words, row summaries tvsum), as pmask_hit_fused: a frontier tile
+// under the full-visibility row is a hit, else the masks of the partial frontier tiles decide.  Lane `lane`
+// takes the row words k*64 + lane whose summary bit is set (the cell's non-zero words) under a frontier tile
+// row; a mask's position is ppre (the word's partial prefix) plus the partial bits before it.  (Regular cells
+// come here after phase C's row pass found no certain hit; special nodes with no Missing cell in the frontier
+// come directly.)  No hint is recorded: a wide grid's tile index does not fit the hint's 15-bit field.
+__device__ __forceinline__ bool pmask_hit_wide(const VgaTileParams& P, const unsigned long long* F,
+                                               const unsigned long long* Fsr, int id, unsigned& nload) {
+    const int lane = threadIdx.x & 63;
+    const int tvw = P.tvw, tw = P.tw, wr = (P.tw + 63) / 64, tvsw = (tvw + 63) / 64;
+    const size_t row = (size_t)id * tvw;
+    const unsigned long long sm = lane < tvsw ? P.tvsum[(size_t)id * tvsw + lane] : 0ull;
+    const unsigned long long* pm = P.pmask + P.poff[id];
+#pragma unroll 1
+    for (int k = 0; k < tvsw; k++) {
+        const unsigned long long s =
+            (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)sm, k) |
+            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(sm >> 32), k) << 32);
+        if (s == 0ull) continue;
+        const int w = k * 64 + lane;
+        unsigned long long p = 0ull, c = 0ull;
+        int bk = 0;
+        bool cert = false;
+        if ((s >> lane) & 1ull) {
+            const unsigned long long fs = Fsr[w];
+            if (fs) {
+                const unsigned long long f = P.ftvis[row + w];
+                cert = (f & fs) != 0ull;
+                p = P.tvis[row + w] & ~f;
+                c = p & fs;
+                if (c) bk = P.ppre[row + w];
+            }
+        }
+        if (__ballot(cert) != 0ull) return true;
+        const int trow = (w / wr) * tw + (w % wr) * 64;
+        while (__ballot(c != 0ull) != 0ull) {
+            constexpr int NM = 4;
+            unsigned long long mk[NM];
+            int tl[NM];
+#pragma unroll
+            for (int j = 0; j < NM; j++) {
+                tl[j] = -1;
+                if (c) {
+                    const int b = __ffsll((long long)c) - 1;
+                    c &= c - 1;
+                    tl[j] = trow + b;
+                    mk[j] = pm[bk + __popcll(p & ((1ull << b) - 1ull))];
+                    nload++;
+                }
+            }
+            bool h = false;
+#pragma unroll
+            for (int j = 0; j < NM; j++)
+                if (tl[j] >= 0 && (F[tl[j]] & mk[j])) h = true;
+            if (__ballot(h) != 0ull) return true;
+        }
+    }
+    return false;
+}
+
 // V (visited) and X (next level) are per-workgroup bitmaps in HBM (they stay in the L2/MALL; a
 // source touches each word a few times), F (frontier, read by every run test) is in LDS.
 // SPECIAL = false: the graph has no asymmetric nodes (every U_f cell is regular), no exact path.
@@ -926,7 +986,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const int cn = min(CCH, hn - it0);
                     const int myv = lane < cn ? L[it0 + lane] : -1;
                     unsigned long long certain_m = 0ull, pruned_m = 0ull;   // bit j: chunk entry j
-                    if (P.tvis && !P.pmask) {
+                    if (P.tvis && (!P.pmask || P.tvsum)) {   // (wide grids: the row pass in front of the masks)
                         for (int j = 0; j < cn; j += 2) {
                             const int v0 = __builtin_amdgcn_readlane(myv, j);
                             const int v1 = __builtin_amdgcn_readlane(myv, j + 1);
@@ -1018,7 +1078,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                 // no Missing cell in the frontier: in-set meets F iff cells(v) does (the masks)
                                 unsigned nl = 0;
                                 int how = 0;
-                                found = pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+                                found = P.tvsum ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
                             } else if (!found) {
                                 found = special_hit(P, FV, id, x, y, &nr);
                                 if (lane == 0) rt += (unsigned)nr;
@@ -1027,7 +1087,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (P.pmask) {
                             unsigned nl = 0;
                             int how = 0;
-                            found = pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+                            found = P.tvsum ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
                             if (lane == 0) {
                                 ST(14, 1);
                                 if (how == 1) { ST(16, 1); }
@@ -1430,20 +1490,24 @@ __global__ void tile_pcount_kernel(int64_t Ct, int tvw, const unsigned long long
 // Partial-tile masks: for every tile a cell sees only in part (tvis & ~ftvis), the 64-bit mask of the
 // tile's cells it sees, stored at pmask[poff[id] + rank] with rank = partial bits before the tile in
 // row-word then bit order.  One workgroup per node walks the node's runs as tile_vis_kernel does and
-// ORs the per-tile masks into LDS slots (global atomics for a node with more than PM_CAP partial
+// ORs the per-tile masks into LDS slots (global atomics for a node with more than pmcap partial
 // tiles; pmask is zeroed beforehand).  A node's runs are disjoint, so every seen cell is one bit.
-constexpr int PM_CAP = 4096;
+// Dynamic LDS: the partial words and their prefix [tvw] and the slots [pmcap] (tile_pmask_lds).
+constexpr int PM_CAP = 4096;        // slots in LDS up to 1024 cells a side
+constexpr int PM_CAP_WIDE = 8192;   // wider grids (a cell sees ~2,500 partial tiles at 2000^2)
+__host__ __device__ inline size_t tile_pmask_lds(int tvw, int pmcap) { return (size_t)tvw * 12 + (size_t)pmcap * 8; }
 __global__ void __launch_bounds__(64 * TV_WAVES) tile_pmask_kernel(int rows, int tw, int th, const int32_t* node_cell,
                                                                    int64_t n, const int64_t* node_run_start,
                                                                    const int32_t* node_nruns, const Run* pool,
                                                                    const unsigned long long* tvis,
                                                                    const unsigned long long* ftvis, const int64_t* poff,
-                                                                   unsigned long long* pmask) {
-    __shared__ unsigned long long part[256];
-    __shared__ int pre[256];
-    __shared__ unsigned long long lm[PM_CAP];
+                                                                   unsigned long long* pmask, int pmcap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long pmlds[];
     __shared__ int ptotal;
     const int wr = (tw + 63) / 64, tvw = th * wr;
+    unsigned long long* part = pmlds;             // [tvw]
+    unsigned long long* lm = part + tvw;          // [pmcap]
+    int* pre = (int*)(lm + pmcap);                // [tvw]
     constexpr int TB = 64 * TV_WAVES;
     const int tid = threadIdx.x, lane = tid & 63;
     for (int64_t k = blockIdx.x; k < n; k += gridDim.x) {
@@ -1451,22 +1515,24 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_pmask_kernel(int rows, int
         const int id = tile_id_of(c / rows, c % rows, tw);
         __syncthreads();   // the previous node's masks are written out
         if (tid < 64) {
-            // partial words and their exclusive popcount prefix (tvw <= 256: 4 words a lane)
+            // partial words and their exclusive popcount prefix
             int run = 0;
-            for (int kk = 0; kk < 4; kk++) {
+            for (int kk = 0; kk * 64 < tvw; kk++) {
                 const int w = kk * 64 + lane;
                 const unsigned long long p = w < tvw ? (tvis[(size_t)id * tvw + w] & ~ftvis[(size_t)id * tvw + w]) : 0ull;
                 const int cnt = __popcll(p);
                 const int incl = wave_incl_scan(cnt);
-                part[w] = p;
-                pre[w] = run + incl - cnt;
+                if (w < tvw) {
+                    part[w] = p;
+                    pre[w] = run + incl - cnt;
+                }
                 run += __builtin_amdgcn_readlane(incl, 63);
             }
             if (lane == 0) ptotal = run;
         }
         __syncthreads();
         const int P = ptotal;
-        const bool in_lds = P <= PM_CAP;
+        const bool in_lds = P <= pmcap;
         unsigned long long* gout = pmask + poff[id];
         if (in_lds)
             for (int i = tid; i < P; i += TB) lm[i] = 0ull;
@@ -1512,6 +1578,16 @@ __global__ void __launch_bounds__(64 * TV_WAVES) tile_pmask_kernel(int rows, int
         if (in_lds)
             for (int i = tid; i < P; i += TB) gout[i] = lm[i];
     }
+}
+
+// Runs in pool order for the tile search (the scan order released for the wide-grid masks): each cell's
+// first run is its node's first run in the pool.
+__global__ void tile_pool_order_kernel(int rows, int tw, const int32_t* node_cell, int64_t n, const int64_t* node_run_start,
+                                       int64_t* tscan_start) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int c = node_cell[k];
+    tscan_start[tile_id_of(c / rows, c % rows, tw)] = node_run_start[k];
 }
 
 // Tile-to-tile full visibility: row t = AND of the ftvis rows of tile t's regular cells (bit u set
