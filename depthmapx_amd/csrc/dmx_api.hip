@@ -1911,7 +1911,7 @@ static int prepare_tiles(dmx_graph* g) {
         if (ftv)
             if (int rc = prep_allreduce(g, g->ftvis.p, Ct * tvw, DMX_I64)) return rc;
         const char* tt_env = getenv("DMX_VGA_TTVIS");
-        if (ftv && !wide && !(tt_env && atoi(tt_env) == 0)) {
+        if (ftv && !(tt_env && atoi(tt_env) == 0)) {
             HIPCHK(g->ttvis.alloc((size_t)2 * nt * tvw));   // ttvis, then ttany
             hipLaunchKernelGGL(tile_tt_kernel, dim3((unsigned)((nt + 3) / 4)), dim3(256), 0, s, nt, tvw, g->regular_tiles.p,
                                g->ftvis.p, g->tvis.p, g->ttvis.p, g->ttvis.p + (size_t)nt * tvw);
@@ -2049,6 +2049,13 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     P.list = list.p;
     P.tlist = tlist.p;
     P.hint = hint.p;
+    DevBuf<unsigned long long> hintw;   // (wide grids with the masks) mask hints
+    P.hintw = nullptr;
+    if (P.pmask && P.tvsum) {
+        HIPCHK(hintw.alloc((size_t)nt * 64));
+        HIPCHK(hipMemsetAsync(hintw.p, 0, (size_t)nt * 64 * 8, ctx->stream));
+        P.hintw = hintw.p;
+    }
     // chunks of consecutive sources per workgroup, small enough to balance the tail
     P.chunk = 1;   // concurrent workgroups on neighbouring sources share L2 lines and hints
     if (const char* c = getenv("DMX_VGA_CHUNK")) P.chunk = std::max(1, atoi(c));

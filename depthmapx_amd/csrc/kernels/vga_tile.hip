@@ -75,6 +75,8 @@ struct VgaTileParams {
     uint32_t* hint;           // [nt*64] what last hit for a recent source: the scan position of a run, or
                               // (bit 31) a partial-tile mask: tile << 16 | its slot in the cell's list (~0u:
                               // none); shared by all workgroups: a stale value only costs one test
+    unsigned long long* hintw;// [nt*64] wide grids' mask hints (their tile index needs 16 bits): (tile + 1) << 32 |
+                              // slot, 0 none (null below 1024 cells a side)
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
     unsigned long long* fg;   // per workgroup [nt]: the frontier F (vga_tile_kernel<..., FG = true> only)
     int4* queue;              // per workgroup [nt]: (tile, 0, mask lo, mask hi)
@@ -183,6 +185,13 @@ struct FView {
     const unsigned long long* CB;   // [tw*8][wc]: bit ty of column x: tile (x>>3, ty) has one in column x
     int tw, wr, wc;
 };
+#ifndef VGA_WIDE_PAIR
+#define VGA_WIDE_PAIR 1      // wide grids: the mask test takes two row-summary groups a round
+#endif
+#ifndef VGA_WIDE_ROWPASS
+#define VGA_WIDE_ROWPASS 0   // wide grids with masks: 1 = phase C row pass (2 cells a round) before the mask test (2000^2: 2.32 ms a source; 0: 2.17)
+#endif
+
 // A run as one 64-bit word: the runs a loop picks with a non-constant index are kept as separate words and
 // chosen by selects (an indexed private array would live in scratch memory: a store and a load a lane per
 // element and use, ~1 TB a launch at 1000^2 with the spills)
@@ -577,7 +586,7 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
 // takes the row words k*64 + lane whose summary bit is set (the cell's non-zero words) under a frontier tile
 // row; a mask's position is ppre (the word's partial prefix) plus the partial bits before it.  (Regular cells
 // come here after phase C's row pass found no certain hit; special nodes with no Missing cell in the frontier
-// come directly.)  No hint is recorded: a wide grid's tile index does not fit the hint's 15-bit field.
+// come directly.)  A mask that hits is recorded in hintw (the next source's phase B tests it first).
 __device__ __forceinline__ bool pmask_hit_wide(const VgaTileParams& P, const unsigned long long* F,
                                                const unsigned long long* Fsr, int id, unsigned& nload) {
     const int lane = threadIdx.x & 63;
@@ -585,11 +594,64 @@ __device__ __forceinline__ bool pmask_hit_wide(const VgaTileParams& P, const uns
     const size_t row = (size_t)id * tvw;
     const unsigned long long sm = lane < tvsw ? P.tvsum[(size_t)id * tvsw + lane] : 0ull;
     const unsigned long long* pm = P.pmask + P.poff[id];
+    auto sum_word = [&](int k) -> unsigned long long {
+        return (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)sm, k) |
+               ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(sm >> 32), k) << 32);
+    };
+    // the masks of one group's partial frontier tiles, NM a lane in flight; a hit is recorded as a hint
+    auto mask_group = [&](unsigned long long c, unsigned long long p, int bk, int w) -> bool {
+        const int trow = (w / wr) * tw + (w % wr) * 64;
+        while (__ballot(c != 0ull) != 0ull) {
+            constexpr int NM = 4;
+            unsigned long long mk[NM];
+            int tl[NM], sl[NM];
+#pragma unroll
+            for (int j = 0; j < NM; j++) {
+                tl[j] = -1;
+                if (c) {
+                    const int b = __ffsll((long long)c) - 1;
+                    c &= c - 1;
+                    tl[j] = trow + b;
+                    sl[j] = bk + __popcll(p & ((1ull << b) - 1ull));
+                    mk[j] = pm[sl[j]];
+                    nload++;
+                }
+            }
+            int ht = -1, hq = 0;
+#pragma unroll
+            for (int j = NM - 1; j >= 0; j--)
+                if (tl[j] >= 0 && (F[tl[j]] & mk[j])) { ht = tl[j]; hq = sl[j]; }
+            const unsigned long long hb = __ballot(ht >= 0);
+            if (hb != 0ull) {
+                if (P.hintw && lane == __ffsll((long long)hb) - 1)
+                    P.hintw[id] = ((unsigned long long)(ht + 1) << 32) | (unsigned)hq;
+                return true;
+            }
+        }
+        return false;
+    };
+#if VGA_WIDE_PAIR
+    // two summary groups a round: their row-word loads are independent, so they overlap
+#pragma unroll 1
+    for (int k = 0; k < tvsw; k += 2) {
+        const unsigned long long s0 = sum_word(k), s1 = k + 1 < tvsw ? sum_word(k + 1) : 0ull;
+        if ((s0 | s1) == 0ull) continue;
+        const int w0 = k * 64 + lane, w1 = w0 + 64;
+        const unsigned long long fs0 = ((s0 >> lane) & 1ull) ? Fsr[w0] : 0ull;
+        const unsigned long long fs1 = ((s1 >> lane) & 1ull) ? Fsr[w1] : 0ull;
+        unsigned long long f0 = 0ull, t0 = 0ull, f1 = 0ull, t1 = 0ull;
+        if (fs0) { f0 = P.ftvis[row + w0]; t0 = P.tvis[row + w0]; }
+        if (fs1) { f1 = P.ftvis[row + w1]; t1 = P.tvis[row + w1]; }
+        if (__ballot(((f0 & fs0) | (f1 & fs1)) != 0ull) != 0ull) return true;
+        const unsigned long long p0 = t0 & ~f0, c0 = p0 & fs0, p1 = t1 & ~f1, c1 = p1 & fs1;
+        const int b0 = c0 ? (int)P.ppre[row + w0] : 0, b1 = c1 ? (int)P.ppre[row + w1] : 0;
+        if (mask_group(c0, p0, b0, w0)) return true;
+        if (mask_group(c1, p1, b1, w1)) return true;
+    }
+#else
 #pragma unroll 1
     for (int k = 0; k < tvsw; k++) {
-        const unsigned long long s =
-            (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)sm, k) |
-            ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(sm >> 32), k) << 32);
+        const unsigned long long s = sum_word(k);
         if (s == 0ull) continue;
         const int w = k * 64 + lane;
         unsigned long long p = 0ull, c = 0ull;
@@ -606,29 +668,9 @@ __device__ __forceinline__ bool pmask_hit_wide(const VgaTileParams& P, const uns
             }
         }
         if (__ballot(cert) != 0ull) return true;
-        const int trow = (w / wr) * tw + (w % wr) * 64;
-        while (__ballot(c != 0ull) != 0ull) {
-            constexpr int NM = 4;
-            unsigned long long mk[NM];
-            int tl[NM];
-#pragma unroll
-            for (int j = 0; j < NM; j++) {
-                tl[j] = -1;
-                if (c) {
-                    const int b = __ffsll((long long)c) - 1;
-                    c &= c - 1;
-                    tl[j] = trow + b;
-                    mk[j] = pm[bk + __popcll(p & ((1ull << b) - 1ull))];
-                    nload++;
-                }
-            }
-            bool h = false;
-#pragma unroll
-            for (int j = 0; j < NM; j++)
-                if (tl[j] >= 0 && (F[tl[j]] & mk[j])) h = true;
-            if (__ballot(h) != 0ull) return true;
-        }
+        if (mask_group(c, p, bk, w)) return true;
     }
+#endif
     return false;
 }
 
@@ -855,6 +897,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     int64_t ss = 0;
                     int nr = 0;
                     uint32_t hp = 0xFFFFFFFFu;
+                    unsigned long long hmw = 0ull;   // (wide grids) a mask hint
                     int64_t pof = 0;
                     // heads loaded with the cell's first loads, the rest of the KH heads in the extension loop
                     // (round 4 at 1000^2: 4 -> 2 heads 4.67 -> 4.60 s, fewer live registers at the head tests)
@@ -864,6 +907,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         ss = P.tscan_start[id];
                         nr = P.tnruns[id];
                         hp = Hn[id];
+                        if (P.hintw) hmw = P.hintw[id];
                         if (P.pmask) pof = P.poff[id];
                         hd0 = run_word(P.heads + id);
                         hd1 = run_word(P.heads + hstride + id);
@@ -871,13 +915,25 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     unsigned long long acc = 0ull, acca = ~0ull;
                     if (P.ttvis) {
                         acca = 0ull;
+                        if (P.tvw <= 256) {
 #pragma unroll
-                        for (int k = 0; k < 4; k++) {
-                            const int w = k * 64 + lane;
-                            const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
-                            if (fs) {
-                                acc |= P.ttvis[(size_t)t * P.tvw + w] & fs;
-                                acca |= P.ttany[(size_t)t * P.tvw + w] & fs;
+                            for (int k = 0; k < 4; k++) {
+                                const int w = k * 64 + lane;
+                                const unsigned long long fs = w < P.tvw ? Fsr[w] : 0ull;
+                                if (fs) {
+                                    acc |= P.ttvis[(size_t)t * P.tvw + w] & fs;
+                                    acca |= P.ttany[(size_t)t * P.tvw + w] & fs;
+                                }
+                            }
+                        } else {
+                            // wide rows (above 1024 cells a side): the words under frontier tile rows, 64 a round
+#pragma unroll 1
+                            for (int w = lane; w < P.tvw; w += 64) {
+                                const unsigned long long fs = Fsr[w];
+                                if (fs) {
+                                    acc |= P.ttvis[(size_t)t * P.tvw + w] & fs;
+                                    acca |= P.ttany[(size_t)t * P.tvw + w] & fs;
+                                }
                             }
                         }
                     }
@@ -907,7 +963,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         hr.x0 = -1;
                         unsigned long long hmk = 0ull;
                         int htile = -1;
-                        if (hp != 0xFFFFFFFFu && (hp >> 31)) {
+                        if (hmw && P.pmask) {
+                            htile = (int)(hmw >> 32) - 1;
+                            hmk = P.pmask[pof + (uint32_t)hmw];
+                        } else if (hp != 0xFFFFFFFFu && (hp >> 31)) {
                             if (P.pmask) { htile = (int)((hp >> 16) & 0x7FFFu); hmk = P.pmask[pof + (hp & 0xFFFFu)]; }
                         } else if (hp >= KH && hp < (uint32_t)nr) {
                             hr = P.scan_pool[ss + hp];
@@ -986,7 +1045,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const int cn = min(CCH, hn - it0);
                     const int myv = lane < cn ? L[it0 + lane] : -1;
                     unsigned long long certain_m = 0ull, pruned_m = 0ull;   // bit j: chunk entry j
-                    if (P.tvis && (!P.pmask || P.tvsum)) {   // (wide grids: the row pass in front of the masks)
+                    if (P.tvis && (!P.pmask || (VGA_WIDE_ROWPASS && P.tvsum))) {   // (wide grids: a row pass in front of the masks)
                         for (int j = 0; j < cn; j += 2) {
                             const int v0 = __builtin_amdgcn_readlane(myv, j);
                             const int v1 = __builtin_amdgcn_readlane(myv, j + 1);
