@@ -72,15 +72,15 @@ def nearest_filled(pm, x, y):
     raise RuntimeError("no filled cell")
 
 
-# the newest round's PMC summary of the shipped build (scripts/gpu_r4_evidence.sh writes r4)
-PMC_SUMMARY = next((p for p in (os.path.join(REPO, "profiles", "r%d_pmc.json" % r) for r in (4, 3)) if os.path.exists(p)),
-                   os.path.join(REPO, "profiles", "r4_pmc.json"))
+# the newest round's PMC summary of the shipped build (scripts/gpu_r5_evidence.sh writes r5)
+PMC_SUMMARY = next((p for p in (os.path.join(REPO, "profiles", "r%d_pmc.json" % r) for r in (5, 4, 3)) if os.path.exists(p)),
+                   os.path.join(REPO, "profiles", "r5_pmc.json"))
 FP64_PEAK_TF = 78.6    # MI355X FP64 vector (MI355X_MICROARCH.md)
 
 
 def load_pmc(workload):
     """Per-kernel PMC summary of the same workload and build (scripts/gpu_pmc.sh -> scripts/pmc_summary.py ->
-    profiles/r4_pmc.json): HBM bytes raw and 2x-FETCH corrected, L2 hit rate, VALU issue, FP64 instruction
+    profiles/r5_pmc.json): HBM bytes raw and 2x-FETCH corrected, L2 hit rate, VALU issue, FP64 instruction
     counts."""
     if not os.path.exists(PMC_SUMMARY):
         return {}
@@ -359,6 +359,8 @@ def main():
             g.vga_visual_global_device(out_full.data_ptr())
         t_vga = ctx.last_timing()[1]
         st.update({k: v for k, v in ctx.last_stats().items() if k.startswith("vga")})
+        if mk_auto is not None and "sym_s" not in mk_auto and "mk_shard_s" in mk_auto:
+            mk_auto["sym_s"] = st.get("vga_sym_scatter_us", 0) * 1e-6   # the sharded warm-up's scatter
         # 4. all-gather the 7 float columns
         if world > 1:
             allgather_rows_chunked(out_full, N, dist)
@@ -382,7 +384,7 @@ def main():
         if w == 0 and mk_auto is not None:
             mk_mode, dec = choose_mk_mode(dist, dev, world, mk_auto["mk_shard_s"], mk_auto["blob_s"] +
                                           mk_auto["allgather_s"] + mk_auto["assemble_s"],
-                                          (shard_be[1] - shard_be[0]) / max(N, 1))
+                                          (shard_be[1] - shard_be[0]) / max(N, 1), mk_auto.get("sym_s", 0.0))
             mk_auto.update(dec)
             mk_auto["chosen"] = mk_mode
     torch.cuda.synchronize()

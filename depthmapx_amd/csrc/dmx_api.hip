@@ -1632,7 +1632,9 @@ static int prepare_symmetry(dmx_graph* g) {
         // so no all-reduce either
         diff = g->sym_diff.p;
         ho = g->sym_ho.p;
+        ctx->last_stats[39] = 0;
     } else {
+        const double t_sym = now_s();   // the scatter a sharded or assembled graph pays here (last_stats[39])
         HIPCHK(prefix.alloc((size_t)4 * C));
         HIPCHK(diff_own.alloc((size_t)4 * C));
         HIPCHK(ho_own.alloc(std::max<int64_t>(N, 1)));
@@ -1653,6 +1655,8 @@ static int prepare_symmetry(dmx_graph* g) {
         }
         if (int rc = prep_allreduce(g, diff, (int64_t)4 * C, DMX_I64)) return rc;
         if (int rc = prep_allreduce(g, ho, N, DMX_I64)) return rc;
+        HIPCHK(hipStreamSynchronize(s));
+        ctx->last_stats[39] = (long long)((now_s() - t_sym) * 1e6);
     }
     hipLaunchKernelGGL(sym_lines_kernel, dim3((maxlines + 127) / 128, 4), dim3(128), 0, s, cols, rows,
                        g->pm->d_cell_node.p, diff, 1);

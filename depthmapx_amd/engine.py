@@ -110,7 +110,7 @@ class Context:
                 "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",
                 "vga_hard_cells", "vga_hard_certain", "vga_topdown_cycles", "vga_b_tiles", "vga_b_cells", "vga_tt_tiles", "vga_c_busy", "vga_c_scan", "vga_c_spec", "vga_n_spec", "vga_tt_pruned", "vga_b_row_cycles", "vga_b_cell_tiles",
                 "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks", "mk_reruns", "vga_pmask_loads", "vga_pmask_cells", "vga_pmask_bytes",
-                "vga_order_reruns"]
+                "vga_order_reruns", "vga_sym_scatter_us"]
         # vga_c_scan, vga_c_spec, vga_b_row_cycles and vga_b_cell_cycles stay 0: the kernel no longer reads
         # the clock per hard cell or per tile (2.6 % of the 1000^2 VGA); the per-phase clocks remain
         d = {k: int(v) for k, v in zip(keys, out)}

@@ -98,19 +98,28 @@ def exchange_graph(pm, ctx, shard, dist, device):
                "padded_bytes": world * mx, "device_peak_bytes": peak[0] if cuda else None}
 
 
-def choose_mk_mode(dist, device, world, mk_shard_s, exchange_s, shard_frac):
+# a whole-graph makeGraph does the VGA preparation's symmetry scatter as it publishes the runs (DESIGN.md section 2,
+# prep): +0.9 % of its time at 1000^2 (4.62 -> 4.66 s, round 4), where a shard leaves it to the preparation
+FUSED_SCATTER_COST = 1.009
+
+
+def choose_mk_mode(dist, device, world, mk_shard_s, exchange_s, shard_frac, sym_shard_s=0.0):
     """--mk-mode auto after a warm-up step run sharded: replicate (every rank builds the whole graph, no
     data-path collective) when building it all costs less than building the shard and exchanging it.
-    Times are the max over ranks so that every rank takes the same branch."""
-    t = torch.tensor([mk_shard_s, exchange_s, shard_frac], dtype=torch.float64,
+    The sharded step also pays the symmetry scatter in the VGA preparation (sym_shard_s, measured in the
+    warm-up: the rank's share plus the all-reduces of its difference arrays), which a whole-graph build does
+    inside makeGraph for FUSED_SCATTER_COST.  Times are the max over ranks so that every rank takes the same
+    branch."""
+    t = torch.tensor([mk_shard_s, exchange_s, shard_frac, sym_shard_s], dtype=torch.float64,
                      device=device if _rccl(dist) else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    mk, ex, frac = (float(v) for v in t.tolist())
-    replicate_s = mk / max(frac, 1e-9)
-    shard_s = mk + ex
+    mk, ex, frac, sym = (float(v) for v in t.tolist())
+    replicate_s = mk / max(frac, 1e-9) * FUSED_SCATTER_COST
+    shard_s = mk + ex + sym
     return ("replicate" if replicate_s < shard_s else "shard"), {"predicted_replicate_s": replicate_s,
                                                                  "predicted_shard_s": shard_s,
-                                                                 "mk_shard_s": mk, "exchange_s": ex}
+                                                                 "mk_shard_s": mk, "exchange_s": ex,
+                                                                 "sym_shard_s": sym}
 
 
 def device_view(ptr, count, dtype, device):

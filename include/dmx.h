@@ -82,7 +82,8 @@ int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
  * [10] bitmaps in HBM (direction-optimising), [11] tiles resolved by common runs, [12] launch
  * shape, [13] hard cells rejected by their tile-visibility row, [14] bytes of those rows read,
  * [15] runs scanned by hard cells, [16] hard cells that hit, [17] hard cells, ... [38] searches the last VGA
- * global / visual step depth call ran again in the reference's level order (vga_ordered.hip). */
+ * global / visual step depth call ran again in the reference's level order (vga_ordered.hip), [39] microseconds
+ * the last VGA preparation spent on the symmetry scatter and its all-reduces (0 when makeGraph did it). */
 int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
 
 /* The sources the last makeGraph swept a second time (graph node indices, in the order the passes listed

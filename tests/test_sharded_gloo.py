@@ -87,6 +87,10 @@ def _worker(rank, world, port, q):
     om.set_graph(bins, runs)
     # --mk-mode auto: ranks measure different times but must take the same branch
     mode, dec = choose_mk_mode(dist, torch.device("cpu"), world, 1.0 + rank, 0.5 * rank, (e - b) / N)
+    # the sharded step's symmetry scatter (VGA preparation) counts against sharding: a large one flips it
+    mode_sym, dec_sym = choose_mk_mode(dist, torch.device("cpu"), world, 1.0 + rank, 0.5 * rank, (e - b) / N,
+                                       100.0 * (rank + 1))
+    assert mode_sym == "replicate" and dec_sym["sym_shard_s"] == 100.0 * world
     out = torch.full((N, 7), -1.0)
     # VGA sources: 16-node chunks dealt round-robin (bench.py uses 4096)
     mine = vga_nodes(N, rank, world, chunk=16)
