@@ -23,6 +23,9 @@
 
 namespace dmx {
 
+#ifndef MK_PFIND
+#define MK_PFIND 1   // the prefetch also keeps the first chunk's candidate index and gap bounds in registers (A/B hook)
+#endif
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
 // open-run state of rows 0 .. MK_OPEN_LDS-1 lives in LDS, of farther rows (grids above ~1020 cells a
 // side) in per-wave scratch memory: rows past 1024 are reached only by sight lines longer than 1024
@@ -503,6 +506,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             // next depth's candidates are known before its collectgarbage, and they stay the same
             // when that adds no block (nb == 0: the gap list is unchanged)
             uint32_t pf_w = 0;
+#if MK_PFIND
+            int pf_ind = 0;                     // the prefetched depth's first chunk: candidate index and gap bounds
+            int2 pf_gc = make_int2(0, -1);
+#endif
             bool pf_ok = false;
             int pf_T = 0;   // candidates of the prefetched depth (its ranges are in L.ga / gpre / gc)
             for (;;) {
@@ -756,9 +763,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     bool ingrid = false, add = false;
                     uint32_t w = 0;
                     if (valid) {
-                        while (L.gpre[gcur + 1] <= t) gcur++;
-                        ind = L.ga[gcur] + (t - L.gpre[gcur]);
-                        gcr = L.gc[gcur];
+#if MK_PFIND
+                        if (pf_ok && t0 == 0) {   // the prefetch laid this chunk out already
+                            ind = pf_ind;
+                            gcr = pf_gc;
+                        } else
+#endif
+                        {
+                            while (L.gpre[gcur + 1] <= t) gcur++;
+                            ind = L.ga[gcur] + (t - L.gpre[gcur]);
+                            gcr = L.gc[gcur];
+                        }
                         octant_cell(q, cx, cy, depth, ind, hx, hy);
                         ingrid = (hx >= 0 && hx < P.cols && hy >= 0 && hy < P.rows);
                     }
@@ -913,16 +928,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         const int b = min(hi, d1);
                         const int a = max(lo, F1);
                         const int c = (b >= a) ? (b - a + 1) : 0;
-                        if (lane >= T1 && lane < T1 + c) pind = a + (lane - T1);
+                        const int2 gcg = make_int2((int)ceil(z.x * d1), (int)floor(z.y * d1));
+                        if (lane >= T1 && lane < T1 + c) {
+                            pind = a + (lane - T1);
+#if MK_PFIND
+                            pf_gc = gcg;
+#endif
+                        }
                         if (lane == 0) {   // depth d1's visit ranges, reused if no block changes the gaps
                             L.ga[g] = a;
                             L.gpre[g] = T1;
-                            L.gc[g] = make_int2((int)ceil(z.x * d1), (int)floor(z.y * d1));
+                            L.gc[g] = gcg;
                         }
                         T1 += c;
                         if (b >= lo) F1 = max(F1, b);
                     }
                     pf_T = T1;
+#if MK_PFIND
+                    pf_ind = pind;
+#endif
                     if (pind >= 0) {
                         int px, py;
                         octant_cell(q, cx, cy, d1, pind, px, py);
