@@ -206,7 +206,8 @@ bool vgaVisualGlobal(PointMap& map, Communicator* comm, double radius, bool gate
     {
         ScopedProgress sp(ctx, comm);
         const int rc = dmx_vga_global(ctx, g.p, radius, gates_only ? 1 : 0, 0, -1, out.data(), nullptr);
-        // merge links on context-filled cells with a radius (pop-order dependent): the reference path
+        // a configuration the engine does not take (none on this path since round 5: the searches whose result
+        // depends on the reference's pop order are re-run in that order, vga_ordered.hip): the reference path
         if (rc == DMX_ERR_UNSUPPORTED) return false;
         check(rc);
     }

@@ -389,6 +389,33 @@ def test_2000_vga_sources_match_oracle(big2000, ctx):
     np.testing.assert_array_equal(got[:, 5], want[:, 5])
     assert (np.abs(got - want) <= 1e-6 * np.maximum(1.0, np.abs(want))).all()
     assert (want[:, 5] > 0.5 * N).all()
+    # the wide-grid partial-tile masks decided cells (they take the scan order's place at this size)
+    assert st["vga_pmask_cells"] > 0, st
+
+
+def test_2000_vga_masks_release_and_restore_the_scan_order(big2000, ctx, monkeypatch):
+    """Above 1024^2 the partial-tile masks take the scan order's memory (prepare_pmask releases it and the tile
+    search reads runs in pool order); the direction-optimising kernel reads the scan order itself, so a vga_do
+    call frees the tile data and rebuilds it (restore_scan_order), and the next tile call builds the masks
+    again.  The three answers on the same sources are bit-identical."""
+    pm, g, om = big2000
+    N = g.info()["nnodes"]
+    b = N // 3   # (the source-range entry point honours DMX_VGA_KERNEL; the list entry point takes the tile path)
+
+    def run():
+        out = g.vga_visual_global(src_begin=b, src_end=b + 4)
+        return out[b:b + 4].copy(), ctx.last_stats()
+
+    a, st_a = run()
+    assert st_a["vga_kernel"] == "tile-resolved" and st_a["vga_pmask_cells"] > 0, st_a
+    monkeypatch.setenv("DMX_VGA_KERNEL", "do")
+    b, st_b = run()
+    assert st_b["vga_kernel"] != "tile-resolved", st_b
+    monkeypatch.delenv("DMX_VGA_KERNEL")
+    c, st_c = run()
+    assert st_c["vga_kernel"] == "tile-resolved" and st_c["vga_pmask_cells"] > 0, st_c
+    np.testing.assert_array_equal(a.view(np.uint32), b.view(np.uint32))
+    np.testing.assert_array_equal(a.view(np.uint32), c.view(np.uint32))
 
 
 def test_2000_metric_stepdepth_matches_oracle(big2000, ctx):
