@@ -1818,6 +1818,25 @@ static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_
     return DMX_OK;
 }
 
+// LDS of the tile BFS workgroup: the frontier bitmap (unless FG), the tile-row summary Fsr, then either the
+// per-tile column summary Fsc or the line-resolved summaries RB / CB, then the level histogram.  Returns the
+// bytes (0: does not fit) and the variant: *fg the frontier in HBM, *rbm the line summaries.
+static size_t tile_lds_layout(int tw, int th, bool* fg, bool* rbm) {
+    const size_t nt = (size_t)tw * th, wr_ = (tw + 63) / 64, wc_ = (th + 63) / 64;
+    const size_t lds_f = nt * 8, lds_h = (size_t)VGA_HMAX * 4;
+    const size_t lds_sc = (size_t)(th * wr_ + tw * wc_) * 8, lds_rbcb = (size_t)(th * wr_ + th * 8 * wr_ + tw * 8 * wc_) * 8;
+    const size_t lds_cap = (size_t)160 * 1024 - 1024;
+    const char* rb_env = getenv("DMX_VGA_RB");
+    const bool rb_ok = !(rb_env && atoi(rb_env) == 0);
+    *fg = false;
+    *rbm = false;
+    if (rb_ok && lds_f + lds_rbcb + lds_h <= lds_cap) { *rbm = true; return lds_f + lds_rbcb + lds_h; }
+    if (lds_f + lds_sc + lds_h <= lds_cap) return lds_f + lds_sc + lds_h;
+    if (rb_ok && lds_rbcb + lds_h <= lds_cap) { *fg = true; *rbm = true; return lds_rbcb + lds_h; }
+    if (lds_sc + lds_h <= lds_cap) { *fg = true; return lds_sc + lds_h; }
+    return 0;
+}
+
 // Tile-ordered per-cell arrays, head runs and tile-common runs for vga_tile_kernel (O(runs)).
 static int prepare_tiles(dmx_graph* g) {
     if (g->tiles_ready) return DMX_OK;
@@ -1876,7 +1895,11 @@ static int prepare_tiles(dmx_graph* g) {
     // test) when both leave 24 GiB free for the search's own buffers.
     const bool wide = tvw > 256;
     const size_t free_all = free_b + cached_bytes();
-    bool ftv = ftv_on && (!wide || 2 * tv_bytes + (24ull << 30) <= free_all);
+    // (the wide-grid ftvis, tile rows and masks serve the HBM-frontier variant, whose code reads wide rows; a
+    // wide grid whose frontier fits the LDS -- a few tiles high, very long -- keeps tvis alone)
+    bool fg_grid = false, rbm_grid = false;
+    tile_lds_layout(tw, th, &fg_grid, &rbm_grid);
+    bool ftv = ftv_on && (!wide || (fg_grid && 2 * tv_bytes + (24ull << 30) <= free_all));
     bool tv_build = tv_on && N && tv_bytes <= (32ull << 30) &&
                     (wide ? tv_bytes <= free_all / 3 : tv_bytes * (ftv ? 2 : 1) <= free_b / 4);
     if (g->prep_fn) {
@@ -2148,21 +2171,9 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     HIPCHK(d_hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));
     HIPCHK(d_nlev.alloc(std::max<int64_t>(N, 1)));
     Q.maxlev = maxlev; Q.hist_out = d_hist.p; Q.nlev_out = d_nlev.p; Q.stats = ctx->stats.p;
-    const size_t wr_ = (tw + 63) / 64, wc_ = (th + 63) / 64;
-    // LDS: the frontier bitmap (unless FG), the tile-row summary Fsr, then either the per-tile column summary
-    // Fsc or the line-resolved summaries RB / CB, then the level histogram
-    const size_t lds_f = (size_t)nt * 8, lds_h = (size_t)VGA_HMAX * 4;
-    const size_t lds_sc = (size_t)(th * wr_ + tw * wc_) * 8, lds_rbcb = (size_t)(th * wr_ + th * 8 * wr_ + tw * 8 * wc_) * 8;
-    const size_t lds_cap = (size_t)160 * 1024 - 1024;
-    const char* rb_env = getenv("DMX_VGA_RB");
-    const bool rb_ok = !(rb_env && atoi(rb_env) == 0);
     bool fg = false, rbm = false;
-    size_t L = 0;
-    if (rb_ok && lds_f + lds_rbcb + lds_h <= lds_cap) { rbm = true; L = lds_f + lds_rbcb + lds_h; }
-    else if (lds_f + lds_sc + lds_h <= lds_cap) { L = lds_f + lds_sc + lds_h; }
-    else if (rb_ok && lds_rbcb + lds_h <= lds_cap) { fg = true; rbm = true; L = lds_rbcb + lds_h; }
-    else if (lds_sc + lds_h <= lds_cap) { fg = true; L = lds_sc + lds_h; }
-    else return fail(DMX_ERR_CAPACITY, "grid too large for the tile BFS's LDS summaries");
+    const size_t L = tile_lds_layout(tw, th, &fg, &rbm);
+    if (!L) return fail(DMX_ERR_CAPACITY, "grid too large for the tile BFS's LDS summaries");
     // With the frontier in HBM a top-down level's run rasterisation takes global atomics: past level 1 the
     // bottom-up levels win (2000^2 interior block: alpha 60 -> 200: 2.70 -> 2.28 s, identical output;
     // 1000 and 100000 the same, profiles/r5_vga2000_alpha.jsonl)

@@ -907,7 +907,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         ss = P.tscan_start[id];
                         nr = P.tnruns[id];
                         hp = Hn[id];
-                        if (P.hintw) hmw = P.hintw[id];
+                        if (FG && P.hintw) hmw = P.hintw[id];
                         if (P.pmask) pof = P.poff[id];
                         hd0 = run_word(P.heads + id);
                         hd1 = run_word(P.heads + hstride + id);
@@ -915,7 +915,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     unsigned long long acc = 0ull, acca = ~0ull;
                     if (P.ttvis) {
                         acca = 0ull;
-                        if (P.tvw <= 256) {
+                        if (!FG) {   // (the host drops ttvis for a wide grid whose frontier fits the LDS)
 #pragma unroll
                             for (int k = 0; k < 4; k++) {
                                 const int w = k * 64 + lane;
@@ -963,7 +963,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         hr.x0 = -1;
                         unsigned long long hmk = 0ull;
                         int htile = -1;
-                        if (hmw && P.pmask) {
+                        if (FG && hmw && P.pmask) {
                             htile = (int)(hmw >> 32) - 1;
                             hmk = P.pmask[pof + (uint32_t)hmw];
                         } else if (hp != 0xFFFFFFFFu && (hp >> 31)) {
@@ -1045,7 +1045,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const int cn = min(CCH, hn - it0);
                     const int myv = lane < cn ? L[it0 + lane] : -1;
                     unsigned long long certain_m = 0ull, pruned_m = 0ull;   // bit j: chunk entry j
-                    if (P.tvis && (!P.pmask || (VGA_WIDE_ROWPASS && P.tvsum))) {   // (wide grids: a row pass in front of the masks)
+                    if (P.tvis && (!P.pmask || (FG && VGA_WIDE_ROWPASS && P.tvsum))) {   // (wide grids: a row pass in front of the masks)
                         for (int j = 0; j < cn; j += 2) {
                             const int v0 = __builtin_amdgcn_readlane(myv, j);
                             const int v1 = __builtin_amdgcn_readlane(myv, j + 1);
@@ -1137,7 +1137,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                 // no Missing cell in the frontier: in-set meets F iff cells(v) does (the masks)
                                 unsigned nl = 0;
                                 int how = 0;
-                                found = P.tvsum ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+                                found = (FG && P.tvsum) ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
                             } else if (!found) {
                                 found = special_hit(P, FV, id, x, y, &nr);
                                 if (lane == 0) rt += (unsigned)nr;
@@ -1146,7 +1146,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (P.pmask) {
                             unsigned nl = 0;
                             int how = 0;
-                            found = P.tvsum ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+                            found = (FG && P.tvsum) ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
                             if (lane == 0) {
                                 ST(14, 1);
                                 if (how == 1) { ST(16, 1); }
