@@ -400,11 +400,11 @@ def test_2000_vga_masks_release_and_restore_the_scan_order(big2000, ctx, monkeyp
     again.  The three answers on the same sources are bit-identical."""
     pm, g, om = big2000
     N = g.info()["nnodes"]
-    b = N // 3   # (the source-range entry point honours DMX_VGA_KERNEL; the list entry point takes the tile path)
+    s0 = N // 3   # (the source-range entry point honours DMX_VGA_KERNEL; the list entry point takes the tile path)
 
     def run():
-        out = g.vga_visual_global(src_begin=b, src_end=b + 4)
-        return out[b:b + 4].copy(), ctx.last_stats()
+        out = g.vga_visual_global(src_begin=s0, src_end=s0 + 4)
+        return out[s0:s0 + 4].copy(), ctx.last_stats()
 
     a, st_a = run()
     assert st_a["vga_kernel"] == "tile-resolved" and st_a["vga_pmask_cells"] > 0, st_a
