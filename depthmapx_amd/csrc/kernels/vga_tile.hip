@@ -1162,7 +1162,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else {
                             const int64_t rs = P.tscan_start[id];
                             nr = P.tnruns[id];
-                            int base = KH + P.bext;   // the first KH + bext runs were tested in phase B
+                            // the first KH + bext runs were tested in phase B (in pool order -- the scan order
+                            // released for the masks -- the heads are not the first runs: scan them all)
+                            int base = P.scan_pool == P.pool ? 0 : KH + P.bext;
                             for (; base < nr && !found; base += CSTEP * 64) {
                                 Run rr[CSTEP];
 #pragma unroll
