@@ -98,6 +98,11 @@ def _release(ctx, *objs):
     N.lib().dmx_release_cached_memory()
 
 
+# module-scoped graphs still alive; the 2000^2 fixture closes the 1000^2 one first (the 1000^2 tests come first in
+# this file): its ~90 GB would otherwise leave no room for the 2000^2 partial-tile masks
+_LIVE = {}
+
+
 @pytest.fixture(scope="module")
 def big1000(ctx):
     from pyoracle import OracleMap
@@ -109,8 +114,10 @@ def big1000(ctx):
     g.reruns = ctx.last_mk_reruns()
     om = OracleMap(region, 1.0, lines)
     assert om.fill(0.5, 0.5)
+    _LIVE["1000"] = g
     yield pm, g, om
-    _release(ctx, g)
+    if _LIVE.pop("1000", None) is not None:
+        _release(ctx, g)
 
 
 def test_1000_makegraph_blocks_match_oracle(big1000):
@@ -274,6 +281,9 @@ def test_1000_vga_per_tile_summary_path_agrees(big1000, ctx, monkeypatch):
 
 @pytest.fixture(scope="module")
 def big2000(ctx):
+    g1000 = _LIVE.pop("1000", None)
+    if g1000 is not None:
+        _release(ctx, g1000)
     from pyoracle import OracleMap
     lines = read_csv_lines(os.path.join(GOLDEN, "inputs", "syn2000_5000.csv"))
     region = [0.0, 0.0, 1999.0, 1999.0]
