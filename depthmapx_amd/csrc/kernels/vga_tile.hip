@@ -185,6 +185,9 @@ struct FView {
     const unsigned long long* CB;   // [tw*8][wc]: bit ty of column x: tile (x>>3, ty) has one in column x
     int tw, wr, wc;
 };
+#ifndef VGA_CCH
+#define VGA_CCH 16           // phase C: hard-list entries a wave takes at once (1000^2 VGA: 8 -> 4.133 s, 16 -> 4.143, 32 -> 4.218)
+#endif
 #ifndef VGA_WIDE_PAIR
 #define VGA_WIDE_PAIR 1      // wide grids: the mask test takes two row-summary groups a round
 #endif
@@ -1032,7 +1035,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 // flight): a frontier tile the cell sees completely is a certain hit (regular cell:
                 // in-set == out-set), no tile in view holding a frontier cell a certain miss.  C1
                 // scans the run lists of the undecided cells, CSTEP * 64 runs a step (CSTEP loads a lane).
-                constexpr int CCH = 16;
+                constexpr int CCH = VGA_CCH;
                 // runs a lane loads per scan step (1000^2: 4 -> 9.61 s, 8 -> 9.71 s, 16 -> 14.6 s: more loads
                 // in flight per round trip do not pay for the registers and the over-read past the first hit)
                 constexpr int CSTEP = 4;
