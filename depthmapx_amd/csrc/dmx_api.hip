@@ -193,7 +193,7 @@ struct dmx_ctx {
     long long phase_cycles[5] = {0, 0, 0, 0, 0};   // tile BFS: level 1, A, B, C, bookkeeping (sum over workgroups)
     DevBuf<int> counters;   // [0] work counter, [1] error word, [2..3] pool cursor (u64)
     DevBuf<unsigned long long> stats; // [0..1] makegraph, [4..6] vga
-    long long last_stats[40] = {};
+    long long last_stats[48] = {};
     std::vector<int64_t> last_mk_reruns;   // sources the last makeGraph re-ran (MK_CAPACITY_TAG: capacity)
     // progress / cancel (dmx_ctx_set_progress, dmx_ctx_cancel): host-mapped block polled by the kernels
     DmxCtl* h_ctl = nullptr;
@@ -336,6 +336,51 @@ int prepare_merges(dmx_graph* g) {
     return DMX_OK;
 }
 
+// makeGraph's span certificate (makegraph.hip): every clean cell (FILLED, no occluder piece) gets in its cell
+// word, in place of the unused segment offset, its clean distance -- the Chebyshev distance to the nearest cell
+// that is not clean or lies outside the grid.  Two raster passes of the 8-neighbour chamfer (Rosenfeld-Pfaltz),
+// exact for the Chebyshev metric; the outside enters as each cell's distance to the border.
+static void clean_distance(const PointMapHost& h, std::vector<uint32_t>& cellw) {
+    const int W = h.cols(), H = h.rows();
+    std::vector<uint32_t> d((size_t)W * H);
+    for (int x = 0; x < W; x++)
+        for (int y = 0; y < H; y++) {
+            const size_t c = (size_t)x * H + y;
+            const bool clean = (cellw[c] & 0xFFu) == 1u;   // FILLED, 0 pieces
+            d[c] = clean ? (uint32_t)std::min(std::min(x + 1, y + 1), std::min(W - x, H - y)) : 0u;
+        }
+    for (int x = 0; x < W; x++)
+        for (int y = 0; y < H; y++) {
+            const size_t c = (size_t)x * H + y;
+            uint32_t v = d[c];
+            if (!v) continue;
+            if (y > 0) v = std::min(v, d[c - 1] + 1);
+            if (x > 0) {
+                const size_t l = c - H;
+                v = std::min(v, d[l] + 1);
+                if (y > 0) v = std::min(v, d[l - 1] + 1);
+                if (y + 1 < H) v = std::min(v, d[l + 1] + 1);
+            }
+            d[c] = v;
+        }
+    for (int x = W - 1; x >= 0; x--)
+        for (int y = H - 1; y >= 0; y--) {
+            const size_t c = (size_t)x * H + y;
+            uint32_t v = d[c];
+            if (!v) continue;
+            if (y + 1 < H) v = std::min(v, d[c + 1] + 1);
+            if (x + 1 < W) {
+                const size_t r = c + H;
+                v = std::min(v, d[r] + 1);
+                if (y > 0) v = std::min(v, d[r - 1] + 1);
+                if (y + 1 < H) v = std::min(v, d[r + 1] + 1);
+            }
+            d[c] = v;
+        }
+    for (size_t c = 0; c < d.size(); c++)
+        if ((cellw[c] & 0xFFu) == 1u) cellw[c] = (std::min(d[c], CELL_DIST_MAX) << 8) | 1u;
+}
+
 int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
     PointMapHost& h = *pm->host;
     if (!h.lines_blocked()) h.block_lines();
@@ -366,6 +411,7 @@ int upload_pointmap(dmx_ctx* ctx, dmx_pointmap* pm) {
         }
     }
     pm->nnodes = (int64_t)pm->node_cell.size();
+    clean_distance(h, cellw);
     // seed bitmap for the BFS: 1 = not a filled cell (or padding), 8x8 tiles
     const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
     std::vector<unsigned long long> seed((size_t)tw * th, ~0ull), nonexp((size_t)tw * th, 0ull);
@@ -604,7 +650,7 @@ int dmx_ctx_free(dmx_ctx* c) {
 
 int dmx_ctx_last_stats(dmx_ctx* c, int64_t* out, int n) {
     if (!c || !out) return fail(DMX_ERR_ARG, "bad arguments");
-    for (int i = 0; i < n && i < 40; i++) out[i] = c->last_stats[i];
+    for (int i = 0; i < n && i < 48; i++) out[i] = c->last_stats[i];
     return DMX_OK;
 }
 
@@ -920,7 +966,12 @@ static int mk_sqrt_err(dmx_ctx* ctx, long long nmax, double* err) {
         HIPCHK(copy_sync(ctx->stream, &bits, e.p, 8, hipMemcpyDeviceToHost));
         double v;
         std::memcpy(&v, &bits, 8);
-        if (!(v >= 0.0 && v < 0x1p-30)) return fail(DMX_ERR_STATE, "internal: the device square root is not accurate enough");
+        // a device square root worse than 2^-30: no source can pass the moment certificate, so every source runs the
+        // serial chains (which do not use it) from the first pass (makegraph_impl)
+        if (!(v >= 0.0 && v < 0x1p-30)) {
+            VLOG("makegraph: square-root error %.3g over 1..%lld: certified moment sums off\n", v, nmax);
+            v = INFINITY;
+        }
         ctx->sqrt_err = v;
         ctx->sqrt_err_nmax = nmax;
         VLOG("makegraph: square-root error bound %.3g over 1..%lld\n", v, nmax);
@@ -1057,7 +1108,8 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         for (int attempt = 0; attempt < 8; attempt++) {
             size_t lds = makegraph_lds(gcap, bcap, D);
             if (lds > 160 * 1024) return fail(DMX_ERR_CAPACITY, "makegraph LDS requirement exceeds 160 KiB");
-            const bool exact_pass = attempt > 0 || getenv("DMX_MK_EXACT");   // re-runs: the serial moment chains
+            // re-runs (and every pass when the device square root is not accurate enough): the serial moment chains
+            const bool exact_pass = attempt > 0 || getenv("DMX_MK_EXACT") || !(sqrt_err < 0x1p-30) || getenv("DMX_MK_SQRT_BAD");
             const mk_kernel_t kern = mk_kernel(gcap == MK_GCAP0 && bcap == MK_BCAP0 && !exact_pass &&
                                                    !getenv("DMX_MK_NOFIXED"),
                                                d_work != nullptr, maxdist != -1.0, D + 4 > MK_OPEN_LDS);
@@ -1118,6 +1170,8 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
             P.sym_prefix = sym_pass ? g->sym_prefix.p : nullptr;
             P.sym_diff = sym_pass ? g->sym_diff.p : nullptr;
             P.sym_ho = sym_pass ? g->sym_ho.p : nullptr;
+            // the shortest span taken (DMX_MK_SPAN: A/B hook; DMX_MK_NOSPAN: every depth cell by cell)
+            P.spans = getenv("DMX_MK_NOSPAN") ? 0 : (getenv("DMX_MK_SPAN") ? std::max(1, atoi(getenv("DMX_MK_SPAN"))) : MK_SPAN_MIN);
             HIPCHK(hipEventRecord(ctx->ev0, ctx->stream));
             if (todo > 0) {
                 HIPCHK(dP.alloc(1));
@@ -1191,10 +1245,10 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
         HIPCHK(copy_sync(ctx->stream, hc, ctx->counters.p, sizeof(hc), hipMemcpyDeviceToHost));
         unsigned long long used = 0;
         std::memcpy(&used, &hc[2], 8);
-        unsigned long long st[22];
+        unsigned long long st[26];
         HIPCHK(copy_sync(ctx->stream, st, ctx->stats.p, sizeof(st), hipMemcpyDeviceToHost));
         if (verbose()) {
-            double tot = 0;
+            double tot = (double)st[22];
             for (int i = 8; i < 18; i++) tot += (double)st[i];
             VLOG("makegraph phases (wave clocks): garbage %.1f%%, ranges %.1f%%, candidates %.1f%%, bins %.1f%%, "
                  "moments %.1f%%, run tracking %.1f%%, placement %.1f%%, publish %.1f%%, depth tail %.1f%%, "
@@ -1203,6 +1257,9 @@ static int makegraph_impl(dmx_ctx* ctx, dmx_pointmap* pm, double maxdist, int bo
                  100 * st[14] / tot, 100 * st[15] / tot, 100 * st[16] / tot, 100 * st[17] / tot, tot, st[2], st[3], st[0]);
             VLOG("makegraph merges: %llu (%llu with one block), %.2f blocks and %.2f gaps a merge\n", st[18], st[19],
                  st[18] ? (double)st[20] / st[18] : 0.0, st[18] ? (double)st[21] / st[18] : 0.0);
+            VLOG("makegraph spans: %.1f%% of the clocks; %llu spans over %llu depths (%.1f each), %llu of %llu visible cells "
+                 "(%.1f%%)\n", 100 * st[22] / tot, st[23], st[24], st[23] ? (double)st[24] / st[23] : 0.0, st[25], st[1],
+                 st[1] ? 100.0 * st[25] / st[1] : 0.0);
         }
         ctx->last_stats[0] = (long long)st[0];
         ctx->last_stats[1] = (long long)st[1];
@@ -1796,6 +1853,8 @@ static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_
             HIPCHK(hipGetLastError());
             VLOG("vga prep: scan order released for %.1f GB of partial-tile masks\n", mask_b / 1e9);
             build = true;
+            if (getenv("DMX_VGA_PMASK_FAIL"))   // test hook: a failure after the release (the next call recovers)
+                return fail(DMX_ERR_HIP, "injected failure after the scan order was released");
         } else {
             build = false;
         }
@@ -1816,6 +1875,23 @@ static int prepare_pmask(dmx_graph* g, int rows, int tw, int th, int tvw, int64_
         HIPCHK(hipGetLastError());
     }
     return DMX_OK;
+}
+
+// Which memory-dependent VGA preparation structures the graph holds (last_stats[40..42]; bench.py prints them):
+// the search a call takes depends on what fitted next to the graph (DESIGN.md sections 1 and 5).
+static void prep_state_stats(dmx_ctx* ctx, const dmx_graph* g) {
+    long long f = 0;
+    if (g->scan_pool.p) f |= 1;          // the BFS scan order
+    if (g->scan_released) f |= 2;        // ... released for the masks (runs read in pool order)
+    if (g->tvis.p) f |= 4;               // tile-visibility rows
+    if (g->ftvis.p) f |= 8;              // fully-seen tile rows
+    if (g->ttvis.p) f |= 16;             // tile-to-tile rows
+    if (g->pmask.p) f |= 32;             // partial-tile masks
+    if (g->tvsum.p) f |= 64;             // row summaries (wide grids)
+    ctx->last_stats[40] = f;
+    ctx->last_stats[41] = (long long)((g->tvis.p ? g->tvis.n * 8 : 0) + (g->ftvis.p ? g->ftvis.n * 8 : 0) +
+                                      (g->ttvis.p ? g->ttvis.n * 8 : 0) + (g->tvsum.p ? g->tvsum.n * 8 : 0));
+    ctx->last_stats[42] = (long long)(g->scan_pool.p ? g->scan_pool.n * sizeof(Run) : 0);
 }
 
 // LDS of the tile BFS workgroup: the frontier bitmap (unless FG), the tile-row summary Fsr, then either the
@@ -1840,6 +1916,10 @@ static size_t tile_lds_layout(int tw, int th, bool* fg, bool* rbm) {
 // Tile-ordered per-cell arrays, head runs and tile-common runs for vga_tile_kernel (O(runs)).
 static int prepare_tiles(dmx_graph* g) {
     if (g->tiles_ready) return DMX_OK;
+    // a preparation that released the scan order for the masks and then failed (prepare_pmask) left the tile data
+    // half built: rebuild the scan order before the heads and the tile-common runs read it
+    if (g->scan_released)
+        if (int rc = restore_scan_order(g)) return rc;
     dmx_ctx* ctx = g->ctx;
     hipStream_t s = ctx->stream;
     PointMapHost& h = *g->pm->host;
@@ -1997,18 +2077,24 @@ static int ordered_search(dmx_ctx* ctx, dmx_graph* g, double radius, const std::
     P.cell_node = g->pm->d_cell_node.p; P.node_cell = g->pm->d_node_cell.p; P.node_flags = g->pm->d_node_flags.p;
     P.merge_cell = g->merges.empty() ? nullptr : g->d_merge_cell.p;
     P.src = nullptr; P.nsrc = 0; P.radius = (int)radius; P.hist_all = nullptr; P.nlev_all = nullptr;
+    // levels kept per search: a radius r search has at most r + 2 (the cells at level r are counted, not
+    // expanded); radius n as deep as the direction-optimising kernel follows (vga_do: 4096 levels)
+    P.hmax = (radius == -1.0) ? 4096 : (int)std::min<double>(4096.0, radius + 2.0);
     P.seeds = nullptr; P.nseeds = 0; P.cell_level = d_cell_level;
     P.misc = misc.p; P.ext = ext.p; P.vec = vec.p;
     P.error = ctx->counters.p + 1;
-    HIPCHK(hipMemsetAsync(ctx->counters.p + 1, 0, sizeof(int), ctx->stream));
+    P.work_counter = ctx->counters.p + 0;
+    P.ctl = ctx->d_ctl;
+    ctx->h_ctl->progress = 0;
+    HIPCHK(hipMemsetAsync(ctx->counters.p, 0, 2 * sizeof(int), ctx->stream));
     if (vsd) {
         HIPCHK(d_seeds.alloc(seed_cells.size()));
         HIPCHK(hipMemcpyAsync(d_seeds.p, seed_cells.data(), seed_cells.size() * 4, hipMemcpyHostToDevice, ctx->stream));
         P.seeds = d_seeds.p; P.nseeds = (int)seed_cells.size();
     } else {
         HIPCHK(d_src.alloc(src.size()));
-        HIPCHK(hist.alloc((size_t)std::max<int64_t>(N, 1) * VGA_HMAX));
-        HIPCHK(nlev.alloc(std::max<int64_t>(N, 1)));
+        HIPCHK(hist.alloc((size_t)nsearch * P.hmax));
+        HIPCHK(nlev.alloc(nsearch));
         HIPCHK(hipMemcpyAsync(d_src.p, src.data(), src.size() * 4, hipMemcpyHostToDevice, ctx->stream));
         P.src = d_src.p; P.nsrc = (int)src.size(); P.hist_all = hist.p; P.nlev_all = nlev.p;
     }
@@ -2017,13 +2103,17 @@ static int ordered_search(dmx_ctx* ctx, dmx_graph* g, double radius, const std::
     HIPCHK(hipMemcpyAsync(dP.p, &P, sizeof(P), hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(vga_ordered_kernel, dim3((unsigned)blocks), dim3(ORD_NT), 0, ctx->stream, (const OrderedParams*)dP.p);
     HIPCHK(hipGetLastError());
+    HIPCHK(wait_progress(ctx, DMX_PHASE_VGA, nsearch, 1));   // progress posts, the cancel flag
+    CANCEL_POINT(ctx);
     int err = 0;
     HIPCHK(copy_sync(ctx->stream, &err, ctx->counters.p + 1, sizeof(int), hipMemcpyDeviceToHost));
-    if (err) return fail(DMX_ERR_CAPACITY, "VGA BFS (reference order) exceeded its level capacity");
+    // deeper than the reference-order search keeps (the engine's own deepest search): declined, so that a
+    // caller with a CPU path (integration/dmx_salalib.cpp) can take it
+    if (err) return fail(DMX_ERR_UNSUPPORTED, "VGA BFS in the reference's order deeper than 4096 levels");
     if (!vsd) {
         HIPCHK(junk.alloc(32));
         hipLaunchKernelGGL(vga_measures_kernel, dim3((unsigned)((nsearch + 255) / 256)), dim3(256), 0, ctx->stream,
-                           (int64_t)0, nsearch, hist.p, nlev.p, outp, d_levels, junk.p, (const int32_t*)d_src.p);
+                           (int64_t)0, nsearch, hist.p, nlev.p, outp, d_levels, junk.p, (const int32_t*)d_src.p, P.hmax, true);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipStreamSynchronize(ctx->stream));
@@ -2262,6 +2352,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[35] = (long long)st[30];                          // phase-C partial-tile masks read
     ctx->last_stats[36] = (long long)st[31];                          // phase-C cells tested by masks
     ctx->last_stats[37] = (long long)(g->pmask.p ? g->pmask.n * 8 : 0);  // bytes of partial-tile masks held
+    prep_state_stats(ctx, g);
     if (nseeds > 0) return DMX_OK;
     if (!out_on_device && nsrc > 0)
         HIPCHK(copy_sync(ctx->stream, out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));

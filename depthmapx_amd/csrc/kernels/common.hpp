@@ -46,6 +46,11 @@ __host__ __device__ inline uint32_t pack_cell(bool filled, uint32_t nseg, uint32
 __device__ __forceinline__ bool cell_filled(uint32_t w) { return w & 1u; }
 __device__ __forceinline__ int cell_nseg(uint32_t w) { return (int)((w >> 1) & 127u); }
 __device__ __forceinline__ int cell_seg_off(uint32_t w) { return (int)(w >> 8); }
+// A FILLED cell without occluder pieces ("clean") has no segment offset; its bits 8..31 hold instead its clean
+// distance: the Chebyshev distance to the nearest cell that is not clean or lies outside the grid (capped at
+// 2^24 - 1; upload_pointmap).  0 for every other cell.  makeGraph's span certificate (makegraph.hip).
+constexpr uint32_t CELL_DIST_MAX = (1u << 24) - 1u;
+__device__ __forceinline__ int cell_span_dist(uint32_t w) { return ((w & 0xFFu) == 1u) ? (int)(w >> 8) : 0; }
 
 // Run record in HBM: cells from (x0,y0) to (x1,y1) along H, V or a diagonal (PixelVec,
 // ngraph.h:31-46).  The direction is implied: y0==y1 -> H, x0==x1 -> V, otherwise diagonal.

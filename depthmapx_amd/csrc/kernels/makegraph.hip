@@ -19,6 +19,7 @@
 //     symmetry certificate's scatter there (sym_run_scatter, common.hpp), run by run.
 //   All geometry is IEEE double in the reference's operation order (-ffp-contract=off).
 #include "common.hpp"
+#include "span.hpp"
 
 
 namespace dmx {
@@ -27,6 +28,9 @@ namespace dmx {
 #define MK_PFIND 1   // the prefetch also keeps the first chunk's candidate index and gap bounds in registers (A/B hook)
 #endif
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
+// shortest occluder-free span taken, in depths (DMX_MK_SPAN overrides): configs[2] / configs[4] makeGraph with
+// 1: 3.23 / 9.61 s, 2: 3.17 / 9.02, 4: 3.11 / 8.61, 8: 3.11 / 8.75 (profiles/r6_span_ab.jsonl)
+constexpr int MK_SPAN_MIN = 4;
 // open-run state of rows 0 .. MK_OPEN_LDS-1 lives in LDS, of farther rows (grids above ~1020 cells a
 // side) in per-wave scratch memory: rows past 1024 are reached only by sight lines longer than 1024
 // cells, and a full-length LDS array would cost a 2000^2 grid a quarter of its waves
@@ -85,6 +89,9 @@ struct MakeGraphParams {
     const unsigned long long* sym_prefix;   // [4][C] line prefix sums of the cell weights
     unsigned long long* sym_diff;           // [4][C] difference arrays (zeroed by the host per pass)
     unsigned long long* sym_ho;             // [N] (indexed by node - node_begin)
+    // occluder-free depth spans (span.hpp): the shortest span taken, in depths (0: off); the cell words of FILLED
+    // cells without an occluder piece carry their clean distance (common.hpp cell_span_dist)
+    int spans;
 };
 
 // phase clocks (profile builds of a run only; wave-uniform scalar reads)
@@ -130,27 +137,7 @@ __device__ __forceinline__ double tanify(double cxp, double cyp, double px, doub
     }
 }
 
-// whichbin (pointdata.h:432-520)
-__device__ __forceinline__ int whichbin(double gx, double gy) {
-    int bin;
-    double ratio;
-    if (!(fabs(gy) > fabs(gx))) {
-        ratio = fabs(gy) / fabs(gx);
-        if (gx > 0.0) bin = (gy >= 0.0) ? 0 : -32;
-        else bin = (gy >= 0.0) ? -16 : 16;
-    } else {
-        ratio = fabs(gx) / fabs(gy);
-        if (gy > 0.0) bin = (gx >= 0.0) ? -8 : 8;
-        else bin = (gx >= 0.0) ? 24 : -24;
-    }
-    if (ratio < 1e-12) {
-    } else if (ratio < 0.2679491924311227) bin += 1;
-    else if (ratio < 0.5773502691896257) bin += 2;
-    else if (ratio < 1.0 - 1e-12) bin += 3;
-    else bin += 4;
-    if (bin < 0) bin = -bin;
-    return bin % 32;
-}
+// whichbin (pointdata.h:432-520): span.hpp (shared with the span arithmetic and its host test)
 
 // block zone ordering (sparksieve2.h:72-75)
 __device__ __forceinline__ bool zone_less(double as, double ae, double bs, double be) {
@@ -180,6 +167,11 @@ __device__ __forceinline__ int wave_incl_max(int v) {
         int t = __shfl_up(v, o);
         if (lane_id() >= o) v = max(v, t);
     }
+    return v;
+}
+// max over all 64 lanes (every lane gets it)
+__device__ __forceinline__ int wave_incl_max_all(int v) {
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
     return v;
 }
 __device__ __forceinline__ double wave_max_d(double v) {
@@ -357,6 +349,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     // FIXED kernels run the first pass: certified moment sums, maxdist test only in the MAXD variant
     const bool exact = FIXED ? false : (P.exact_moments != 0);
     const bool hasmax = FIXED ? MAXD : (P.maxdist != -1.0);
+    // spans need the certified parallel moment sums (the serial chains sum in the reference's per-depth
+    // addlist order) and no maxdist test
+    const bool spans = !exact && !hasmax && P.spans > 0;
+    const int span_min = P.spans;   // shortest span taken (depths)
     Lds L;
     {
         unsigned char* p = smem;
@@ -416,8 +412,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     // 0 collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible: bins, 4 visible: serial
     // moments, 5 visible: run tracking, 6 octant flush + placement, 7 publish, 8 depth tail (next depth's
     // prefetch), 9 octant setup + depth 0
-    unsigned long long cyc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long cyc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // (10: spans)
     unsigned long long mst[4] = {0, 0, 0, 0};   // PROF: merges, one-block merges, blocks, gaps at merges
+    unsigned long long spst[3] = {0, 0, 0};     // PROF: spans, span depths, span cells
     unsigned long long tmark = PROF ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
@@ -433,7 +430,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             if (node >= P.node_end) break;
         }
         const int cell = P.node_cell[node];
-        const int cx = cell / P.rows, cy = cell % P.rows;
+        // wave-uniform: in scalar registers (held in VGPRs they were spilled around the candidate loop)
+        const int cx = __builtin_amdgcn_readfirstlane(cell / P.rows), cy = __builtin_amdgcn_readfirstlane(cell % P.rows);
         const double c0x = P.blx + sp * 1.0 * (double)cx, c0y = P.bly + sp * 1.0 * (double)cy;
         if (lane < 32) { L.binc[lane] = 0; L.bfar[lane] = 0; L.bnr[lane] = 0; }
         __syncthreads();
@@ -753,6 +751,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 examined += (unsigned long long)T;
                 MK_T(1);
                 bool hasgaps = false;
+                int lmin = INT_MAX;   // smallest clean distance of this lane's candidates (span certificate)
                 int gcur = 0; // per-lane gap pointer (t increases monotonically)
                 for (int t0 = 0; t0 < T; t0 += 64) {
                     if (COUNT || PROF) nchunks++;
@@ -810,6 +809,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             put_block(slot, (ta < tb) ? make_double2(ta - 1e-10, tb + 1e-10) : make_double2(tb - 1e-10, ta + 1e-10));
                         }
                     }
+                    if (valid) lmin = min(lmin, ingrid ? cell_span_dist(w) : 0);
                     hasgaps |= (ballot(ingrid) != 0ull);
                     MK_T(2);
                     // ---- visible cells: bins, moments (reference order), run tracking
@@ -914,6 +914,176 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
                 if (!hasgaps) break;      // sieve2 returned false (pointdata.cpp:1458)
                 dq = depth;
+                // ---------------- occluder-free span: depths depth+1 .. depth+k in one pass (span.hpp)
+                // Certificate: this depth added no block, and every cell it visited has clean distance >= k + 2.
+                // The rows a gap visits at depth + j lie within j + 1 rows of the rows it visits here (lo and
+                // firstind never fall, hi rises by at most j + 1), so every cell visited at depths depth+1 ..
+                // depth+k is within Chebyshev distance k + 1 of a cell visited here: FILLED, in the grid, without
+                // an occluder piece.  Those depths add no block (the gap list stays), every visited cell in a
+                // gap's centre is visible, and a row's visible depths are an interval per gap.  The rows are
+                // spread over the lanes; a row's runs, bin counts and far distances come per (gap, ratio class)
+                // interval, only the first moment's square roots per cell.
+                // (expect false: the register allocator weighs the span's loops below the candidate loop's)
+                if (__builtin_expect(spans && !failed && L.misc[1] == 0 && ballot(lmin < span_min + 2) == 0ull, 0)) {
+                    int mind = lmin;
+                    for (int off = 32; off >= 1; off >>= 1) mind = min(mind, __shfl_xor(mind, off));
+                    const int d0 = depth + 1, d1 = depth + (mind - 2);
+                    if (far_rows) __syncthreads(); else wave_sync();   // this depth's open-row stores
+                    SpanOct so;
+                    so.q = q; so.cx = cx; so.cy = cy; so.blx = P.blx; so.bly = P.bly; so.sp = sp; so.c0x = c0x; so.c0y = c0y;
+                    so.obinp = obinp;
+                    const bool axis_row = (q == 0 || q == 1 || q == 5 || q == 6);
+                    // reciprocals of the gap ends in L.gaps2 (free outside collectgarbage): row estimates, which the
+                    // exact predicates then settle
+                    for (int g = lane; g < ng; g += 64) {
+                        const double2 z = L.gaps[g];
+                        L.gaps2[g] = make_double2(1.0 / z.x, 1.0 / z.y);
+                    }
+                    wave_sync();
+                    const int R0 = max(0, gap_cl(L.gaps[0].x, d0)), R1 = min(d1, gap_ch(L.gaps[ng - 1].y, d1));
+                    int nsp = 0;   // this lane's visible cells in the span
+                    for (int rb = R0; rb <= R1; rb += 64) {
+                        if (COUNT || PROF) nchunks++;
+                        const int ind = rb + lane;
+                        const bool live = ind <= R1;
+                        // last depths of ratio classes 3 and 2 (span.hpp class_last), settled exactly only when
+                        // they fall near the span (ind / tan is within 1e-11 of the product below)
+                        int t3 = ind, t2 = ind;
+                        if (live && ind > 0) {
+                            const double x3 = (double)ind * 1.7320508075688772, x2 = (double)ind * 3.7320508075688776;
+                            t3 = (x3 + 3.0 < (double)d0) ? d0 - 1 : (x3 - 3.0 > (double)d1) ? d1
+                                                                  : class_last(so, ind, 3, 0.5773502691896257);
+                            t2 = (x2 + 3.0 < (double)d0) ? d0 - 1 : (x2 - 3.0 > (double)d1) ? d1
+                                                                  : class_last(so, ind, 2, 0.2679491924311227);
+                            t3 = max(t3, ind);
+                            t2 = max(t2, t3);
+                        }
+                        uint32_t o = live ? ld_open(ind) : 0u;
+                        bool diag = false;
+                        for (int g = ng - 1; g >= 0; g--) {   // later gaps first: the row's depths in order
+                            const double2 z = L.gaps[g], iz = L.gaps2[g];
+                            const double gs_ = z.x, ge_ = z.y;
+                            int p = 1, r = 0;
+                            if (live) {
+                                // first d with ch(e, d) >= ind; last d with cl(s, d) <= ind and b(e_prev, d) <= ind
+                                int a = (ind == 0) ? d0 : clamp_est(ceil((double)ind * iz.y), d0, d1 + 1);
+                                while (a > d0 && gap_ch(ge_, a - 1) >= ind) a--;
+                                while (a <= d1 && gap_ch(ge_, a) < ind) a++;
+                                int c = (gs_ > 0.0) ? clamp_est(floor((double)ind * iz.x), d0 - 1, d1) : d1;
+                                while (c < d1 && gap_cl(gs_, c + 1) <= ind) c++;
+                                while (c >= d0 && gap_cl(gs_, c) > ind) c--;
+                                if (g > 0) {
+                                    const double gp_ = L.gaps[g - 1].y;
+                                    int f = clamp_est(floor(((double)ind + 0.5) * L.gaps2[g - 1].y - 0.5), d0 - 1, d1);
+                                    const int m = min(ind, d1);
+                                    if (f < m) f = m;
+                                    while (f < d1 && gap_b(gp_, f + 1) <= ind) f++;
+                                    while (f >= d0 && gap_b(gp_, f) > ind) f--;
+                                    c = min(c, f);
+                                }
+                                p = a;
+                                r = c;
+                                if (ind == 0 && !axis_row) r = p - 1;      // (ind != 0 || q in {0,1,5,6})
+                                if (q >= 4 && p <= ind) p = ind + 1;       // (ind != depth || q < 4)
+                            }
+                            if (p <= r) {
+                                // two independent chains (any summation order is within the certificate's bound)
+                                double sa = 0.0, sb = 0.0;
+                                const unsigned i2 = (unsigned)(ind * ind);
+                                int d = p;
+                                for (; d + 1 <= r; d += 2) {
+                                    sa += sqrt_nr((double)((unsigned)(d * d) + i2));
+                                    sb += sqrt_nr((double)((unsigned)((d + 1) * (d + 1)) + i2));
+                                }
+                                if (d <= r) sa += sqrt_nr((double)((unsigned)(d * d) + i2));
+                                s1 += sa + sb;
+                                const unsigned long long ur = (unsigned long long)r, up = (unsigned long long)(p - 1);
+                                s2n += (ur * (ur + 1) * (2 * ur + 1) - up * (up + 1) * (2 * up + 1)) / 6 +
+                                       (unsigned long long)(r - p + 1) * (unsigned long long)(ind * ind);
+                                mcnt += r - p + 1;
+                                nsp += r - p + 1;
+                            }
+                            // pieces in depth order: the diagonal cell, ratio classes 3, 2, 1 (row 0: the axis, class 0);
+                            // only the classes some lane has
+                            const bool has = p <= r;
+                            const int chi = (ind == 0) ? 0 : (ind >= p && ind <= r) ? 4 : (p <= t3) ? 3 : (p <= t2) ? 2 : 1;
+                            const int clo = (ind == 0) ? 0 : (r <= t3) ? 3 : (r <= t2) ? 2 : 1;
+                            int cmax = wave_incl_max_all(has ? chi : -1), cmin = -wave_incl_max_all(has ? -clo : -5);
+                            for (int cc = cmax; cc >= cmin; cc--) {
+                                int a = 1, b = 0;
+                                if (ind == 0) { if (cc == 0) { a = p; b = r; } }
+                                else if (cc == 4) { a = max(p, ind); b = min(r, ind); }
+                                else if (cc == 3) { a = max(p, ind + 1); b = min(r, t3); }
+                                else if (cc == 2) { a = max(p, t3 + 1); b = min(r, t2); }
+                                else if (cc == 1) { a = max(p, t2 + 1); b = r; }
+                                bool emit = false;
+                                unsigned long long rec = 0;
+                                if (live && a <= b) {
+                                    const int bin = OBIN(cc);
+                                    atomicAdd(&L.binc[bin], (unsigned)(b - a + 1));
+                                    atomicMax(&L.bfar[bin], (unsigned)(b * b + ind * ind));
+                                    if (cc == 4) {
+                                        diag = true;
+                                    } else {   // the per-cell run tracking below, for the cells a..b at once
+                                        const int slot = (cc == 0) ? 3 : bin - q_sector;
+                                        const int oslot = (o >> 1) & 3, os = (o >> 3) & 0x3fff, ol = (o >> 17) & 0x3fff;
+                                        if ((o & 1u) && oslot == slot && ol == a - 1) {
+                                            o = pack_open(slot, os, b) | (o & MK_OPEN_ADJ);
+                                        } else {
+                                            const bool adj = (o & 1u) && ol == a - 1;
+                                            if (o & 1u) {
+                                                emit = true;
+                                                rec = pack_emit(oslot, ind, os, ol, 0) | ((unsigned long long)(o >> 31) << MK_REC_SHALLOW) |
+                                                      ((unsigned long long)adj << MK_REC_DEEP);
+                                            }
+                                            o = pack_open(slot, a, b) | (adj ? MK_OPEN_ADJ : 0u);
+                                        }
+                                    }
+                                }
+                                const unsigned long long em = ballot(emit);
+                                if (em) {
+                                    const int pos = nA + prefix_popc(em);
+                                    if (emit && pos < P.capA) stA[pos] = rec;
+                                    nA += __popcll(em);
+                                }
+                            }
+                        }
+                        if (live) st_open(ind, o);
+                        const unsigned long long dm = ballot(diag);   // diagonal cells: rows ascending = depths ascending
+                        if (dm) {
+                            if (diag_n == 0) diag_min = rb + (__ffsll((long long)dm) - 1);
+                            diag_max = rb + 63 - __clzll((long long)dm);
+                            diag_n += __popcll(dm);
+                        }
+                    }
+                    // cells examined (stats[0]): the visit ranges of every span depth, one depth a lane
+                    unsigned long long exs = 0;
+                    for (int db = d0; db <= d1; db += 64) {
+                        const int d = db + lane;
+                        int F = 0, T = 0;
+                        for (int g = 0; g < ng; g++) {
+                            const double2 z = L.gaps[g];
+                            const int lo = gap_lo(z.x, d), b = min(gap_hi(z.y, d), d), a = max(lo, F);
+                            T += (b >= a) ? (b - a + 1) : 0;
+                            if (b >= lo) F = max(F, b);
+                        }
+                        if (d <= d1) exs += (unsigned long long)T;
+                    }
+                    for (int off = 32; off >= 1; off >>= 1) {
+                        exs += __shfl_xor(exs, off);
+                        nsp += __shfl_xor(nsp, off);
+                    }
+                    examined += __shfl(exs, 0);
+                    nsize += __shfl(nsp, 0);
+                    if (PROF) { spst[0]++; spst[1] += (unsigned long long)(d1 - d0 + 1); spst[2] += (unsigned long long)__shfl(nsp, 0); }
+                    if (COUNT || PROF) nsteps++;
+                    depth = d1;
+                    dq = depth;
+                    if (nA > P.capA) { failed = true; if (lane == 0) atomicOr(P.error, KERR_STAGE_CAPACITY); }
+                    // the open-row stores (LDS; scratch rows past MK_OPEN_LDS) before the next depth reads them
+                    if (far_rows) __syncthreads(); else wave_sync();
+                    MK_T(10);
+                }
                 // prefetch: candidate t = lane of depth + 1 under the current gap list (few-gap case)
                 pf_ok = false;
                 // (a depth that added blocks changes the gap list: its next depth recomputes the ranges and
@@ -1197,15 +1367,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 atomicAdd(&P.stats[3], (unsigned long long)nchunks);
                 for (int i = 0; i < 4; i++) atomicAdd(&P.stats[18 + i], mst[i]);
             }
-            if (PROF)
+            if (PROF) {
                 for (int i = 0; i < 10; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
+                atomicAdd(&P.stats[22], cyc[10]);
+                for (int i = 0; i < 3; i++) atomicAdd(&P.stats[23 + i], spst[i]);
+            }
             P.attrs[k * 3 + 0] = (float)nsize;
             P.attrs[k * 3 + 1] = m1f;
             P.attrs[k * 3 + 2] = m2f;
         }
         __syncthreads();
-        for (int i = 0; i < 10; i++) cyc[i] = 0;
+        for (int i = 0; i < 11; i++) cyc[i] = 0;
         for (int i = 0; i < 4; i++) mst[i] = 0;
+        for (int i = 0; i < 3; i++) spst[i] = 0;
         MK_T(7);
     }
 }

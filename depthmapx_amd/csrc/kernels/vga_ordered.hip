@@ -21,8 +21,6 @@
 namespace dmx {
 
 constexpr int ORD_NT = 256;
-constexpr int ORD_HMAX = 64;   // levels kept per VGA source (the tile kernel's VGA_HMAX)
-static_assert(ORD_HMAX == VGA_HMAX, "the measures kernel reads [N][VGA_HMAX] histograms");
 
 struct OrderedParams {
     int rows;
@@ -38,8 +36,9 @@ struct OrderedParams {
     const int32_t* src;
     int nsrc;
     int radius;
-    int32_t* hist_all;            // [N][ORD_HMAX] counted cells per level
-    int32_t* nlev_all;            // [N] levels
+    int hmax;                     // levels kept per search (radius + 2, or the deepest search vga_do follows)
+    int32_t* hist_all;            // [nsrc][hmax] counted cells per level (by search index)
+    int32_t* nlev_all;            // [nsrc] levels
     // visual step depth: one search from the level-0 cells (PixelRef order), levels into cell_level
     const int32_t* seeds;
     int nseeds;
@@ -49,6 +48,8 @@ struct OrderedParams {
     int16_t* ext;                 // [C][2] extent along x (H runs) and y (V runs)
     int32_t* vec;                 // [2][N] level vectors (cells)
     int* error;
+    int* work_counter;            // searches are taken from it (zeroed by the host)
+    DmxCtl* ctl;                  // progress / cancel block (nullptr: none)
 };
 
 __device__ __forceinline__ bool cf_odd(const OrderedParams& P, int c) {
@@ -136,13 +137,17 @@ __global__ void __launch_bounds__(ORD_NT) vga_ordered_kernel(const OrderedParams
     P.vec += (size_t)blockIdx.x * 2 * P.N;
     __shared__ int wsum[ORD_NT / 64];
     __shared__ int sh_n[2];
-    __shared__ int sh_cell, sh_act;
+    __shared__ int sh_cell, sh_act, sh_si;
     const int tid = threadIdx.x;
     const bool vsd = P.seeds != nullptr;
     const int nsearch = vsd ? 1 : P.nsrc;
     int32_t* vec0 = P.vec;
     int32_t* vec1 = P.vec + P.N;
-    for (int si = blockIdx.x; si < nsearch; si += gridDim.x) {
+    for (;;) {   // searches from the shared counter, which also carries the cancel flag (ctl_poll)
+        if (tid == 0) sh_si = ctl_poll(P.ctl, atomicAdd(P.work_counter, 1));
+        __syncthreads();
+        const int si = sh_si;
+        if (si >= nsearch) break;
         for (int64_t c = tid; c < P.C; c += ORD_NT) {
             P.misc[c] = 0;
             P.ext[2 * c] = (int16_t)(c / P.rows);
@@ -197,7 +202,7 @@ __global__ void __launch_bounds__(ORD_NT) vga_ordered_kernel(const OrderedParams
                 __syncthreads();
             }
             if (!vsd && tid == 0) {
-                if (level < ORD_HMAX) P.hist_all[src * ORD_HMAX + level] = counted;
+                if (level < P.hmax) P.hist_all[(int64_t)si * P.hmax + level] = counted;
                 else atomicOr(P.error, KERR_LEVELS);
             }
             level++;
@@ -205,7 +210,7 @@ __global__ void __launch_bounds__(ORD_NT) vga_ordered_kernel(const OrderedParams
             int32_t* t = cur; cur = nxt; nxt = t;
             __syncthreads();
         }
-        if (!vsd && tid == 0) P.nlev_all[src] = min(level, ORD_HMAX);
+        if (!vsd && tid == 0) P.nlev_all[si] = min(level, P.hmax);
         __syncthreads();
     }
 }

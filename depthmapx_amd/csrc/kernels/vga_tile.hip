@@ -982,7 +982,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             }
                         if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
                         else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
-                        const int lim = min(nr, KH + P.bext);
+                        // past the heads only in scan order: after the masks took the scan order's place (wide grids)
+                        // the runs are in pool order, where positions KH.. are not the runs after the heads
+                        const int next = (P.scan_pool == P.pool) ? KH : KH + P.bext;
+                        const int lim = min(nr, next);
                         if (!hit) ST(29, 1);
                         bool skipped = false;
                         for (int base = KH0; base < lim && !hit; base += 4) {
@@ -1013,7 +1016,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             if (fj >= 0) { hit = true; if (hp != (uint32_t)(base + fj)) Hn[id] = (uint32_t)(base + fj); }
                         }
                         if (!hit) {
-                            if (nr > KH + P.bext || skipped) { to_hard = true; hard_val = id; }
+                            if (nr > next || skipped) { to_hard = true; hard_val = id; }
                             else { ST(5, 1); ST(6, nr); }
                         }
                     }
@@ -1834,12 +1837,16 @@ __global__ void __launch_bounds__(CR_THREADS) tile_cr_kernel(int cols, int rows,
 }
 
 // K4: the 7 VGA measures per source from its level histogram (vgavisualglobal.cpp:131-193).
+// hist_all / nlev_all are indexed by source, or (by_index: vga_ordered's re-runs) by position in src_list, with
+// hstride levels a row
 __global__ void vga_measures_kernel(int64_t sb, int64_t se, const int32_t* hist_all, const int32_t* nlev_all, float* out,
-                                    int64_t* levels_out, unsigned long long* stats, const int32_t* src_list = nullptr) {
+                                    int64_t* levels_out, unsigned long long* stats, const int32_t* src_list = nullptr,
+                                    int hstride = VGA_HMAX, bool by_index = false) {
     const int64_t i = sb + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= se) return;
     const int64_t src = src_list ? (int64_t)src_list[i] : i;
-    const int nlev = nlev_all[src];
+    const int64_t hi = by_index ? i : src;
+    const int nlev = nlev_all[hi];
     float* o = out + src * 7;
     if (nlev == 0) {   // skipped source (context-filled odd cell / gates_only)
         for (int i = 0; i < 7; i++) o[i] = -1.0f;
@@ -1847,7 +1854,7 @@ __global__ void vga_measures_kernel(int64_t sb, int64_t se, const int32_t* hist_
         return;
     }
     long long tn, td;
-    vga_measures(hist_all + src * VGA_HMAX, nlev, o, tn, td);
+    vga_measures(hist_all + hi * hstride, nlev, o, tn, td);
     if (levels_out) {
         levels_out[src * 3 + 0] = tn;
         levels_out[src * 3 + 1] = td;

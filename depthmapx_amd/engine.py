@@ -103,14 +103,14 @@ class Context:
         return dict(zip(["level1", "tile_common", "heads", "hard", "bookkeeping"], (int(v) for v in out)))
 
     def last_stats(self):
-        out = np.zeros(40, dtype=np.int64)
-        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 40))
+        out = np.zeros(48, dtype=np.int64)
+        N.check(N.lib().dmx_ctx_last_stats(self.h, N.ptr(out), 48))
         keys = ["mk_cells_examined", "mk_visible_pairs", "mk_runs", "vga_kernel", "vga_runs_expanded", "vga_levels",
                 "vga_cells_reached", "vga_sources", "vga_fail_cells", "vga_fail_runs", "vga_hbm_bitmaps",
                 "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",
                 "vga_hard_cells", "vga_hard_certain", "vga_topdown_cycles", "vga_b_tiles", "vga_b_cells", "vga_tt_tiles", "vga_c_busy", "vga_c_scan", "vga_c_spec", "vga_n_spec", "vga_tt_pruned", "vga_b_row_cycles", "vga_b_cell_tiles",
                 "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks", "mk_reruns", "vga_pmask_loads", "vga_pmask_cells", "vga_pmask_bytes",
-                "vga_order_reruns", "vga_sym_scatter_us"]
+                "vga_order_reruns", "vga_sym_scatter_us", "vga_prep_flags", "vga_tile_rows_bytes", "vga_scan_bytes"]
         # vga_c_scan, vga_c_spec, vga_b_row_cycles and vga_b_cell_cycles stay 0: the kernel no longer reads
         # the clock per hard cell or per tile (2.6 % of the 1000^2 VGA); the per-phase clocks remain
         d = {k: int(v) for k, v in zip(keys, out)}
@@ -119,6 +119,10 @@ class Context:
         d["vga_special_nodes"] = d["vga_kernel"] >> 8
         d["vga_frontier_hbm"] = (d["vga_launch"] >> 56) & 1   # tile BFS with its frontier in HBM (grids > 1024^2)
         d["vga_launch"] &= (1 << 56) - 1
+        f = d["vga_prep_flags"]   # the memory-dependent preparation the last VGA search ran with
+        d["vga_scan_order"], d["vga_scan_released"] = f & 1, (f >> 1) & 1
+        d["vga_prep"] = "+".join(n for b, n in enumerate(["scan", "scan-released", "tvis", "ftvis", "ttvis", "masks",
+                                                            "tvsum"]) if (f >> b) & 1) or "none"
         d["vga_kernel"] = ["topdown-v1", "direction-optimizing(top-down only)",
                            "direction-optimizing", "tile-resolved"][d["vga_kernel"] & 0xFF]
         return d

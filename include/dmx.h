@@ -83,7 +83,10 @@ int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
  * shape, [13] hard cells rejected by their tile-visibility row, [14] bytes of those rows read,
  * [15] runs scanned by hard cells, [16] hard cells that hit, [17] hard cells, ... [38] searches the last VGA
  * global / visual step depth call ran again in the reference's level order (vga_ordered.hip), [39] microseconds
- * the last VGA preparation spent on the symmetry scatter and its all-reduces (0 when makeGraph did it). */
+ * the last VGA preparation spent on the symmetry scatter and its all-reduces (0 when makeGraph did it), [40] the
+ * memory-dependent VGA preparation the last tile search ran with (bits: 0 scan order, 1 scan order released for
+ * the partial-tile masks, 2 tile-visibility rows, 3 fully-seen rows, 4 tile-to-tile rows, 5 partial-tile masks,
+ * 6 row summaries), [41] bytes of tile-visibility rows held, [42] bytes of the scan order held.  n <= 48. */
 int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
 
 /* The sources the last makeGraph swept a second time (graph node indices, in the order the passes listed

@@ -811,6 +811,23 @@ static int bin_contains(const NodeG* nd, const Run* br, int b, int x, int y) {
     return 0;
 }
 
+/* addGridConnections (pointdata.cpp:1735-1768) for node k */
+static uint8_t grid_connections(const dmxo_map* m, int64_t k) {
+    static const int mv[8][2] = {{0, 1}, {-1, 0}, {-1, 0}, {0, -1}, {0, -1}, {1, 0}, {1, 0}, {0, 0}};
+    int32_t c = m->node_cell[k];
+    int cx = c / m->rows, cy = c % m->rows;
+    int nx = cx + 1, ny = cy;
+    const NodeG* nd = &m->nodes[k];
+    uint8_t gc = 0;
+    for (int i = 0; i < 32; i += 4) {
+        const Run* br = nd->runs;
+        for (int b = 0; b < i; b++) br += nd->nruns[b];
+        if (bin_contains(nd, br, i, nx, ny)) gc |= (uint8_t)(1 << (i / 4));
+        nx += mv[i / 4][0]; ny += mv[i / 4][1];
+    }
+    return gc;
+}
+
 int dmxo_makegraph(dmxo_map* m, double maxdist, int boundary, int64_t nb, int64_t ne, int nthreads) {
     if (!m->blocked_lines) block_lines(m);
     int64_t C = (int64_t)m->cols * m->rows;
@@ -843,23 +860,82 @@ int dmxo_makegraph(dmxo_map* m, double maxdist, int boundary, int64_t nb, int64_
         }
         free_work(&w);
     }
-    /* addGridConnections (pointdata.cpp:1735-1768) */
-    static const int mv[8][2] = {{0, 1}, {-1, 0}, {-1, 0}, {0, -1}, {0, -1}, {1, 0}, {1, 0}, {0, 0}};
-    for (int64_t k = nb; k < ne; k++) {
-        int32_t c = m->node_cell[k];
-        int cx = c / m->rows, cy = c % m->rows;
-        int nx = cx + 1, ny = cy;
-        const NodeG* nd = &m->nodes[k];
-        uint8_t gc = 0;
-        for (int i = 0; i < 32; i += 4) {
-            const Run* br = nd->runs;
-            for (int b = 0; b < i; b++) br += nd->nruns[b];
-            if (bin_contains(nd, br, i, nx, ny)) gc |= (uint8_t)(1 << (i / 4));
-            nx += mv[i / 4][0]; ny += mv[i / 4][1];
+    for (int64_t k = nb; k < ne; k++) m->gridconn[k] = grid_connections(m, k);
+    return 0;
+}
+
+/* Whole-map digests (tests/golden/gen_mk_digests.py): sparkGraph2 + addGridConnections for the nodes
+ * [nb, ne) only, keeping the graph arrays of the map between calls, so a caller can sweep the map in
+ * chunks, read each chunk back (dmxo_get_graph_range) and free its runs (dmxo_release_range) without
+ * ever holding the whole 36-90 GB graph. */
+int dmxo_makegraph_range(dmxo_map* m, double maxdist, int64_t nb, int64_t ne, int nthreads) {
+    if (!m->blocked_lines) block_lines(m);
+    if (m->runs_borrowed) release_nodes(m);
+    if (!m->nodes) {
+        index_nodes(m);
+        int64_t N = m->nnodes;
+        m->nodes = (NodeG*)calloc(N ? N : 1, sizeof(NodeG));
+        free(m->attrs); m->attrs = (float*)calloc((N ? N : 1) * 3, sizeof(float));
+        free(m->gridconn); m->gridconn = (uint8_t*)calloc(N ? N : 1, 1);
+    }
+    if (nb < 0 || ne > m->nnodes || nb > ne) return -1;
+#ifdef _OPENMP
+    if (nthreads < 1) nthreads = 1;
+#pragma omp parallel num_threads(nthreads)
+#endif
+    {
+        Work w;
+        memset(&w, 0, sizeof(w));
+        w.sv.capg = 64; w.sv.gaps = (Zone*)malloc(64 * sizeof(Zone));
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 4)
+#endif
+        for (int64_t k = nb; k < ne; k++) {
+            free(m->nodes[k].runs);
+            memset(&m->nodes[k], 0, sizeof(NodeG));
+            int32_t c = m->node_cell[k];
+            spark_pixel(m, &w, (int)(c / m->rows), (int)(c % m->rows), maxdist, &m->nodes[k], &m->attrs[3 * k]);
+            m->gridconn[k] = grid_connections(m, k);
         }
-        m->gridconn[k] = gc;
+        free_work(&w);
     }
     return 0;
+}
+
+int64_t dmxo_num_runs_range(const dmxo_map* m, int64_t nb, int64_t ne) {
+    int64_t r = 0;
+    for (int64_t k = nb; k < ne; k++) r += m->nodes[k].total_runs;
+    return r;
+}
+
+/* dmxo_get_graph's layout for the nodes [nb, ne): attrs [n][3], bins [n][32][4], runs of those nodes. */
+void dmxo_get_graph_range(const dmxo_map* m, int64_t nb, int64_t ne, float* attrs, int32_t* bins, int16_t* runs,
+                          uint8_t* gridconn) {
+    int64_t ro = 0;
+    for (int64_t k = nb; k < ne; k++) {
+        const NodeG* nd = &m->nodes[k];
+        const int64_t i = k - nb;
+        if (attrs) memcpy(attrs + 3 * i, m->attrs + 3 * k, 3 * sizeof(float));
+        if (gridconn) gridconn[i] = m->gridconn[k];
+        if (bins)
+            for (int b = 0; b < 32; b++) {
+                int32_t* o = bins + (i * 32 + b) * 4;
+                o[0] = nd->dir[b]; o[1] = nd->count[b];
+                memcpy(&o[2], &nd->dist[b], 4);
+                o[3] = nd->nruns[b];
+            }
+        if (runs) memcpy(runs + 4 * ro, nd->runs, nd->total_runs * sizeof(Run));
+        ro += nd->total_runs;
+    }
+}
+
+void dmxo_release_range(dmxo_map* m, int64_t nb, int64_t ne) {
+    if (m->runs_borrowed) return;
+    for (int64_t k = nb; k < ne; k++) {
+        free(m->nodes[k].runs);
+        m->nodes[k].runs = NULL;
+        m->nodes[k].total_runs = 0;
+    }
 }
 
 /* bench.py cpu_baseline: makeGraph (sparkPixel2) of a sample of nodes, each on one thread, its wall

@@ -96,6 +96,14 @@ int dmxo_vga_local(dmxo_map* m, int gates_only, int64_t node_begin, int64_t node
 /* CPU-baseline sampling (bench.py): makeGraph / VGA global for a list of nodes, one node per thread,
  * per-node wall seconds in secs[n]. */
 int dmxo_makegraph_sample(dmxo_map* m, double maxdist, const int64_t* nodes, int64_t n, int nthreads, double* secs);
+/* Chunked whole-map sweep (tests/golden/gen_mk_digests.py): sparkGraph2 + addGridConnections of nodes
+ * [nb, ne) into the map's node arrays (allocated on first use), read back in dmxo_get_graph's layout, and
+ * the chunk's runs freed again. */
+int dmxo_makegraph_range(dmxo_map* m, double maxdist, int64_t nb, int64_t ne, int nthreads);
+int64_t dmxo_num_runs_range(const dmxo_map* m, int64_t nb, int64_t ne);
+void dmxo_get_graph_range(const dmxo_map* m, int64_t nb, int64_t ne, float* attrs, int32_t* bins, int16_t* runs,
+                          uint8_t* gridconn);
+void dmxo_release_range(dmxo_map* m, int64_t nb, int64_t ne);
 int dmxo_vga_global_sample(dmxo_map* m, double radius, const int64_t* nodes, int64_t n, int nthreads, float* out,
                            double* secs);
 

@@ -76,6 +76,14 @@ def lib():
         L.dmxo_set_merges.argtypes = [vp, vp, i64]
         L.dmxo_set_graph.restype = i32
         L.dmxo_set_graph.argtypes = [vp, vp, vp, i64]
+        L.dmxo_makegraph_range.restype = i32
+        L.dmxo_makegraph_range.argtypes = [vp, dbl, i64, i64, i32]
+        L.dmxo_num_runs_range.restype = i64
+        L.dmxo_num_runs_range.argtypes = [vp, i64, i64]
+        L.dmxo_get_graph_range.restype = None
+        L.dmxo_get_graph_range.argtypes = [vp, i64, i64, vp, vp, vp, vp]
+        L.dmxo_release_range.restype = None
+        L.dmxo_release_range.argtypes = [vp, i64, i64]
         _lib = L
     return _lib
 
@@ -223,6 +231,22 @@ class OracleMap:
         out = np.full(self.num_nodes, -1.0, dtype=np.float32)
         lib().dmxo_angular_stepdepth(self.h, _p(sel), len(sel), _p(out))
         return out
+
+    def make_graph_range(self, node_begin, node_end, maxdist=-1.0, threads=1):
+        """sparkGraph2 + addGridConnections of nodes [node_begin, node_end) only, returned in graph()'s layout
+        for those nodes, and their runs freed again: a whole-map sweep in chunks (gen_mk_digests.py)."""
+        L = lib()
+        if L.dmxo_makegraph_range(self.h, float(maxdist), int(node_begin), int(node_end), int(threads)):
+            raise ValueError("node range out of bounds")
+        n = node_end - node_begin
+        R = L.dmxo_num_runs_range(self.h, int(node_begin), int(node_end))
+        attrs = np.zeros((n, 3), dtype=np.float32)
+        bins = np.zeros((n, 32, 4), dtype=np.int32)
+        runs = np.zeros((max(R, 1), 4), dtype=np.int16)
+        gc = np.zeros(n, dtype=np.uint8)
+        L.dmxo_get_graph_range(self.h, int(node_begin), int(node_end), _p(attrs), _p(bins), _p(runs), _p(gc))
+        L.dmxo_release_range(self.h, int(node_begin), int(node_end))
+        return dict(attrs=attrs, bins=bins, runs=runs[:R], gridconn=gc)
 
     def make_graph_sample(self, nodes, maxdist=-1.0, threads=1):
         """sparkPixel2 for each listed node (one node per thread); per-node seconds."""

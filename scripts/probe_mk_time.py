@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--tag", default="")
     a = ap.parse_args()
     W, occ, lmin, lmax = (1999, 5000, 0.0025, 0.01) if a.config == 5 else (1000, 50, 0.02, 0.10)
     ctx = dmx.Context(0)
@@ -28,7 +29,7 @@ def main():
         ts.append(ctx.last_timing()[0])
         st = ctx.last_stats()
         g.close()
-    print(json.dumps({"lib": os.environ.get("DMX_LIB", "default"), "config": a.config, "mk_s": ts,
+    print(json.dumps({"lib": os.environ.get("DMX_LIB", "default"), "tag": a.tag, "config": a.config, "mk_s": ts,
                       "pairs": st["mk_visible_pairs"], "runs": st["mk_runs"],
                       "reruns": st["mk_reruns"]}), flush=True)
 
