@@ -1376,7 +1376,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
         }
         __syncthreads();
         if (overflow) {
-            if (tid == 0) atomicOr(P.error, KERR_LEVELS);
+            // the source's histogram is incomplete: marked skipped (0 levels) so that the measures kernel, launched
+            // before the host reads the error and falls back to vga_do, reads none of it (it used to read this
+            // source's unwritten level count)
+            if (tid == 0) { atomicOr(P.error, KERR_LEVELS); P.nlev_out[node] = 0; }
             continue;
         }
         {   // flush this lane-group's run-test count (32-bit per lane, per source)
@@ -1848,7 +1851,7 @@ __global__ void vga_measures_kernel(int64_t sb, int64_t se, const int32_t* hist_
     const int64_t hi = by_index ? i : src;
     const int nlev = nlev_all[hi];
     float* o = out + src * 7;
-    if (nlev == 0) {   // skipped source (context-filled odd cell / gates_only)
+    if (nlev <= 0 || nlev > hstride) {   // skipped source (context-filled odd cell / gates_only; a level overflow)
         for (int i = 0; i < 7; i++) o[i] = -1.0f;
         if (levels_out) { levels_out[src * 3] = 0; levels_out[src * 3 + 1] = 0; levels_out[src * 3 + 2] = 0; }
         return;

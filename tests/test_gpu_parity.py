@@ -497,6 +497,33 @@ def test_makegraph_certified_moments_equal_serial_chains(ctx, monkeypatch):
     np.testing.assert_array_equal(fast.view(np.uint32), A["attrs"].view(np.uint32))
 
 
+def test_makegraph_spans_equal_cell_by_cell(ctx, monkeypatch):
+    """Occluder-free depth spans (makegraph.hip, span.hpp) against the cell-by-cell sweep of the same kernel
+    (DMX_MK_NOSPAN) and the reference's own graph of syn256mk: bins, runs, attributes and grid connections
+    bit for bit, with spans of every length taken (DMX_MK_SPAN=1)."""
+    meta, A = load_case("syn256mk")
+    pm = _map(meta)
+    monkeypatch.setenv("DMX_MK_SPAN", "1")
+    a = pm.make_graph(ctx).copy(runs=True)
+    monkeypatch.delenv("DMX_MK_SPAN")
+    monkeypatch.setenv("DMX_MK_NOSPAN", "1")
+    b = pm.make_graph(ctx).copy(runs=True)
+    for k in ("bins", "runs", "gridconn"):
+        np.testing.assert_array_equal(a[k], b[k])
+    np.testing.assert_array_equal(a["attrs"].view(np.uint32), b["attrs"].view(np.uint32))
+    np.testing.assert_array_equal(a["attrs"].view(np.uint32), A["attrs"].view(np.uint32))
+
+
+def test_makegraph_without_the_certified_sums_is_exact(ctx, monkeypatch):
+    """A device square root too coarse for the moment certificate (forced with DMX_MK_SQRT_BAD) no longer fails
+    makeGraph: every source takes the serial chains from the first pass, with the same bits."""
+    meta, A = load_case("syn64")
+    pm = _map(meta)
+    monkeypatch.setenv("DMX_MK_SQRT_BAD", "1")
+    g = pm.make_graph(ctx)
+    _assert_graph_equal(g.copy(runs=True), A, False)
+
+
 def test_vga_source_list_matches_full_run(ctx):
     """dmx_vga_global_device_list (the interleaved multi-GPU shards): listed rows equal the full
     run's rows bit for bit, every other row is left untouched."""

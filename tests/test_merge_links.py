@@ -327,3 +327,57 @@ def test_gpu_visual_step_depth_with_contextfilled_links(ctx, seed):
         np.testing.assert_array_equal(got.view(np.uint32), ref.view(np.uint32))
         ran += 1
     assert ran > 0
+
+
+def _deep_serpentine_links(W=320, H=12, pitch=4, gap=3):
+    """A serpentine corridor (walls every `pitch` cells, openings alternating top / bottom): visual depths past
+    64 levels from the ends.  Merge links join neighbouring cells of one corridor, the odd-x end context-filled
+    (SEMIFILL), so a search finds both ends at one level and the reference's pop order decides the count."""
+    import depthmapx_amd as dmx
+    from pyoracle import OracleMap
+    lines = [(0.0, 0.0, W, 0.0), (W, 0.0, W, H), (W, H, 0.0, H), (0.0, H, 0.0, 0.0)]
+    for k, x in enumerate(range(pitch, W, pitch)):
+        lines.append((x, 0.0, x, H - gap) if k % 2 == 0 else (x, gap, x, H))
+    lines = np.array(lines, dtype=np.float64)
+    region = [0.0, 0.0, float(W), float(H)]
+    pm = dmx.PointMap(region, lines, 1.0)
+    om = OracleMap(region, 1.0, lines)
+    assert pm.make_points(1.5, 1.5) and om.fill(1.5, 1.5)
+    rows = pm.rows
+    st = np.ascontiguousarray(pm.state(), dtype=np.int32)
+    pairs = []
+    for x in range(pitch + 1, W - pitch, 3 * pitch):
+        a, b = x * rows + 5, (x + 1) * rows + 5
+        if st[a] & 2 and st[b] & 2:
+            st[a] |= 0x8   # Point::CONTEXTFILLED at an odd PixelRef
+            pairs.append((a, b))
+    pairs = np.array(pairs, dtype=np.int32)
+    N = dmx._native
+    N.check(N.lib().dmx_pointmap_set_state(pm.h, N.ptr(st)))
+    om2 = OracleMap.from_grid(pm.cols, rows, 1.0, pm.info()["bottom_left"], st)
+    return pm, om, om2, pairs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernel", ["tile", "do"])
+def test_gpu_contextfilled_links_reference_order_past_64_levels(ctx, monkeypatch, kernel):
+    """The reference-order re-run (vga_ordered.hip) keeps as many levels as the radius needs (it kept
+    64, so a flagged source whose search went deeper failed the whole call): a radius-100 search on a serpentine
+    map deeper than 64 levels, with order-dependent links, equals the reference's order (the oracle)."""
+    if kernel == "do":
+        monkeypatch.setenv("DMX_VGA_KERNEL", "do")
+    pm, om, om2, pairs = _deep_serpentine_links()
+    assert len(pairs) >= 8
+    pm.set_merges(pairs)
+    g = pm.make_graph(ctx)
+    om.make_graph(threads=8)
+    b = om.graph()
+    om2.set_graph(b["bins"], b["runs"])
+    om2.set_merges(pairs)
+    ref, rlv = om2.vga_global(radius=100, threads=8, levels=True)
+    assert rlv[:, 2].max() > 64
+    got, lv = g.vga_visual_global(radius=100, levels=True)
+    assert ctx.last_stats()["vga_order_reruns"] > 0
+    np.testing.assert_array_equal(lv[:, :2], rlv[:, :2])
+    np.testing.assert_array_equal(got[:, 5], ref[:, 5])
+    assert np.allclose(got, ref, rtol=1e-6, atol=1e-6)
