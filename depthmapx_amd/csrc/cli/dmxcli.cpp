@@ -249,9 +249,20 @@ void write_document(const std::string& path, Document& d) {
     }
 }
 
+// -p: the PrintCommunicator's record lines (depthmapXcli/printcommunicator.cpp:19-38), posted by the library's
+// progress callback every 0.5 s (the Communicator contract, genlib/comm.h)
+bool g_print_progress = false;
+int print_progress(void*, int32_t, int64_t done, int64_t total) {
+    std::cout << "step: 1/1 record: " << std::min(done, total) << "/" << total << std::endl;
+    return 0;
+}
+
 struct Context {
     dmx_ctx* ctx = nullptr;
-    Context() { check(dmx_ctx_create(0, &ctx)); }
+    Context() {
+        check(dmx_ctx_create(0, &ctx));
+        if (g_print_progress) check(dmx_ctx_set_progress(ctx, print_progress, nullptr, 0.5));
+    }
     ~Context() { dmx_ctx_free(ctx); }
 };
 
@@ -623,10 +634,16 @@ struct Vga : Mode {
     }
     void run(const Args& a, Perf& perf) override {
         Document d;
-        timed(perf, "Load graph file", [&] { read_document(a.file, d); });
+        // the reference's loadGraph reads and parses the whole file: the chunk decode and the upload count in
+        // "Load graph file" too (the device context's creation does not)
+        const auto t0 = std::chrono::steady_clock::now();
+        read_document(a.file, d);
+        const auto t1 = std::chrono::steady_clock::now();
         Context C;
         LoadedMap m;
+        const auto t2 = std::chrono::steady_clock::now();
         load_map(C, d, m);
+        perf.add("Load graph file", std::chrono::duration<double>((t1 - t0) + (std::chrono::steady_clock::now() - t2)).count());
         std::cout << "Getting options..." << std::flush;
         if (mode == METRIC || mode == ANGULAR) {
             run_metric(a, perf, d, C, m);
@@ -856,6 +873,7 @@ int main(int argc, char* argv[]) {
                 a.simple = true;
             } else if (!std::strcmp("-p", argv[i])) {
                 a.progress = true;
+                g_print_progress = true;
             }
             ++i;
         }
