@@ -72,6 +72,7 @@ SIGNATURES = {
     "dmx_chunk_load": (_i32, [_vp, _vp, _vp, _vp, _vp]),
     "dmx_graph_from_runs": (_i32, [_vp, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp]),
     "dmx_graph_set_merges": (_i32, [_vp, _vp, _i64]),
+    "dmx_graph_set_drawing": (_i32, [_vp, _vp, _i64]),
     "dmx_pointmap_set_merges": (_i32, [_vp, _vp, _i64]),
     "dmx_chunk_merges": (_i32, [_vp, _vp, _vp]),
     "dmx_chunk_flags": (_i32, [_vp, _vp, _vp, _vp, _vp]),

@@ -643,6 +643,8 @@ struct Vga : Mode {
         LoadedMap m;
         const auto t2 = std::chrono::steady_clock::now();
         load_map(C, d, m);
+        // the document's drawing: VGA global on the re-read (asymmetric) graph takes the asymmetric mode with it
+        if (!d.lines.empty()) check(dmx_graph_set_drawing(m.g, d.lines.data(), (int64_t)d.lines.size() / 4));
         perf.add("Load graph file", std::chrono::duration<double>((t1 - t0) + (std::chrono::steady_clock::now() - t2)).count());
         std::cout << "Getting options..." << std::flush;
         if (mode == METRIC || mode == ANGULAR) {

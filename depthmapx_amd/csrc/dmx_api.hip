@@ -283,7 +283,20 @@ struct dmx_graph {
     int64_t prep_b = 0, prep_e = -1;
     dmx_allreduce_fn prep_fn = nullptr;
     void* prep_user = nullptr;
+    // asymmetric mode (prepare_asym): the drawing the graph's map was made from (dmx_graph_set_drawing), the
+    // symmetric reference graph R made from it again, and A, the nodes whose runs differ from R's (plus R's own
+    // asymmetric nodes), as a tile bitmap
+    std::vector<double> drawing;
+    bool has_drawing = false;
+    int asym_state = 0;   // 0 not tried, 1 ready, -1 not usable (reason in asym_why)
+    std::string asym_why;
+    std::unique_ptr<dmx_pointmap> aref_pm;
+    std::unique_ptr<dmx_graph> aref;
+    DevBuf<unsigned long long> asym_tiles;
+    int64_t nasym = 0;
+    ~dmx_graph();
 };
+dmx_graph::~dmx_graph() = default;
 
 namespace {
 
@@ -2154,7 +2167,12 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     HIPCHK(hint.alloc((size_t)nt * 64));
     HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
     DevBuf<int32_t> mseen;   // per workgroup: merge_order_check stamps
+    DevBuf<int32_t> alist;   // asymmetric mode: per workgroup, the frontier's A cells
     VgaTileParams P = Q;
+    if (Q.asym_tiles) {
+        HIPCHK(alist.alloc((size_t)blocks * Q.alist_cap));
+        P.alist = alist.p;
+    }
     P.fg = FG ? xg.p + (size_t)blocks * 2 * nt : nullptr;   // per workgroup [nt] after every V / X pair
     if (Q.nmamb) {
         HIPCHK(mseen.alloc((size_t)blocks * Q.nmamb));
@@ -2193,7 +2211,9 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
 
 static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, int64_t sb, int64_t se, float* out,
                          bool out_on_device, int64_t* levels, int tw, int th, const int32_t* d_seeds = nullptr,
-                         int nseeds = 0, int32_t* d_cell_level = nullptr, const int32_t* d_src_list = nullptr) {
+                         int nseeds = 0, int32_t* d_cell_level = nullptr, const int32_t* d_src_list = nullptr,
+                         dmx_graph* pg = nullptr) {
+    // pg (asymmetric mode): the graph analysed; g is its symmetric reference (prepare_asym)
     int rc = prepare_tiles(g);
     if (rc) return rc;
     PointMapHost& h = *g->pm->host;
@@ -2249,6 +2269,16 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
         Q.oflag = oflag.p;
     }
     Q.src_list = d_src_list;   // [sb, se) index this list of source nodes (out must be on the device)
+    Q.asym_tiles = nullptr; Q.asym_uf = nullptr; Q.apool = nullptr; Q.arun_start = nullptr; Q.anruns = nullptr;
+    Q.alist = nullptr; Q.alist_cap = 0;
+    if (pg) {   // asymmetric mode: pg's own universe (pre-visited cells, early-exit count) and runs for A's pushes
+        Q.seed_tiles = pg->notuf_tiles.p;
+        Q.uf_count = pg->uf_count;
+        Q.asym_tiles = pg->asym_tiles.p;
+        Q.asym_uf = g->uf_tiles.p;
+        Q.apool = pg->pool.p; Q.arun_start = pg->node_run_start.p; Q.anruns = pg->node_nruns.p;
+        Q.alist_cap = (int)std::max<int64_t>(pg->nasym, 1);
+    }
     // Beamer's direction test on cell counts (top-down levels run on the LDS frontier bitmap)
     Q.alpha = 60;   // top-down costs a frontier cell its whole run list (~R/N runs): keep it rare
     if (const char* a = getenv("DMX_VGA_ALPHA")) Q.alpha = atoi(a);
@@ -2353,11 +2383,97 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     ctx->last_stats[36] = (long long)st[31];                          // phase-C cells tested by masks
     ctx->last_stats[37] = (long long)(g->pmask.p ? g->pmask.n * 8 : 0);  // bytes of partial-tile masks held
     prep_state_stats(ctx, g);
+    if (pg) {   // asymmetric mode (bit 7) and |A|
+        ctx->last_stats[40] |= 128;
+        ctx->last_stats[43] = pg->nasym;
+    }
     if (nseeds > 0) return DMX_OK;
     if (!out_on_device && nsrc > 0)
         HIPCHK(copy_sync(ctx->stream, out + sb * 7, d_out.p + sb * 7, nsrc * 7 * 4, hipMemcpyDeviceToHost));
     if (levels && nsrc > 0)
         HIPCHK(copy_sync(ctx->stream, levels + sb * 3, d_lv.p + sb * 3, nsrc * 3 * 8, hipMemcpyDeviceToHost));
+    return DMX_OK;
+}
+
+// Asymmetric mode (vga_tile.hip): a graph whose runs are not symmetric at scale -- a map re-read from a .graph file,
+// where PixelVec's 4-bit row shift (ngraph.cpp:536-583) moved the runs after a jump of more than 15 rows and a bin
+// of 65536 k cells lost its runs (Bin::write's unsigned short count) -- has almost every node asymmetric, beyond
+// the in-set correction lists.  Made again from the drawing, the map's graph R is symmetric but for a few nodes;
+// A = the nodes whose runs differ between the graph and R, plus R's asymmetric nodes.  Every edge between two
+// nodes outside A is in both graphs and in both directions, so the search runs bottom-up on R with the frontier
+// limited to cells outside A, and the A cells of each frontier push the graph's own runs top-down.  Needs the
+// drawing (dmx_graph_set_drawing), the whole graph, no merge links, R on the same grid and |A| <= N/4.
+static int prepare_asym(dmx_ctx* ctx, dmx_graph* g) {
+    if (g->asym_state) return g->asym_state > 0 ? DMX_OK : DMX_ERR_UNSUPPORTED;
+    g->asym_state = -1;
+    if (!g->has_drawing) { g->asym_why = "no drawing"; return DMX_ERR_UNSUPPORTED; }
+    if (!g->merges.empty()) { g->asym_why = "merge links"; return DMX_ERR_UNSUPPORTED; }
+    if (g->node_begin != 0 || g->node_end != g->nnodes) { g->asym_why = "a shard"; return DMX_ERR_UNSUPPORTED; }
+    const PointMapHost& h = *g->pm->host;
+    std::unique_ptr<dmx_pointmap> pm(new dmx_pointmap());
+    pm->host.reset(new PointMapHost(h.parent_region(), h.spacing(), g->drawing.data(), (int64_t)g->drawing.size() / 4));
+    PointMapHost& hr = *pm->host;
+    if (hr.cols() != h.cols() || hr.rows() != h.rows() || hr.bottom_left().x != h.bottom_left().x ||
+        hr.bottom_left().y != h.bottom_left().y) {
+        g->asym_why = "the drawing's grid differs from the map's";
+        return DMX_ERR_UNSUPPORTED;
+    }
+    hr.block_lines();
+    hr.restore_fill(h.state().data());
+    pm->version++;
+    const double t0 = now_s();
+    // (makeGraph's timing and counters are the reference graph's from here on)
+    dmx_graph* r = nullptr;
+    if (int rc = makegraph_impl(ctx, pm.get(), -1.0, 0, 0, -1, nullptr, nullptr, &r)) {
+        g->asym_why = "makeGraph of the reference failed";
+        return rc;
+    }
+    std::unique_ptr<dmx_graph> R(r);
+    if (R->nnodes != g->nnodes) { g->asym_why = "the reference has other nodes"; return DMX_ERR_UNSUPPORTED; }
+    if (int rc = prepare_uf(R.get())) return rc;
+    if (int rc = prepare_symmetry(R.get())) return rc;
+    if (R->symmetric != 1) { g->asym_why = "the reference is not symmetric enough"; return DMX_ERR_UNSUPPORTED; }
+    const int64_t N = g->nnodes;
+    DevBuf<uint8_t> d_flag;
+    HIPCHK(d_flag.alloc(std::max<int64_t>(N, 1)));
+    if (N) {
+        hipLaunchKernelGGL(node_runs_differ_kernel, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, ctx->stream, N,
+                           g->bin_nruns.p, g->node_run_start.p, g->node_nruns.p, g->pool.p, R->bin_nruns.p,
+                           R->node_run_start.p, R->node_nruns.p, R->pool.p, d_flag.p);
+        HIPCHK(hipGetLastError());
+    }
+    std::vector<uint8_t> flag((size_t)std::max<int64_t>(N, 1));
+    HIPCHK(copy_sync(ctx->stream, flag.data(), d_flag.p, (size_t)N, hipMemcpyDeviceToHost));
+    for (int32_t k : R->special_nodes) flag[k] = 1;
+    const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
+    std::vector<unsigned long long> at((size_t)tw * th, 0ull);
+    int64_t na = 0;
+    for (int64_t k = 0; k < N; k++)
+        if (flag[k]) {
+            const int c = g->pm->node_cell[k], x = c / h.rows(), y = c % h.rows();
+            at[(size_t)(y >> 3) * tw + (x >> 3)] |= 1ull << ((y & 7) * 8 + (x & 7));
+            na++;
+        }
+    if (na > N / 4) { g->asym_why = "too many nodes differ from the reference"; return DMX_ERR_UNSUPPORTED; }
+    HIPCHK(g->asym_tiles.alloc(at.size()));
+    HIPCHK(copy_sync(ctx->stream, g->asym_tiles.p, at.data(), at.size() * 8, hipMemcpyHostToDevice));
+    g->nasym = na;
+    g->aref = std::move(R);
+    g->aref_pm = std::move(pm);
+    g->asym_state = 1;
+    VLOG("asymmetric mode: reference graph %.2f s, %lld of %lld nodes differ (%zu asymmetric in the reference)\n",
+         now_s() - t0, (long long)na, (long long)N, g->aref->special_nodes.size());
+    return DMX_OK;
+}
+
+int dmx_graph_set_drawing(dmx_graph* g, const double* lines, int64_t nlines) {
+    if (!g || nlines < 0 || (nlines > 0 && !lines)) return fail(DMX_ERR_ARG, "bad arguments");
+    g->drawing.assign(lines, lines + 4 * nlines);
+    g->has_drawing = true;
+    g->asym_state = 0;
+    g->aref.reset();
+    g->aref_pm.reset();
+    g->asym_tiles.reset();
     return DMX_OK;
 }
 
@@ -2374,6 +2490,8 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
     if (rc) return rc;
     rc = prepare_symmetry(g);
     if (rc) return rc;
+    ctx->last_stats[40] = 0;   // (the tile search sets its preparation flags; the other searches leave none)
+    ctx->last_stats[43] = 0;
     PointMapHost& h = *g->pm->host;
     const int tw = (h.cols() + 7) / 8, th = (h.rows() + 7) / 8;
     const int maxlev = 4096;
@@ -2381,9 +2499,18 @@ static int vga_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_only, i
         const char* fk = getenv("DMX_VGA_KERNEL");
         const bool forced_other = fk && (std::string(fk) == "v1" || std::string(fk) == "do" || std::string(fk) == "topdown");
         const int nt = tw * th;
-        if (!forced_other && g->symmetric == 1 && !ctx->tile_disabled) {
+        // DMX_VGA_ASYM (test hook): the asymmetric mode also for a graph whose few asymmetric nodes the in-set
+        // correction lists handle (small re-read maps), so that both exact paths can be compared
+        const bool force_asym = getenv("DMX_VGA_ASYM") && g->has_drawing && g->symmetric == 1 && g->nspecial > 0;
+        if (!forced_other && g->symmetric == 1 && !ctx->tile_disabled && !force_asym) {
             int rc2 = vga_tile_impl(ctx, g, radius, gates_only, sb, se, out, out_on_device, levels, tw, th);
             if (rc2 != DMX_ERR_CAPACITY) return rc2;   // capacity (level histogram): retry with vga_do
+        } else if (!forced_other && (g->symmetric == 0 || force_asym) && !ctx->tile_disabled && !getenv("DMX_VGA_NOASYM") &&
+                   prepare_asym(ctx, g) == DMX_OK) {
+            // asymmetric at scale (a re-read .graph): the tile search on the reference graph, A pushing its own runs
+            int rc2 = vga_tile_impl(ctx, g->aref.get(), radius, gates_only, sb, se, out, out_on_device, levels, tw, th,
+                                    nullptr, 0, nullptr, nullptr, g);
+            if (rc2 != DMX_ERR_CAPACITY) return rc2;
         }
     }
     if (int rc3 = restore_scan_order(g)) return rc3;   // (vga_do reads the scan order)

@@ -102,6 +102,17 @@ struct VgaTileParams {
     int32_t* hist_out;        // [N][VGA_HMAX] level histogram per source (measures: vga_measures_kernel)
     int32_t* nlev_out;        // [N] levels (0: source skipped)
     int* error;
+    // Asymmetric mode (a graph re-read from a .graph file, whose 4-bit row shifts moved runs): the search runs on a
+    // symmetric reference graph R (the structures above) with the frontier F limited to cells outside A, the nodes
+    // whose runs differ from R's (plus R's own asymmetric nodes); A's frontier cells push the graph's actual runs
+    // (apool) top-down instead.  Exact: every edge between two cells outside A is in both graphs and symmetric.
+    const unsigned long long* asym_tiles;   // [nt] cells of A (null: off)
+    const unsigned long long* asym_uf;      // [nt] cells on some run of R (the bottom-up candidates)
+    const Run* apool;                       // the graph's own runs
+    const int64_t* arun_start;
+    const int32_t* anruns;
+    int32_t* alist;                         // per workgroup [alist_cap]: A cells of the frontier (tile ids)
+    int alist_cap;
     unsigned long long* stats;  // [0] runs tested, [2] cells reached, [3] BU levels, [4] TD levels,
                                 // [5] hard cells without a hit, [6] their runs, [7] tiles resolved by CR,
                                 // [8..12] phase clocks, [13] hard cells rejected by their tile-visibility row,
@@ -319,6 +330,7 @@ __device__ __forceinline__ bool run_hits_fs(const FView& V, Run ru) {
 
 struct TileShared {
     int src, qn, hn, item, bn;
+    int an, aitem;        // asymmetric mode: A cells listed for the next push, the push's work counter
     int tn[2];            // entries of the two unvisited-tile lists (level parity)
     int mpart;            // merge partner cell of the source (-1: none)
     unsigned long long cnt, mass;
@@ -723,6 +735,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
     if (tid == 0) {
         S.qn = 0; S.hn = 0; S.item = 0; S.bn = 0; S.cnt = 0; S.mass = 0; S.src = -1;
         S.mpart = -1; S.mcorr = 0; S.mdisc = 0;
+        S.an = 0; S.aitem = 0;
     }
     int64_t chunk_end = 0;
     int64_t src = -1;
@@ -800,6 +813,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
         bool overflow = false;
         if (tid == 0) {
             S.tn[0] = 0; S.tn[1] = 0;
+            S.an = 0; S.aitem = 0;   // (a search that stopped at its radius leaves A cells listed)
             S.target = P.uf_count - n_in_uf;
             S.m_f = seeded ? P.nseeds : (spart >= 0 ? 2 : 1);
             S.m_u = S.target;
@@ -816,9 +830,12 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 // ---- level 1: rasterise the source's runs (top-down from {s}, or from every seed)
                 for (int i = 0; i < (seeded ? P.nseeds : (spart >= 0 ? 2 : 1)); i++) {
                     const int64_t sn = seeded ? P.seeds[i] : (i == 0 ? node : spart);
-                    const int64_t rs = P.node_run_start[sn];
-                    const int nr = P.node_nruns[sn];
-                    for (int r = tid; r < nr; r += NT) run_or(F, tw, P.pool[rs + r]);
+                    // (asymmetric mode: a source in A sees along the graph's own runs)
+                    const bool own = P.asym_tiles && i == 0 && !seeded && (P.asym_tiles[stile] & sbit);
+                    const int64_t rs = own ? P.arun_start[sn] : P.node_run_start[sn];
+                    const int nr = own ? P.anruns[sn] : P.node_nruns[sn];
+                    const Run* pl = own ? P.apool : P.pool;
+                    for (int r = tid; r < nr; r += NT) run_or(F, tw, pl[rs + r]);
                     if (tid < nr) rt += (unsigned)((nr - tid + NT - 1) / NT);
                 }
                 sync_global();
@@ -838,6 +855,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         const unsigned long long c0 = run_word(P.cr + CRK * t), c1 = run_word(P.cr + CRK * t + 1),
                                                  c2 = run_word(P.cr + CRK * t + 2), c3 = run_word(P.cr + CRK * t + 3);
                         U = ~Vg[t];
+                        if (P.asym_tiles) U &= P.asym_uf[t];   // (cells off R's runs: only A pushes reach them)
                         rg = P.regular_tiles[t];
                         const unsigned long long R = U & rg;
                         if (R) {
@@ -856,7 +874,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                     hit = run_hits_fs(FV, cj);
                                 }
                             }
-                            if (hit) { Xg[t] = R; U &= ~R; ST(7, 1); }
+                            if (hit) { Xg[t] = R; U &= ~R; ST(7, 1); }   // (X holds nothing else yet: one thread a tile)
                         }
                     }
                     const unsigned long long want = __ballot(U != 0ull);
@@ -1245,6 +1263,41 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                 for (int t = tid; t < nt; t += NT) Xg[t] = F[t] & ~Vg[t];
             }
             sync_global();
+            if (P.asym_tiles) {
+                // asymmetric mode: the frontier's A cells (listed by the last bookkeeping) push the graph's own runs
+                // (a wave a cell, lanes over its runs) into F -- free until the bookkeeping rebuilds it, and in LDS
+                // below 1024 cells a side -- and the unvisited part joins X
+                const int an = min(uni(S.an), P.alist_cap);
+                if (an > 0) {
+                    unsigned long long* PB = F;
+                    for (int t = tid; t < nt; t += NT) PB[t] = 0ull;
+                    sync_global();
+                    for (;;) {
+                        int it = 0;
+                        if (lane == 0) it = atomicAdd(&S.aitem, 1);
+                        it = __builtin_amdgcn_readlane(it, 0);
+                        if (it >= an) break;
+                        int x, y;
+                        xy_of_tile_id(P.alist[(size_t)blockIdx.x * P.alist_cap + it], tw, x, y);
+                        const int an_node = P.cell_node[x * rows + y];
+                        const int64_t rs = P.arun_start[an_node];
+                        const int nr = P.anruns[an_node];
+                        for (int r = lane; r < nr; r += 64) run_or(PB, tw, P.apool[rs + r]);
+                        if (lane == 0) rt += (unsigned)nr;
+                    }
+                    sync_global();
+                    for (int t = tid; t < nt; t += NT) {
+                        const unsigned long long pb = FG ? ld_wg(&PB[t]) : PB[t];
+                        if (pb) {
+                            const unsigned long long nw = pb & ~Vg[t];
+                            if (nw) or_wg(&Xg[t], nw);
+                        }
+                    }
+                }
+                __syncthreads();
+                if (tid == 0) { S.an = 0; S.aitem = 0; }
+                __syncthreads();   // (before the bookkeeping appends the next level's A cells)
+            }
             {
                 const unsigned long long n = __builtin_amdgcn_s_memtime();
                 if (tid == 0) {
@@ -1284,6 +1337,16 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     // step depth never expands contextfilled odd cells (vgavisualglobaldepth.cpp:53)
                     if (P.radius != -1 || seeded) x &= ~P.nonexp_tiles[t];
                     m_loc += (unsigned long long)__popcll(x);
+                    if (P.asym_tiles) {   // asymmetric mode: the A cells expand by pushing their own runs
+                        unsigned long long xa = x & P.asym_tiles[t];
+                        if (xa) {
+                            x &= ~xa;
+                            int pos = atomicAdd(&S.an, __popcll(xa));
+                            int32_t* AL = P.alist + (size_t)blockIdx.x * P.alist_cap;
+                            for (; xa; xa &= xa - 1)
+                                if (pos < P.alist_cap) AL[pos++] = (t << 6) | (__ffsll((long long)xa) - 1);
+                        }
+                    }
                     if (x) {
                         const int tx = t % tw, ty = t / tw;
                         atomicOr(&Fsr[ty * wr + (tx >> 6)], 1ull << (tx & 63));
@@ -1842,6 +1905,21 @@ __global__ void __launch_bounds__(CR_THREADS) tile_cr_kernel(int cols, int rows,
 // K4: the 7 VGA measures per source from its level histogram (vgavisualglobal.cpp:131-193).
 // hist_all / nlev_all are indexed by source, or (by_index: vga_ordered's re-runs) by position in src_list, with
 // hstride levels a row
+// Asymmetric mode's A (dmx_api.hip prepare_asym): flag each node whose bins or runs differ between graphs a and b
+// (same nodes).  One thread a node.
+__global__ void node_runs_differ_kernel(int64_t n, const int32_t* bins_a, const int64_t* rs_a, const int32_t* nr_a,
+                                        const Run* pool_a, const int32_t* bins_b, const int64_t* rs_b, const int32_t* nr_b,
+                                        const Run* pool_b, uint8_t* out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    bool d = nr_a[k] != nr_b[k];
+    for (int b = 0; b < 32 && !d; b++) d = bins_a[k * 32 + b] != bins_b[k * 32 + b];
+    const unsigned long long* ra = (const unsigned long long*)(pool_a + rs_a[k]);
+    const unsigned long long* rb = (const unsigned long long*)(pool_b + rs_b[k]);
+    for (int r = 0; r < nr_a[k] && !d; r++) d = ra[r] != rb[r];
+    out[k] = d ? 1 : 0;
+}
+
 __global__ void vga_measures_kernel(int64_t sb, int64_t se, const int32_t* hist_all, const int32_t* nlev_all, float* out,
                                     int64_t* levels_out, unsigned long long* stats, const int32_t* src_list = nullptr,
                                     int hstride = VGA_HMAX, bool by_index = false) {

@@ -110,7 +110,8 @@ class Context:
                 "vga_cr_tiles", "vga_launch", "vga_pruned_cells", "vga_tvis_bytes", "vga_hard_runs", "vga_hard_hits",
                 "vga_hard_cells", "vga_hard_certain", "vga_topdown_cycles", "vga_b_tiles", "vga_b_cells", "vga_tt_tiles", "vga_c_busy", "vga_c_scan", "vga_c_spec", "vga_n_spec", "vga_tt_pruned", "vga_b_row_cycles", "vga_b_cell_tiles",
                 "vga_b_cell_cycles", "vga_b_ext_cells", "mk_depth_steps", "mk_chunks", "mk_reruns", "vga_pmask_loads", "vga_pmask_cells", "vga_pmask_bytes",
-                "vga_order_reruns", "vga_sym_scatter_us", "vga_prep_flags", "vga_tile_rows_bytes", "vga_scan_bytes"]
+                "vga_order_reruns", "vga_sym_scatter_us", "vga_prep_flags", "vga_tile_rows_bytes", "vga_scan_bytes",
+                "vga_asym_nodes"]
         # vga_c_scan, vga_c_spec, vga_b_row_cycles and vga_b_cell_cycles stay 0: the kernel no longer reads
         # the clock per hard cell or per tile (2.6 % of the 1000^2 VGA); the per-phase clocks remain
         d = {k: int(v) for k, v in zip(keys, out)}
@@ -122,7 +123,8 @@ class Context:
         f = d["vga_prep_flags"]   # the memory-dependent preparation the last VGA search ran with
         d["vga_scan_order"], d["vga_scan_released"] = f & 1, (f >> 1) & 1
         d["vga_prep"] = "+".join(n for b, n in enumerate(["scan", "scan-released", "tvis", "ftvis", "ttvis", "masks",
-                                                            "tvsum"]) if (f >> b) & 1) or "none"
+                                                            "tvsum", "asymmetric-mode"]) if (f >> b) & 1) or "none"
+        d["vga_asym_mode"] = (f >> 7) & 1
         d["vga_kernel"] = ["topdown-v1", "direction-optimizing(top-down only)",
                            "direction-optimizing", "tile-resolved"][d["vga_kernel"] & 0xFF]
         return d
@@ -299,6 +301,13 @@ class Graph:
         angular (the getMergePixel blocks of salalib/vgamodules); pairs of x-major cells."""
         arr = np.ascontiguousarray(cell_pairs, dtype=np.int32).reshape(-1, 2)
         N.check(N.lib().dmx_graph_set_merges(self.h, N.ptr(arr), len(arr)))
+
+    def set_drawing(self, lines):
+        """The drawing lines ([n][4]) the graph's map was made from: VGA global on a graph re-read from a .graph file
+        (asymmetric: 4-bit row shifts, 16-bit bin counts) then runs in the asymmetric mode (dmx_graph_set_drawing)."""
+        arr = np.ascontiguousarray(lines, dtype=np.float64).reshape(-1, 4)
+        self._drawing = arr
+        N.check(N.lib().dmx_graph_set_drawing(self.h, N.ptr(arr), len(arr)))
 
     def blob_size(self):
         b = ctypes.c_int64()

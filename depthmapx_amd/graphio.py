@@ -78,9 +78,10 @@ def read_chunk(blob):
                 displayed_sorted=disp.value, bytes_used=used.value)
 
 
-def load_chunk(ctx, blob, region):
+def load_chunk(ctx, blob, region, lines=None):
     """(PointMap-like handle, Graph) analysing what the reference CLI's VGA / STEPDEPTH step would
-    after loading the .graph (the run-length graph as decoded, 4-bit shift quirk included)."""
+    after loading the .graph (the run-length graph as decoded, 4-bit shift quirk included).  lines: the
+    document's drawing, for VGA global's asymmetric mode (Graph.set_drawing)."""
     from .engine import Graph, PointMap
     c = _Chunk(blob)
     reg = np.ascontiguousarray(region, dtype=np.float64)
@@ -92,4 +93,7 @@ def load_chunk(ctx, blob, region):
     pm.h = hp
     info = read_chunk(blob)
     pm.spacing = info["spacing"]
-    return pm, Graph(hg, ctx, pm)
+    g = Graph(hg, ctx, pm)
+    if lines is not None:
+        g.set_drawing(lines)
+    return pm, g

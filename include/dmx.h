@@ -86,7 +86,8 @@ int dmx_ctx_last_timing(dmx_ctx* ctx, double* makegraph_s, double* vga_s);
  * the last VGA preparation spent on the symmetry scatter and its all-reduces (0 when makeGraph did it), [40] the
  * memory-dependent VGA preparation the last tile search ran with (bits: 0 scan order, 1 scan order released for
  * the partial-tile masks, 2 tile-visibility rows, 3 fully-seen rows, 4 tile-to-tile rows, 5 partial-tile masks,
- * 6 row summaries), [41] bytes of tile-visibility rows held, [42] bytes of the scan order held.  n <= 48. */
+ * 6 row summaries, 7 asymmetric mode), [41] bytes of tile-visibility rows held, [42] bytes of the scan order
+ * held, [43] asymmetric mode: nodes whose runs differ from the reference graph (dmx_graph_set_drawing).  n <= 48. */
 int dmx_ctx_last_stats(dmx_ctx* ctx, int64_t* out, int n);
 
 /* The sources the last makeGraph swept a second time (graph node indices, in the order the passes listed
@@ -315,6 +316,15 @@ int dmx_graph_from_runs(dmx_ctx* ctx, dmx_pointmap* pm, int64_t nnodes, const in
  * graph's point map as well (they belong to the points: a chunk written from it saves them).  A chunk
  * (dmx_chunk_merges, dmx_chunk_load) must store every link on both of its points (DMX_ERR_ARG otherwise). */
 int dmx_graph_set_merges(dmx_graph* g, const int32_t* cell_pairs, int64_t n);
+/* The drawing ([n][4] lines x1,y1,x2,y2, the MetaGraph's drawing layers) the graph's point map was made from.  A
+ * graph read back from a .graph file is asymmetric at scale: PixelVec::write stores each run after a bin's first
+ * as a 4-bit row shift (salalib/ngraph.cpp:536-583), so a jump of more than 15 rows moves every later run of the
+ * bin, and Bin::write's unsigned short node count drops the runs of a bin of 65536 k cells (:447-472).  With the
+ * drawing, VGA global makes the map's graph again as a symmetric reference and runs the tile search on it, the
+ * nodes whose runs differ pushing their own runs (exact; DESIGN.md section 2, asymmetric mode); without it, such
+ * a graph takes the top-down search.  Replaces nothing in the reference: its VGA walks the re-read runs as they
+ * are (vgavisualglobal.cpp:96-128), which this reproduces. */
+int dmx_graph_set_drawing(dmx_graph* g, const double* lines, int64_t nlines);
 /* The same links on a point map: written into its PointMap chunk (Point::write, point.cpp:51-73) and
  * followed by the graphs made from it (dmx_makegraph, dmx_graph_assemble_device, dmx_graph_from_runs). */
 int dmx_pointmap_set_merges(dmx_pointmap* pm, const int32_t* cell_pairs, int64_t n);

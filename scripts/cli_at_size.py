@@ -59,15 +59,16 @@ def run_cli(args, limit=None):
 
 
 def read_dmxg(path):
+    """dmxcli's container for a CSV drawing: region, drawing lines, one PointMap chunk of the .graph format"""
     with open(path, "rb") as f:
         assert f.read(4) == b"DMXG"
         f.read(4)
         region = struct.unpack("<4d", f.read(32))
         nl = struct.unpack("<q", f.read(8))[0]
-        f.seek(nl * 32, 1)
+        lines = np.frombuffer(f.read(nl * 32), dtype="<f8").reshape(-1, 4).copy()
         assert f.read(1) == b"\x01"
         n = struct.unpack("<q", f.read(8))[0]
-        return list(region), f.read(n)
+        return list(region), lines, f.read(n)
 
 
 def heartbeat():
@@ -86,6 +87,7 @@ def main():
     ap.add_argument("--nsrc", type=int, default=256)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--cli-vga-seconds", type=float, default=0)
+    ap.add_argument("--no-drawing", action="store_true", help="without the drawing: the top-down search")
     a = ap.parse_args()
     os.makedirs(a.workdir, exist_ok=True)
     rec = {"workload": "dmxcli VISPREP -pg 1 -pp 0.5,0.5 -pm on syn1000 (configs[2] drawing) -> map file -> VGA -vm "
@@ -101,11 +103,12 @@ def main():
     log("VISPREP", rec["visprep_times"], "file %.2f GB" % (rec["map_file_bytes"] / 1e9))
 
     t0 = time.time()
-    region, blob = read_dmxg(vp)
+    region, lines, blob = read_dmxg(vp)
     rec["file_read_s"] = time.time() - t0
     ctx = dmx.Context(0)
     t0 = time.time()
-    pm2, g2 = graphio.load_chunk(ctx, blob, region)   # parse + ShiftLength decode + upload: what dmxcli VGA loads
+    # parse + ShiftLength decode + upload, and the drawing: what dmxcli's VGA step loads
+    pm2, g2 = graphio.load_chunk(ctx, blob, region, lines=None if a.no_drawing else lines)
     rec["decode_upload_s"] = time.time() - t0
     N = g2.info()["nnodes"]
     rec["nnodes"], rec["nruns"] = N, g2.info()["nruns"]
@@ -157,6 +160,7 @@ def main():
     rec["vga_kernel"] = st["vga_kernel"]
     rec["vga_special_nodes"] = st["vga_special_nodes"]
     rec["vga_prep"] = st["vga_prep"]
+    rec["vga_asym_mode"], rec["vga_asym_nodes"] = st["vga_asym_mode"], st["vga_asym_nodes"]
     rec["vga_projected_whole_map_s"] = rec["vga_ms_per_source"] * 1e-3 * N
     log("VGA on the re-read graph:", st["vga_kernel"], "special nodes", st["vga_special_nodes"],
         "%.3f ms a source" % rec["vga_ms_per_source"])
