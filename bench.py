@@ -526,6 +526,12 @@ def main():
                         "vga_cells_decided_by_partial_tile_masks": stats.get("vga_pmask_cells"),
                         "vga_partial_tile_mask_loads": stats.get("vga_pmask_loads"),
                         "vga_partial_tile_mask_bytes": stats.get("vga_pmask_bytes"),
+                        # the memory-dependent preparation this VGA ran with (DESIGN.md sections 1 and 5): scan order
+                        # (or released for the masks), tile-visibility rows, fully-seen rows, tile-to-tile rows,
+                        # partial-tile masks, row summaries
+                        "vga_path": stats.get("vga_prep"),
+                        "vga_tile_rows_bytes": stats.get("vga_tile_rows_bytes"),
+                        "vga_scan_order_bytes": stats.get("vga_scan_bytes"),
                         "vga_runs_full_bfs_equiv": int(g.info()["nruns"]) * nsrc,
                         "makegraph_algorithmic_bytes": mk_bytes, "vga_algorithmic_bytes": vga_bytes,
                         # the bottom-up BFS's symmetry test and early-exit universe rest on 64-bit random-weight

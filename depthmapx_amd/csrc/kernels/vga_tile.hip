@@ -1282,7 +1282,19 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         const int an_node = P.cell_node[x * rows + y];
                         const int64_t rs = P.arun_start[an_node];
                         const int nr = P.anruns[an_node];
-                        for (int r = lane; r < nr; r += 64) run_or(PB, tw, P.apool[rs + r]);
+                        // 4 run loads in flight a lane (the loop is load-latency bound)
+                        for (int r0 = 0; r0 < nr; r0 += 4 * 64) {
+                            Run rr[4];
+#pragma unroll
+                            for (int k = 0; k < 4; k++) {
+                                const int r = r0 + k * 64 + lane;
+                                if (r < nr) rr[k] = P.apool[rs + r];
+                                else rr[k].x0 = -1;
+                            }
+#pragma unroll
+                            for (int k = 0; k < 4; k++)
+                                if (rr[k].x0 >= 0) run_or(PB, tw, rr[k]);
+                        }
                         if (lane == 0) rt += (unsigned)nr;
                     }
                     sync_global();

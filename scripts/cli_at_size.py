@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--cli-vga-seconds", type=float, default=0)
     ap.add_argument("--no-drawing", action="store_true", help="without the drawing: the top-down search")
+    ap.add_argument("--skip-oracle", action="store_true", help="time the VGA block only (no oracle check)")
     a = ap.parse_args()
     os.makedirs(a.workdir, exist_ok=True)
     rec = {"workload": "dmxcli VISPREP -pg 1 -pp 0.5,0.5 -pm on syn1000 (configs[2] drawing) -> map file -> VGA -vm "
@@ -165,6 +166,9 @@ def main():
     log("VGA on the re-read graph:", st["vga_kernel"], "special nodes", st["vga_special_nodes"],
         "%.3f ms a source" % rec["vga_ms_per_source"])
 
+    if a.skip_oracle:
+        print(json.dumps(rec), flush=True)
+        return
     # the oracle's BFS over the same decoded runs (the chunk's arrays), same sources
     from pyoracle import OracleMap
     info = graphio.read_chunk(blob)
