@@ -273,6 +273,7 @@ struct dmx_graph {
     DevBuf<unsigned long long> ftvis;  // full-visibility rows (every non-seed cell of the tile seen)
     DevBuf<unsigned long long> ttvis;  // tile-to-tile full visibility (AND of ftvis over regular cells)
     DevBuf<unsigned long long> tvsum;  // wide grids: per cell, one bit per non-zero tvis row word
+    DevBuf<unsigned long long> tvnz;   // grids up to 256 row words: the same (phase C skips the zero words)
     DevBuf<unsigned long long> pmask;  // partial-tile masks (the cells of each partly seen tile a cell sees)
     DevBuf<int64_t> poff;              // [Ct + 1] start of each cell's masks
     DevBuf<uint16_t> ppre;             // [Ct][tvw] partial tiles of a cell before each row word
@@ -1668,7 +1669,7 @@ static int build_scan_order(dmx_graph* g) {
 static int restore_scan_order(dmx_graph* g) {
     if (!g->scan_released) return DMX_OK;
     g->pmask.reset(); g->ppre.reset(); g->poff.reset();
-    g->tvis.reset(); g->ftvis.reset(); g->tvsum.reset(); g->ttvis.reset();
+    g->tvis.reset(); g->ftvis.reset(); g->tvsum.reset(); g->tvnz.reset(); g->ttvis.reset();
     g->tvw = 0;
     g->tiles_ready = false;
     return build_scan_order(g);
@@ -1900,10 +1901,10 @@ static void prep_state_stats(dmx_ctx* ctx, const dmx_graph* g) {
     if (g->ftvis.p) f |= 8;              // fully-seen tile rows
     if (g->ttvis.p) f |= 16;             // tile-to-tile rows
     if (g->pmask.p) f |= 32;             // partial-tile masks
-    if (g->tvsum.p) f |= 64;             // row summaries (wide grids)
+    if (g->tvsum.p || g->tvnz.p) f |= 64;   // row summaries
     ctx->last_stats[40] = f;
     ctx->last_stats[41] = (long long)((g->tvis.p ? g->tvis.n * 8 : 0) + (g->ftvis.p ? g->ftvis.n * 8 : 0) +
-                                      (g->ttvis.p ? g->ttvis.n * 8 : 0) + (g->tvsum.p ? g->tvsum.n * 8 : 0));
+                                      (g->ttvis.p ? g->ttvis.n * 8 : 0) + (g->tvsum.p ? g->tvsum.n * 8 : 0) + (g->tvnz.p ? g->tvnz.n * 8 : 0));
     ctx->last_stats[42] = (long long)(g->scan_pool.p ? g->scan_pool.n * sizeof(Run) : 0);
 }
 
@@ -2048,6 +2049,15 @@ static int prepare_tiles(dmx_graph* g) {
                                g->tvsum.p);
             HIPCHK(hipGetLastError());
         }
+        // narrow grids with the masks: phase C's row loads skip the cell's zero words (1000^2: 61 % of the words
+        // under a frontier tile row are zero; 32 B a cell)
+        const char* nz_env = getenv("DMX_VGA_TVNZ");
+        if (VGA_TVNZ && !wide && ftv && g->pmask.p && !(nz_env && atoi(nz_env) == 0)) {
+            HIPCHK(g->tvnz.alloc((size_t)Ct * ((tvw + 63) / 64)));
+            hipLaunchKernelGGL(tile_vsum_kernel, dim3((unsigned)((Ct + 3) / 4)), dim3(256), 0, s, Ct, tvw, g->tvis.p,
+                               g->tvnz.p);
+            HIPCHK(hipGetLastError());
+        }
         g->tvw = tvw;
     }
     HIPCHK(hipStreamSynchronize(s));
@@ -2153,6 +2163,23 @@ static int vga_order_rerun(dmx_ctx* ctx, dmx_graph* g, double radius, const uint
 extern "C++" template <int NT, bool SPECIAL, bool RBM, bool FG>
 static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_t lds, int64_t* blocks_out,
                        DevBuf<unsigned long long>& xg, DevBuf<int4>& queue, DevBuf<int32_t>& list) {
+    // The shapes the kernel and its grid assume, checked before the launch: a tile grid that covers
+    // the cells, the frontier (FG false) and the summaries inside the dynamic LDS, row words the fused phase-C
+    // test covers (4 a lane: 256), the 32-bit narrow hint's tile (15 bits) and mask slot (16 bits; a cell's
+    // partial tiles are at most nt), the asymmetric-mode list capacity.
+    {
+        const int64_t nt = (int64_t)Q.tw * Q.th;
+        const char* why = nullptr;
+        if (Q.tw != (Q.cols + 7) / 8 || Q.th != (Q.rows + 7) / 8 || nt <= 0) why = "tile grid does not cover the cells";
+        else if (lds > (size_t)160 * 1024) why = "dynamic LDS above 160 KiB";
+        else if (!FG && (size_t)nt * 8 > lds) why = "frontier bitmap larger than the dynamic LDS";
+        else if (Q.tvis && Q.tvw != Q.th * ((Q.tw + 63) / 64)) why = "tile-visibility row width differs from the tile grid";
+        else if (!FG && Q.pmask && Q.tvw > 256) why = "row words past the fused phase-C test (256)";
+        else if (Q.tvnz && (FG || Q.tvw > 256)) why = "narrow row summaries on a wide grid";
+        else if (Q.pmask && !FG && nt > 32767) why = "narrow mask hint: tile index above 15 bits";
+        else if (Q.asym_tiles && Q.alist_cap <= 0) why = "asymmetric mode without an A-cell list";
+        if (why) return fail(DMX_ERR_STATE, (std::string("VGA tile launch: ") + why).c_str());
+    }
     int occ = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, vga_tile_kernel<NT, SPECIAL, RBM, FG>, NT, lds));
     if (occ < 1) occ = 1;
@@ -2237,6 +2264,7 @@ static int vga_tile_impl(dmx_ctx* ctx, dmx_graph* g, double radius, int gates_on
     Q.scan_pool = g->scan_released ? g->pool.p : g->scan_pool.p;   // (tscan_start then indexes the pool)
     Q.tvis = g->tvw ? g->tvis.p : nullptr; Q.tvw = g->tvw;
     Q.tvsum = (g->tvw && g->tvsum.p) ? g->tvsum.p : nullptr;
+    Q.tvnz = (g->tvw && g->tvnz.p) ? g->tvnz.p : nullptr;
     Q.ftvis = (g->tvw && g->ftvis.p) ? g->ftvis.p : nullptr;
     Q.ttvis = (g->tvw && g->ttvis.p) ? g->ttvis.p : nullptr;
     Q.ttany = Q.ttvis ? g->ttvis.p + (size_t)tw * th * g->tvw : nullptr;

@@ -53,6 +53,8 @@ struct VgaTileParams {
     const uint16_t* ppre;                     // [nt*64][tvw] partial tiles of the cell before each row word
     int tvw;                                  // th * ceil(tw / 64)
     const unsigned long long* tvsum;          // [nt*64][ceil(tvw / 64)] non-zero row words (wide grids; null: off)
+    const unsigned long long* tvnz;           // [nt*64][ceil(tvw / 64)] the same on grids up to 256 row words: phase C
+                                              // loads only a hard cell's non-zero row words (null: off)
     const int32_t* node_cell;
     const int32_t* cell_node;
     const uint8_t* node_flags;
@@ -196,6 +198,20 @@ struct FView {
     const unsigned long long* CB;   // [tw*8][wc]: bit ty of column x: tile (x>>3, ty) has one in column x
     int tw, wr, wc;
 };
+// attribution builds (scripts/gpu_vga_fetch.sh; off by default): row-word counters in phase C, phase C off,
+// phase C without its mask loads
+#ifndef VGA_ROWSTAT
+#define VGA_ROWSTAT 0
+#endif
+#ifndef VGA_PHASEC_OFF
+#define VGA_PHASEC_OFF 0
+#endif
+#ifndef VGA_PHASEC_ROWSONLY
+#define VGA_PHASEC_ROWSONLY 0
+#endif
+#ifndef VGA_TVNZ
+#define VGA_TVNZ 0           // 1 = phase C loads only a hard cell's non-zero row words (row summaries tvnz)
+#endif
 #ifndef VGA_CCH
 #define VGA_CCH 16           // phase C: hard-list entries a wave takes at once (1000^2 VGA: 8 -> 4.133 s, 16 -> 4.143, 32 -> 4.218)
 #endif
@@ -532,30 +548,51 @@ __device__ __forceinline__ bool pmask_hit(const VgaTileParams& P, const unsigned
 // certain hit, none under the partial bits a certain miss, else the masks of the partial frontier tiles.
 __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const unsigned long long* F,
                                                 const unsigned long long* Fsr, int id, unsigned& nload, uint32_t* Hn,
-                                                int& how) {
+                                                int& how, unsigned nzb = 0xFu, unsigned* rstat = nullptr) {
     const int lane = threadIdx.x & 63;
     const int tvw = P.tvw, tw = P.tw, wr = (P.tw + 63) / 64;
     const size_t row = (size_t)id * tvw;
     unsigned long long pw[4], cw[4];
     int base[4];
     bool cert = false;
+    int ct = -1;   // a frontier tile the cell sees completely (the lane's first): k << 6 | bit
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int w = k * 64 + lane;
         const unsigned long long fs = w < tvw ? Fsr[w] : 0ull;
         unsigned long long t = 0ull, f = 0ull;
         base[k] = 0;
-        if (fs) {
+        if (fs && ((nzb >> k) & 1u)) {   // nzb: the lane's row words that are non-zero (tvnz; ftvis lies in tvis)
             t = P.tvis[row + w];
             f = P.ftvis[row + w];
         }
+        if (ct < 0 && (f & fs) != 0ull) ct = (k << 6) | (__ffsll((long long)(f & fs)) - 1);
         cert |= (f & fs) != 0ull;
         pw[k] = t & ~f;
         cw[k] = pw[k] & fs;
+#if VGA_ROWSTAT
+        if (rstat) {   // diagnostic build: row words loaded (per array), zero in tvis, zero in ftvis
+            rstat[0] += __popcll(__ballot(fs != 0ull && ((nzb >> k) & 1u)));
+            rstat[1] += __popcll(__ballot(fs != 0ull && t == 0ull));
+            rstat[2] += __popcll(__ballot(fs != 0ull && f == 0ull));
+        }
+#endif
     }
-    if (__ballot(cert) != 0ull) { how = 1; return true; }
+    if (const unsigned long long cb = __ballot(cert)) {
+        // the next source's phase B tests that tile first (slot 0xFFFF: the whole tile, no mask)
+        if (lane == __ffsll((long long)cb) - 1) {
+            const int w = (ct >> 6) * 64 + lane;
+            const int t = (w / wr) * tw + (w % wr) * 64 + (ct & 63);
+            Hn[id] = 0x80000000u | ((uint32_t)t << 16) | 0xFFFFu;
+        }
+        how = 1;
+        return true;
+    }
     if (__ballot((cw[0] | cw[1] | cw[2] | cw[3]) != 0ull) == 0ull) { how = 2; return false; }
     how = 0;
+#if VGA_PHASEC_ROWSONLY
+    return false;   // attribution build: no mask loads (results differ)
+#endif
 #pragma unroll
     for (int k = 0; k < 4; k++) base[k] = cw[k] ? (int)P.ppre[row + k * 64 + lane] : 0;
     const unsigned long long* pm = P.pmask + P.poff[id];
@@ -988,7 +1025,10 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             htile = (int)(hmw >> 32) - 1;
                             hmk = P.pmask[pof + (uint32_t)hmw];
                         } else if (hp != 0xFFFFFFFFu && (hp >> 31)) {
-                            if (P.pmask) { htile = (int)((hp >> 16) & 0x7FFFu); hmk = P.pmask[pof + (hp & 0xFFFFu)]; }
+                            if (P.pmask) {   // a partial tile and its mask, or (slot 0xFFFF) a tile seen completely
+                                htile = (int)((hp >> 16) & 0x7FFFu);
+                                hmk = (hp & 0xFFFFu) == 0xFFFFu ? ~0ull : P.pmask[pof + (hp & 0xFFFFu)];
+                            }
                         } else if (hp >= KH && hp < (uint32_t)nr) {
                             hr = P.scan_pool[ss + hp];
                         }
@@ -1068,6 +1108,14 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     if (it0 >= hn) break;
                     const int cn = min(CCH, hn - it0);
                     const int myv = lane < cn ? L[it0 + lane] : -1;
+                    // the chunk's non-zero row summaries (tvnz), one load: lane 4j + k holds word k of entry j
+                    static_assert(CCH * 4 <= 64, "tvnz prefetch: 4 summary words an entry");
+                    unsigned long long nzp = ~0ull;
+                    if (VGA_TVNZ && !FG && P.tvnz) {
+                        const int jj = lane >> 2, kk = lane & 3, tvsw = (P.tvw + 63) >> 6;
+                        const int vj = __shfl(myv, jj);
+                        if (jj < cn && kk < tvsw) nzp = P.tvnz[(size_t)(vj < 0 ? -1 - vj : vj) * tvsw + kk];
+                    }
                     unsigned long long certain_m = 0ull, pruned_m = 0ull;   // bit j: chunk entry j
                     if (P.tvis && (!P.pmask || (FG && VGA_WIDE_ROWPASS && P.tvsum))) {   // (wide grids: a row pass in front of the masks)
                         for (int j = 0; j < cn; j += 2) {
@@ -1152,6 +1200,17 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         if (special) id = -1 - id;
                         bool found = false;
                         int nr = 0;
+                        unsigned nzb = 0xFu;   // row words k*64 + lane (k < 4) that are non-zero for the cell
+                        if (VGA_TVNZ && !FG && P.tvnz) {
+                            nzb = 0u;
+#pragma unroll
+                            for (int k = 0; k < 4; k++) {
+                                const unsigned long long sk =
+                                    (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)nzp, j * 4 + k) |
+                                    ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)(unsigned)(nzp >> 32), j * 4 + k) << 32);
+                                nzb |= (unsigned)((sk >> lane) & 1ull) << k;
+                            }
+                        }
                         if (SPECIAL && special) {
                             int x, y;
                             xy_of_tile_id(id, tw, x, y);
@@ -1161,7 +1220,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                                 // no Missing cell in the frontier: in-set meets F iff cells(v) does (the masks)
                                 unsigned nl = 0;
                                 int how = 0;
-                                found = (FG && P.tvsum) ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+                                found = (FG && P.tvsum) ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how, nzb);
                             } else if (!found) {
                                 found = special_hit(P, FV, id, x, y, &nr);
                                 if (lane == 0) rt += (unsigned)nr;
@@ -1170,7 +1229,15 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         } else if (P.pmask) {
                             unsigned nl = 0;
                             int how = 0;
-                            found = (FG && P.tvsum) ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how);
+#if VGA_PHASEC_OFF
+                            found = false;   // attribution build: phase C reads nothing (results differ)
+#elif VGA_ROWSTAT
+                            unsigned rsv[3] = {0u, 0u, 0u};
+                            found = (FG && P.tvsum) ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how, nzb, rsv);
+                            if (lane == 0) { ST(22, rsv[0]); ST(26, rsv[1]); ST(28, rsv[2]); }
+#else
+                            found = (FG && P.tvsum) ? pmask_hit_wide(P, F, Fsr, id, nl) : pmask_hit_fused(P, F, Fsr, id, nl, Hn, how, nzb);
+#endif
                             if (lane == 0) {
                                 ST(14, 1);
                                 if (how == 1) { ST(16, 1); }
@@ -1757,7 +1824,7 @@ __global__ void tile_tt_kernel(int nt, int tvw, const unsigned long long* regula
     }
 }
 
-// Row summary of the tile-visibility rows on wide grids (tvw > 256 words, no masks): bit w of a cell's
+// Row summary of the tile-visibility rows (wide grids: tvsum; up to 256 words: tvnz): bit w of a cell's
 // summary is set iff its row word w is non-zero, so phase C's miss certificate reads only the words the
 // cell has (a dense map's cell sees a few % of the tiles) instead of every word under a frontier tile row.
 // One wave per cell: summary word j is the ballot of row words 64j .. 64j + 63 being non-zero.
