@@ -2193,9 +2193,16 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     DevBuf<uint32_t> hint;
     HIPCHK(hint.alloc((size_t)nt * 64));
     HIPCHK(hipMemsetAsync(hint.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
+    DevBuf<uint32_t> hint2;   // (narrow grids with the masks) the second, fully-seen-tile hint
     DevBuf<int32_t> mseen;   // per workgroup: merge_order_check stamps
     DevBuf<int32_t> alist;   // asymmetric mode: per workgroup, the frontier's A cells
     VgaTileParams P = Q;
+    P.hint2 = nullptr;
+    if (Q.pmask && !FG && !getenv("DMX_VGA_NOHINT2")) {
+        HIPCHK(hint2.alloc((size_t)nt * 64));
+        HIPCHK(hipMemsetAsync(hint2.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
+        P.hint2 = hint2.p;
+    }
     if (Q.asym_tiles) {
         HIPCHK(alist.alloc((size_t)blocks * Q.alist_cap));
         P.alist = alist.p;

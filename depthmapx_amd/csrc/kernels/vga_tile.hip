@@ -77,6 +77,8 @@ struct VgaTileParams {
     uint32_t* hint;           // [nt*64] what last hit for a recent source: the scan position of a run, or
                               // (bit 31) a partial-tile mask: tile << 16 | its slot in the cell's list (~0u:
                               // none); shared by all workgroups: a stale value only costs one test
+    uint32_t* hint2;          // [nt*64] (narrow grids with the masks) a second hint: the fully seen tile the cell's
+                              // hint held before a later hit replaced it (0x80000000 | tile << 16 | 0xFFFF), or ~0
     unsigned long long* hintw;// [nt*64] wide grids' mask hints (their tile index needs 16 bits): (tile + 1) << 32 |
                               // slot, 0 none (null below 1024 cells a side)
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
@@ -556,6 +558,8 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
     int base[4];
     bool cert = false;
     int ct = -1;   // a frontier tile the cell sees completely (the lane's first): k << 6 | bit
+    // the hint a hit here replaces: a fully seen tile moves to the second hint (loaded with the rows)
+    const uint32_t hold = P.hint2 ? Hn[id] : 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int w = k * 64 + lane;
@@ -583,7 +587,9 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
         if (lane == __ffsll((long long)cb) - 1) {
             const int w = (ct >> 6) * 64 + lane;
             const int t = (w / wr) * tw + (w % wr) * 64 + (ct & 63);
-            Hn[id] = 0x80000000u | ((uint32_t)t << 16) | 0xFFFFu;
+            const uint32_t hnew = 0x80000000u | ((uint32_t)t << 16) | 0xFFFFu;
+            if (P.hint2 && (hold & 0x8000FFFFu) == 0x8000FFFFu && hold != 0xFFFFFFFFu && hold != hnew) P.hint2[id] = hold;
+            Hn[id] = hnew;
         }
         how = 1;
         return true;
@@ -625,7 +631,10 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
                 if (tl[j] >= 0 && (F[tl[j]] & mk[j])) { hj = j; ht = tl[j]; hq = sl[j]; }
             const unsigned long long hb = __ballot(hj >= 0);
             if (hb != 0ull) {
-                if (lane == __ffsll((long long)hb) - 1) Hn[id] = 0x80000000u | ((uint32_t)ht << 16) | (uint32_t)hq;
+                if (lane == __ffsll((long long)hb) - 1) {
+                    if (P.hint2 && (hold & 0x8000FFFFu) == 0x8000FFFFu && hold != 0xFFFFFFFFu) P.hint2[id] = hold;
+                    Hn[id] = 0x80000000u | ((uint32_t)ht << 16) | (uint32_t)hq;
+                }
                 return true;
             }
         }
@@ -954,7 +963,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const bool cand = ((mask >> lane) & 1ull) && lreg;
                     int64_t ss = 0;
                     int nr = 0;
-                    uint32_t hp = 0xFFFFFFFFu;
+                    uint32_t hp = 0xFFFFFFFFu, hp2 = 0xFFFFFFFFu;
                     unsigned long long hmw = 0ull;   // (wide grids) a mask hint
                     int64_t pof = 0;
                     // heads loaded with the cell's first loads, the rest of the KH heads in the extension loop
@@ -965,6 +974,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         ss = P.tscan_start[id];
                         nr = P.tnruns[id];
                         hp = Hn[id];
+                        if (!FG && P.hint2) hp2 = P.hint2[id];
                         if (FG && P.hintw) hmw = P.hintw[id];
                         if (P.pmask) pof = P.poff[id];
                         hd0 = run_word(P.heads + id);
@@ -1040,6 +1050,7 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             }
                         if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
                         else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
+                        if (!hit && hp2 != 0xFFFFFFFFu) { rt++; hit = F[(hp2 >> 16) & 0x7FFFu] != 0ull; }   // a fully seen tile
                         // past the heads only in scan order: after the masks took the scan order's place (wide grids)
                         // the runs are in pool order, where positions KH.. are not the runs after the heads
                         const int next = (P.scan_pool == P.pool) ? KH : KH + P.bext;

@@ -94,6 +94,10 @@ def exchange_graph(pm, ctx, shard, dist, device):
     sync()
     t3 = time.perf_counter()
     del flat
+    if cuda:
+        # hand the buffer back to the device: libdmx sizes the VGA preparation (tile rows, partial-tile masks) from
+        # hipMemGetInfo, which counts torch's cached blocks as used (memory budget)
+        torch.cuda.empty_cache()
     return g, {"blob_s": t1 - t0, "allgather_s": t2 - t1, "assemble_s": t3 - t2, "bytes": sum(sizes),
                "padded_bytes": world * mx, "device_peak_bytes": peak[0] if cuda else None}
 
