@@ -2198,9 +2198,9 @@ static int launch_tile(dmx_ctx* ctx, const VgaTileParams& Q, int64_t nsrc, size_
     DevBuf<int32_t> alist;   // asymmetric mode: per workgroup, the frontier's A cells
     VgaTileParams P = Q;
     P.hint2 = nullptr;
-    if (Q.pmask && !FG && !getenv("DMX_VGA_NOHINT2")) {
-        HIPCHK(hint2.alloc((size_t)nt * 64));
-        HIPCHK(hipMemsetAsync(hint2.p, 0xFF, (size_t)nt * 64 * 4, ctx->stream));
+    if (VGA_H2 > 0 && Q.pmask && !FG && !getenv("DMX_VGA_NOHINT2")) {
+        HIPCHK(hint2.alloc((size_t)nt * 64 * VGA_H2));
+        HIPCHK(hipMemsetAsync(hint2.p, 0xFF, (size_t)nt * 64 * 4 * VGA_H2, ctx->stream));
         P.hint2 = hint2.p;
     }
     if (Q.asym_tiles) {

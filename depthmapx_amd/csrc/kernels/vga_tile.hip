@@ -77,8 +77,9 @@ struct VgaTileParams {
     uint32_t* hint;           // [nt*64] what last hit for a recent source: the scan position of a run, or
                               // (bit 31) a partial-tile mask: tile << 16 | its slot in the cell's list (~0u:
                               // none); shared by all workgroups: a stale value only costs one test
-    uint32_t* hint2;          // [nt*64] (narrow grids with the masks) a second hint: the fully seen tile the cell's
-                              // hint held before a later hit replaced it (0x80000000 | tile << 16 | 0xFFFF), or ~0
+    uint32_t* hint2;          // [VGA_H2][nt*64] (narrow grids with the masks) more hints: the fully seen tiles the
+                              // cell's hint held before later hits replaced it, newest first
+                              // (0x80000000 | tile << 16 | 0xFFFF), or ~0
     unsigned long long* hintw;// [nt*64] wide grids' mask hints (their tile index needs 16 bits): (tile + 1) << 32 |
                               // slot, 0 none (null below 1024 cells a side)
     unsigned long long* xg;   // per workgroup [2][nt]: V (visited) then X (next level)
@@ -211,6 +212,12 @@ struct FView {
 #ifndef VGA_PHASEC_ROWSONLY
 #define VGA_PHASEC_ROWSONLY 0
 #endif
+#ifndef VGA_HINTS
+#define VGA_HINTS 3          // hint slots a cell (narrow grids with the masks): the hint + VGA_HINTS - 1 fully seen
+                             // tiles in hint2 (1000^2 VGA: 1 -> 3.858 s, 2 -> 3.684, 3 -> 3.568)
+#endif
+#define VGA_H2 (VGA_HINTS - 1)   // slots of hint2: [VGA_H2][nt*64]
+static_assert(VGA_HINTS >= 2, "hint2 holds at least one slot");
 #ifndef VGA_TVNZ
 #define VGA_TVNZ 0           // 1 = phase C loads only a hard cell's non-zero row words (row summaries tvnz)
 #endif
@@ -545,6 +552,18 @@ __device__ __forceinline__ bool pmask_hit(const VgaTileParams& P, const unsigned
     return false;
 }
 
+// A hit replaced the cell's hint `hold`: a fully seen tile moves to the front of hint2, whose slots shift down
+// (h2old: the slots before the last, loaded with the cell's row words).  One lane writes.
+__device__ __forceinline__ void hint2_push(const VgaTileParams& P, int id, uint32_t hold, const uint32_t* h2old) {
+    const size_t stride = (size_t)P.tw * P.th * 64;
+#pragma unroll
+    for (int k = 0; k + 1 < VGA_H2; k++)
+        if (h2old[k] == hold) return;   // already held: keep the order
+#pragma unroll
+    for (int k = VGA_H2 - 1; k >= 1; k--) P.hint2[(size_t)k * stride + id] = h2old[k - 1];
+    P.hint2[id] = hold;
+}
+
 // C_FUSED: the row test and the mask test in one pass per cell (no separate row-test pass over the chunk):
 // the 4 row words of tvis and ftvis a lane owns are loaded together, a frontier tile under the full row is a
 // certain hit, none under the partial bits a certain miss, else the masks of the partial frontier tiles.
@@ -560,6 +579,9 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
     int ct = -1;   // a frontier tile the cell sees completely (the lane's first): k << 6 | bit
     // the hint a hit here replaces: a fully seen tile moves to the second hint (loaded with the rows)
     const uint32_t hold = P.hint2 ? Hn[id] : 0xFFFFFFFFu;
+    uint32_t h2old[VGA_H2 > 1 ? VGA_H2 - 1 : 1];   // the slots that shift down when the hint moves into hint2
+#pragma unroll
+    for (int k = 0; k + 1 < VGA_H2; k++) h2old[k] = P.hint2 ? P.hint2[(size_t)k * P.tw * P.th * 64 + id] : 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const int w = k * 64 + lane;
@@ -588,7 +610,9 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
             const int w = (ct >> 6) * 64 + lane;
             const int t = (w / wr) * tw + (w % wr) * 64 + (ct & 63);
             const uint32_t hnew = 0x80000000u | ((uint32_t)t << 16) | 0xFFFFu;
-            if (P.hint2 && (hold & 0x8000FFFFu) == 0x8000FFFFu && hold != 0xFFFFFFFFu && hold != hnew) P.hint2[id] = hold;
+            if (P.hint2 && (hold & 0x8000FFFFu) == 0x8000FFFFu && hold != 0xFFFFFFFFu && hold != hnew) {
+                hint2_push(P, id, hold, h2old);
+            }
             Hn[id] = hnew;
         }
         how = 1;
@@ -632,7 +656,9 @@ __device__ __forceinline__ bool pmask_hit_fused(const VgaTileParams& P, const un
             const unsigned long long hb = __ballot(hj >= 0);
             if (hb != 0ull) {
                 if (lane == __ffsll((long long)hb) - 1) {
-                    if (P.hint2 && (hold & 0x8000FFFFu) == 0x8000FFFFu && hold != 0xFFFFFFFFu) P.hint2[id] = hold;
+                    if (P.hint2 && (hold & 0x8000FFFFu) == 0x8000FFFFu && hold != 0xFFFFFFFFu) {
+                        hint2_push(P, id, hold, h2old);
+                    }
                     Hn[id] = 0x80000000u | ((uint32_t)ht << 16) | (uint32_t)hq;
                 }
                 return true;
@@ -963,7 +989,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                     const bool cand = ((mask >> lane) & 1ull) && lreg;
                     int64_t ss = 0;
                     int nr = 0;
-                    uint32_t hp = 0xFFFFFFFFu, hp2 = 0xFFFFFFFFu;
+                    uint32_t hp = 0xFFFFFFFFu, hp2[VGA_H2];
+#pragma unroll
+                    for (int k = 0; k < VGA_H2; k++) hp2[k] = 0xFFFFFFFFu;
                     unsigned long long hmw = 0ull;   // (wide grids) a mask hint
                     int64_t pof = 0;
                     // heads loaded with the cell's first loads, the rest of the KH heads in the extension loop
@@ -974,7 +1002,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                         ss = P.tscan_start[id];
                         nr = P.tnruns[id];
                         hp = Hn[id];
-                        if (!FG && P.hint2) hp2 = P.hint2[id];
+                        if (!FG && P.hint2)
+#pragma unroll
+                            for (int k = 0; k < VGA_H2; k++) hp2[k] = P.hint2[(size_t)k * nt * 64 + id];
                         if (FG && P.hintw) hmw = P.hintw[id];
                         if (P.pmask) pof = P.poff[id];
                         hd0 = run_word(P.heads + id);
@@ -1050,7 +1080,9 @@ __global__ void __launch_bounds__(NT) vga_tile_kernel(const VgaTileParams* __res
                             }
                         if (!hit && htile >= 0) { rt++; hit = (F[htile] & hmk) != 0ull; }
                         else if (!hit && hr.x0 >= 0) { rt++; hit = run_hits_fs(FV, hr); }
-                        if (!hit && hp2 != 0xFFFFFFFFu) { rt++; hit = F[(hp2 >> 16) & 0x7FFFu] != 0ull; }   // a fully seen tile
+#pragma unroll
+                        for (int k = 0; k < VGA_H2; k++)   // fully seen tiles
+                            if (!hit && hp2[k] != 0xFFFFFFFFu) { rt++; hit = F[(hp2[k] >> 16) & 0x7FFFu] != 0ull; }
                         // past the heads only in scan order: after the masks took the scan order's place (wide grids)
                         // the runs are in pool order, where positions KH.. are not the runs after the heads
                         const int next = (P.scan_pool == P.pool) ? KH : KH + P.bext;
