@@ -72,15 +72,15 @@ def nearest_filled(pm, x, y):
     raise RuntimeError("no filled cell")
 
 
-# the newest round's PMC summary of the shipped build (scripts/gpu_r5_evidence.sh writes r5)
-PMC_SUMMARY = next((p for p in (os.path.join(REPO, "profiles", "r%d_pmc.json" % r) for r in (5, 4, 3)) if os.path.exists(p)),
-                   os.path.join(REPO, "profiles", "r5_pmc.json"))
+# the newest round's PMC summary of the shipped build (scripts/gpu_evidence.sh ROUND=6 writes r6)
+PMC_SUMMARY = next((p for p in (os.path.join(REPO, "profiles", "r%d_pmc.json" % r) for r in (6, 5, 4, 3)) if os.path.exists(p)),
+                   os.path.join(REPO, "profiles", "r6_pmc.json"))
 FP64_PEAK_TF = 78.6    # MI355X FP64 vector (MI355X_MICROARCH.md)
 
 
 def load_pmc(workload):
     """Per-kernel PMC summary of the same workload and build (scripts/gpu_pmc.sh -> scripts/pmc_summary.py ->
-    profiles/r5_pmc.json): HBM bytes raw and 2x-FETCH corrected, L2 hit rate, VALU issue, FP64 instruction
+    profiles/r<round>_pmc.json): HBM bytes raw and 2x-FETCH corrected, L2 hit rate, VALU issue, FP64 instruction
     counts."""
     if not os.path.exists(PMC_SUMMARY):
         return {}

@@ -27,6 +27,15 @@ namespace dmx {
 #ifndef MK_PFIND
 #define MK_PFIND 1   // the prefetch also keeps the first chunk's candidate index and gap bounds in registers (A/B hook)
 #endif
+#ifndef MK_SPAN_CB
+#define MK_SPAN_CB 0      // span pieces: the classes some lane has from 5 ballots (1) or two wave max scans (0) (A/B hook)
+#endif
+#ifndef MK_SPAN_GSKIP
+#define MK_SPAN_GSKIP 0   // span rows: skip a gap no row of the chunk can see over the span (A/B hook)
+#endif
+#ifndef MK_SPAN_LSUM
+#define MK_SPAN_LSUM 0    // span counts (visible, examined) kept per lane and reduced once per source (A/B hook)
+#endif
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
 // shortest occluder-free span taken, in depths (DMX_MK_SPAN overrides): configs[2] / configs[4] makeGraph with
 // 1: 3.23 / 9.61 s, 2: 3.17 / 9.02, 4: 3.11 / 8.61, 8: 3.11 / 8.75 (profiles/r6_span_ab.jsonl)
@@ -412,9 +421,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
     // 0 collectgarbage, 1 visit ranges, 2 candidate tests + blocks, 3 visible: bins, 4 visible: serial
     // moments, 5 visible: run tracking, 6 octant flush + placement, 7 publish, 8 depth tail (next depth's
     // prefetch), 9 octant setup + depth 0
-    unsigned long long cyc[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // (10: spans)
+    // (10: spans, outside 11 its rows' class ends and open state, 12 the per-gap depth searches, 13 the per-class pieces)
+    unsigned long long cyc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long mst[4] = {0, 0, 0, 0};   // PROF: merges, one-block merges, blocks, gaps at merges
-    unsigned long long spst[3] = {0, 0, 0};     // PROF: spans, span depths, span cells
+    unsigned long long spst[6] = {0, 0, 0, 0, 0, 0};   // PROF: spans, span depths, span cells, row chunks, (chunk, gap)
+                                                       // pairs, pairs with no visible row
     unsigned long long tmark = PROF ? __builtin_amdgcn_s_memtime() : 0;
 
     for (;;) {
@@ -442,6 +453,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
         int mcnt = 0;                // this lane's summand count
         int nsize = 0;
         unsigned long long examined = 0;
+#if MK_SPAN_LSUM
+        int nsize_l = 0;                    // this lane's share of the spans' visible cells / cells examined
+        unsigned long long examined_l = 0;
+#endif
         uint32_t nsteps = 0, nchunks = 0;   // sieve depth steps / 64-candidate chunks (the source's work)
         int bpos = 0;        // next free run slot in stageB
         bool failed = false;
@@ -960,9 +975,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         }
                         uint32_t o = live ? ld_open(ind) : 0u;
                         bool diag = false;
+                        if (PROF) spst[3]++;
+                        MK_T(11);
                         for (int g = ng - 1; g >= 0; g--) {   // later gaps first: the row's depths in order
                             const double2 z = L.gaps[g], iz = L.gaps2[g];
                             const double gs_ = z.x, ge_ = z.y;
+#if MK_SPAN_GSKIP
+                            // rows below cl(s, d0) or above ch(e, d1) see no depth of the span in this gap
+                            if (ballot(live && ind >= gap_cl(gs_, d0) && ind <= gap_ch(ge_, d1)) == 0ull) continue;
+#endif
                             int p = 1, r = 0;
                             if (live) {
                                 // first d with ch(e, d) >= ind; last d with cl(s, d) <= ind and b(e_prev, d) <= ind
@@ -1006,10 +1027,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                             // pieces in depth order: the diagonal cell, ratio classes 3, 2, 1 (row 0: the axis, class 0);
                             // only the classes some lane has
                             const bool has = p <= r;
+                            if (PROF) { spst[4]++; spst[5] += (ballot(has) == 0ull); }
+                            MK_T(12);
                             const int chi = (ind == 0) ? 0 : (ind >= p && ind <= r) ? 4 : (p <= t3) ? 3 : (p <= t2) ? 2 : 1;
                             const int clo = (ind == 0) ? 0 : (r <= t3) ? 3 : (r <= t2) ? 2 : 1;
+#if MK_SPAN_CB
+                            // the classes in some lane's [clo, chi], highest first (the others have no piece anywhere)
+                            unsigned cset = 0;
+#pragma unroll
+                            for (int c5 = 0; c5 < 5; c5++) cset |= (ballot(has && clo <= c5 && c5 <= chi) != 0ull) ? (1u << c5) : 0u;
+                            for (; cset; cset &= ~(1u << (31 - __clz((int)cset)))) {
+                                const int cc = 31 - __clz((int)cset);
+#else
                             int cmax = wave_incl_max_all(has ? chi : -1), cmin = -wave_incl_max_all(has ? -clo : -5);
                             for (int cc = cmax; cc >= cmin; cc--) {
+#endif
                                 int a = 1, b = 0;
                                 if (ind == 0) { if (cc == 0) { a = p; b = r; } }
                                 else if (cc == 4) { a = max(p, ind); b = min(r, ind); }
@@ -1047,6 +1079,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                                     nA += __popcll(em);
                                 }
                             }
+                            MK_T(13);
                         }
                         if (live) st_open(ind, o);
                         const unsigned long long dm = ballot(diag);   // diagonal cells: rows ascending = depths ascending
@@ -1069,6 +1102,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                         }
                         if (d <= d1) exs += (unsigned long long)T;
                     }
+#if MK_SPAN_LSUM
+                    examined_l += exs;
+                    nsize_l += nsp;
+                    if (PROF) {
+                        for (int off = 32; off >= 1; off >>= 1) nsp += __shfl_xor(nsp, off);
+                        spst[0]++; spst[1] += (unsigned long long)(d1 - d0 + 1); spst[2] += (unsigned long long)__shfl(nsp, 0);
+                    }
+#else
                     for (int off = 32; off >= 1; off >>= 1) {
                         exs += __shfl_xor(exs, off);
                         nsp += __shfl_xor(nsp, off);
@@ -1076,6 +1117,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     examined += __shfl(exs, 0);
                     nsize += __shfl(nsp, 0);
                     if (PROF) { spst[0]++; spst[1] += (unsigned long long)(d1 - d0 + 1); spst[2] += (unsigned long long)__shfl(nsp, 0); }
+#endif
                     if (COUNT || PROF) nsteps++;
                     depth = d1;
                     dq = depth;
@@ -1273,6 +1315,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
             __syncthreads();
             MK_T(6);
         }
+#if MK_SPAN_LSUM
+        for (int off = 32; off >= 1; off >>= 1) {
+            nsize_l += __shfl_xor(nsize_l, off);
+            examined_l += __shfl_xor(examined_l, off);
+        }
+        nsize += __shfl(nsize_l, 0);
+        examined += __shfl(examined_l, 0);
+#endif
         float m1f = 0.0f, m2f = 0.0f;
         if (!failed) {
             if (exact) {
@@ -1371,15 +1421,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 for (int i = 0; i < 10; i++) atomicAdd(&P.stats[8 + i], cyc[i]);
                 atomicAdd(&P.stats[22], cyc[10]);
                 for (int i = 0; i < 3; i++) atomicAdd(&P.stats[23 + i], spst[i]);
+                for (int i = 0; i < 3; i++) atomicAdd(&P.stats[26 + i], cyc[11 + i]);
+                for (int i = 0; i < 3; i++) atomicAdd(&P.stats[29 + i], spst[3 + i]);
             }
             P.attrs[k * 3 + 0] = (float)nsize;
             P.attrs[k * 3 + 1] = m1f;
             P.attrs[k * 3 + 2] = m2f;
         }
         __syncthreads();
-        for (int i = 0; i < 11; i++) cyc[i] = 0;
+        for (int i = 0; i < 14; i++) cyc[i] = 0;
         for (int i = 0; i < 4; i++) mst[i] = 0;
-        for (int i = 0; i < 3; i++) spst[i] = 0;
+        for (int i = 0; i < 6; i++) spst[i] = 0;
         MK_T(7);
     }
 }

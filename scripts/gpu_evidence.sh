@@ -1,11 +1,12 @@
 #!/bin/bash
-# Round-5 evidence: PART=2 -- configs[2] PMC passes -> profiles/r5_pmc.json, smoke(), the bench (STEPS/WARMUP,
+# Round evidence (ROUND, default 6): PART=2 -- configs[2] PMC passes -> profiles/r${RD}_pmc.json, smoke(), the bench (STEPS/WARMUP,
 # CPU leg) under a kernel-trace + stats profile; PART=5 -- the configs[4] (bench --config 5) PMC passes and its
 # bench line.  The PMC summary is written here on the box and merged back through gpurun_out/.
 set -o pipefail
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$PWD}
-T=${TAG:-r5evidence}
+RD=${ROUND:-6}
+T=${TAG:-r${RD}evidence}
 OUT=$R/gpurun_out/$T
 mkdir -p $OUT
 cd $R
@@ -16,8 +17,8 @@ W5="synthetic-1999/5000-occluders VISPREP -pg 1 -pp 0.5,0.5 -pm + STEPDEPTH -sdt
 if [ "${PART:-2}" = 2 ]; then
   TAG=$T/pmc2 bash scripts/gpu_pmc.sh > $OUT/pmc2.log 2>&1
   rc=$?
-  python3 scripts/pmc_summary.py gpurun_out/$T/pmc2 "$W2" $OUT/r5_pmc.json > $OUT/pmc2_summary.log 2>&1
-  cp $OUT/r5_pmc.json profiles/r5_pmc.json   # the bench below reads it
+  python3 scripts/pmc_summary.py gpurun_out/$T/pmc2 "$W2" $OUT/r${RD}_pmc.json > $OUT/pmc2_summary.log 2>&1
+  cp $OUT/r${RD}_pmc.json profiles/r${RD}_pmc.json   # the bench below reads it
   [ $rc = 0 ] && timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 && \
   t0=$(date +%s.%N) && \
   timeout -k 10 600 python -u bench.py --gpus 1 --steps ${STEPS:-10} --warmup ${WARMUP:-2} > $OUT/bench.log 2> $OUT/bench_progress.txt && \
@@ -25,11 +26,11 @@ if [ "${PART:-2}" = 2 ]; then
   rc=$?
   tail -5 $OUT/pmc2.log; tail -2 $OUT/smoke.log; grep '^{' $OUT/bench.log | cut -c1-300; tail -1 $OUT/bench_progress.txt
 else
-  cp profiles/r5_pmc.json $OUT/r5_pmc.json 2>/dev/null
+  cp profiles/r${RD}_pmc.json $OUT/r${RD}_pmc.json 2>/dev/null
   TAG=$T/pmc5 BENCH_ARGS="--config 5" bash scripts/gpu_pmc.sh > $OUT/pmc5.log 2>&1
   rc=$?
-  python3 scripts/pmc_summary.py gpurun_out/$T/pmc5 "$W5" $OUT/r5_pmc.json > $OUT/pmc5_summary.log 2>&1
-  cp $OUT/r5_pmc.json profiles/r5_pmc.json
+  python3 scripts/pmc_summary.py gpurun_out/$T/pmc5 "$W5" $OUT/r${RD}_pmc.json > $OUT/pmc5_summary.log 2>&1
+  cp $OUT/r${RD}_pmc.json profiles/r${RD}_pmc.json
   [ $rc = 0 ] && timeout -k 10 400 python -u bench.py --gpus 1 --config 5 --steps 2 --warmup 1 > $OUT/bench5.log 2> $OUT/bench5_progress.txt && \
   timeout -k 10 600 python -u -m pytest -x -v --timeout 500 --timeout-method thread -m gpu \
     tests/test_gpu_scale.py -k "2000_vga_sources" > $OUT/vga2000_wide_tests.log 2>&1
