@@ -27,14 +27,15 @@ namespace dmx {
 #ifndef MK_PFIND
 #define MK_PFIND 1   // the prefetch also keeps the first chunk's candidate index and gap bounds in registers (A/B hook)
 #endif
+// span A/B hooks, configs[2] / configs[4] makeGraph seconds on one box (profiles/r6_span_ab2.jsonl; off: 3.118 / 8.692):
 #ifndef MK_SPAN_CB
-#define MK_SPAN_CB 0      // span pieces: the classes some lane has from 5 ballots (1) or two wave max scans (0) (A/B hook)
+#define MK_SPAN_CB 0      // the classes some lane has from 5 ballots instead of two wave max scans: 3.245 / 8.880
 #endif
 #ifndef MK_SPAN_GSKIP
-#define MK_SPAN_GSKIP 0   // span rows: skip a gap no row of the chunk can see over the span (A/B hook)
+#define MK_SPAN_GSKIP 1   // skip a gap no row of the chunk can see over the span: 2.948 / 8.458
 #endif
 #ifndef MK_SPAN_LSUM
-#define MK_SPAN_LSUM 0    // span counts (visible, examined) kept per lane and reduced once per source (A/B hook)
+#define MK_SPAN_LSUM 1    // span counts (visible, examined) kept per lane, reduced once per source: 3.060 / 8.423
 #endif
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
 // shortest occluder-free span taken, in depths (DMX_MK_SPAN overrides): configs[2] / configs[4] makeGraph with
