@@ -34,6 +34,12 @@ namespace dmx {
 #ifndef MK_SPAN_GSKIP
 #define MK_SPAN_GSKIP 1   // skip a gap no row of the chunk can see over the span: 2.948 / 8.458
 #endif
+#ifndef MK_WFRED
+#define MK_WFRED 0        // span integer wave max / min through the DPP whole-wave reductions: 3.020 / 8.365 (gl 2.877 / 8.251)
+#endif
+#ifndef MK_SPAN_RCP
+#define MK_SPAN_RCP 0     // span row estimates from v_rcp_f64 instead of divisions (settled exactly either way): 2.886 / 8.237
+#endif
 #ifndef MK_SPAN_LSUM
 #define MK_SPAN_LSUM 1    // span counts (visible, examined) kept per lane, reduced once per source: 3.060 / 8.423
 #endif
@@ -180,9 +186,14 @@ __device__ __forceinline__ int wave_incl_max(int v) {
     return v;
 }
 // max over all 64 lanes (every lane gets it)
+// (all 64 lanes active at every call)
 __device__ __forceinline__ int wave_incl_max_all(int v) {
+#if MK_WFRED
+    return __ockl_wfred_max_i32(v);
+#else
     for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
     return v;
+#endif
 }
 __device__ __forceinline__ double wave_max_d(double v) {
     for (int o = 32; o >= 1; o >>= 1) v = fmax(v, __shfl_xor(v, o));
@@ -942,7 +953,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                 // (expect false: the register allocator weighs the span's loops below the candidate loop's)
                 if (__builtin_expect(spans && !failed && L.misc[1] == 0 && ballot(lmin < span_min + 2) == 0ull, 0)) {
                     int mind = lmin;
+#if MK_WFRED
+                    mind = __ockl_wfred_min_i32(mind);
+#else
                     for (int off = 32; off >= 1; off >>= 1) mind = min(mind, __shfl_xor(mind, off));
+#endif
                     const int d0 = depth + 1, d1 = depth + (mind - 2);
                     if (far_rows) __syncthreads(); else wave_sync();   // this depth's open-row stores
                     SpanOct so;
@@ -953,7 +968,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) 
                     // exact predicates then settle
                     for (int g = lane; g < ng; g += 64) {
                         const double2 z = L.gaps[g];
+#if MK_SPAN_RCP
+                        L.gaps2[g] = make_double2(__builtin_amdgcn_rcp(z.x), __builtin_amdgcn_rcp(z.y));
+#else
                         L.gaps2[g] = make_double2(1.0 / z.x, 1.0 / z.y);
+#endif
                     }
                     wave_sync();
                     const int R0 = max(0, gap_cl(L.gaps[0].x, d0)), R1 = min(d1, gap_ch(L.gaps[ng - 1].y, d1));

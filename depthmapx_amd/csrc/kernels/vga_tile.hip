@@ -213,8 +213,9 @@ struct FView {
 #define VGA_PHASEC_ROWSONLY 0
 #endif
 #ifndef VGA_HINTS
-#define VGA_HINTS 3          // hint slots a cell (narrow grids with the masks): the hint + VGA_HINTS - 1 fully seen
-                             // tiles in hint2 (1000^2 VGA: 1 -> 3.858 s, 2 -> 3.684, 3 -> 3.568)
+#define VGA_HINTS 4          // hint slots a cell (narrow grids with the masks): the hint + VGA_HINTS - 1 fully seen
+                             // tiles in hint2 (1000^2 VGA: 1 -> 3.858 s, 2 -> 3.684, 3 -> 3.568; on a later box
+                             // 3 -> 3.688, 4 -> 3.513, 5 -> 3.553: profiles/r6_vga_hints_ab.jsonl)
 #endif
 #define VGA_H2 (VGA_HINTS - 1)   // slots of hint2: [VGA_H2][nt*64]
 static_assert(VGA_HINTS >= 2, "hint2 holds at least one slot");
