@@ -21,3 +21,12 @@ def ctx():
     c = dmx.Context(0)
     yield c
     c.close()
+
+
+def pytest_runtest_logreport(report):
+    """DMX_TEST_DURATIONS=<file>: append each test phase's duration as it ends (a run cut off by a time limit
+    still leaves the record of what took the time)."""
+    path = os.environ.get("DMX_TEST_DURATIONS")
+    if path and report.when in ("setup", "call"):
+        with open(path, "a") as f:
+            f.write("%.2f %s %s %s\n" % (report.duration, report.when, report.outcome, report.nodeid))

@@ -57,7 +57,7 @@ def test_vga_on_reread_graph_asymmetric_mode_equals_oracle(ctx, monkeypatch, nam
         st = ctx.last_stats()
         assert st["vga_kernel"] == "tile-resolved" and st["vga_asym_mode"] == 1, st
         assert st["vga_asym_nodes"] > 0, st
-        ref, rlv = om.vga_global(radius=radius, threads=8, levels=True)
+        ref, rlv = om.vga_global(radius=radius, threads=16, levels=True)
         np.testing.assert_array_equal(lv[:, :2], rlv[:, :2])
         np.testing.assert_array_equal(got[:, 5], ref[:, 5])
         assert np.allclose(got, ref, rtol=1e-6, atol=1e-6)
