@@ -45,7 +45,8 @@ namespace dmx {
 #endif
 constexpr int MK_GCAP0 = 16, MK_BCAP0 = 32;   // first-pass LDS gap / block capacities (FIXED kernels)
 // shortest occluder-free span taken, in depths (DMX_MK_SPAN overrides): configs[2] / configs[4] makeGraph with
-// 1: 3.23 / 9.61 s, 2: 3.17 / 9.02, 4: 3.11 / 8.61, 8: 3.11 / 8.75 (profiles/r6_span_ab.jsonl)
+// 1: 3.23 / 9.61 s, 2: 3.17 / 9.02, 4: 3.11 / 8.61, 8: 3.11 / 8.75 (profiles/r6_span_ab.jsonl); with the gap skip
+// 3: 2.884 / 8.261, 4: 2.886 / 8.244, 5: 2.881 / 8.255, 6: 2.889 / 8.306 (r6_span_ab2.jsonl, tags s3..s6)
 constexpr int MK_SPAN_MIN = 4;
 // open-run state of rows 0 .. MK_OPEN_LDS-1 lives in LDS, of farther rows (grids above ~1020 cells a
 // side) in per-wave scratch memory: rows past 1024 are reached only by sight lines longer than 1024
